@@ -1,0 +1,236 @@
+"""The reconcile core: tally -> observe -> decide -> actuate (C5-C14).
+
+Reference: ``autoscaler/autoscaler.py``.  The public method names and
+argument orders match the reference so code written against it keeps
+working; the Kubernetes client layer (C7-C9) is replaced by an *actuator*
+with the same four calls -- by default the node-local GPU manager
+(:mod:`kiosk_autoscaler_amd.gpumgr`), which launches / reaps PyTorch-ROCm
+worker processes pinned to MI355X GPUs instead of patching a Deployment.
+
+Behaviour kept:
+
+* C6 tally: ``LLEN q`` + number of keys matching ``processing-q:*`` (SCAN,
+  COUNT 1000), logged at INFO as ``In-progress or new redis keys``.
+* C10 observe: unknown type -> ``ValueError``; missing resource -> 0;
+  ``None`` -> 0; value ``int()``-cast; ``only_running`` reads READY workers.
+* C11-C14 decide: :mod:`kiosk_autoscaler_amd.policy` (``reference`` default).
+* C13 actuate: no call when ``desired == current`` (returns ``None``);
+  otherwise patch and return ``True``.
+* C14: only the actuator error raised by ``scale_resource`` is swallowed
+  (WARNING); errors from tally/observe propagate (crash-only main loop).
+"""
+import logging
+import timeit
+
+from . import policy as policies
+from .gpumgr.resources import ActuatorError
+from .utils.events import NULL as NULL_EVENTS
+
+
+class Autoscaler(object):
+    """Read Redis and scale GPU worker processes when required.
+
+    Args:
+        redis_client: Redis client (``RedisClient`` proxy, ``Redis`` or fake).
+        queues: delimiter-joined queue names.
+        queue_delim: delimiter for ``queues``.
+        actuator: object with ``list_namespaced_{deployment,job}`` and
+            ``patch_namespaced_{deployment,job}``; defaults to a lazily
+            created embedded GPU manager (:meth:`get_actuator`).
+        policy: ``'reference'`` (bit-compatible) or ``'strict'``.
+        scale_down_delay: seconds a lower target must persist before a
+            scale-down is applied (``strict`` hysteresis; 0 = immediate).
+        events: optional :class:`~kiosk_autoscaler_amd.utils.EventLog`.
+    """
+
+    def __init__(self, redis_client, queues='predict', queue_delim=',',
+                 actuator=None, policy='reference', scale_down_delay=0.0,
+                 events=None, clock=timeit.default_timer):
+        self.redis_keys = {q: 0 for q in queues.split(queue_delim)}
+        self.in_progress = {q: 0 for q in self.redis_keys}
+        self.redis_client = redis_client
+        self.logger = logging.getLogger(str(self.__class__.__name__))
+        self.managed_resource_types = {'deployment', 'job'}
+        self.actuator = actuator
+        if policy not in policies.POLICIES:
+            raise ValueError('unknown policy %r' % policy)
+        self.policy = policy
+        self.scale_down_delay = float(scale_down_delay)
+        self.events = events if events is not None else NULL_EVENTS
+        self._clock = clock
+        self._lower_since = None
+        self.last_decision = None
+
+    # -- C6 ------------------------------------------------------------------
+    def tally_queues(self):
+        """Update ``redis_keys[q] = LLEN q + #keys('processing-q:*')``."""
+        start = self._clock()
+        for queue in self.redis_keys:
+            self.logger.debug('Tallying items in queue `%s`.', queue)
+            waiting = self.redis_client.llen(queue)
+            pattern = 'processing-{}:*'.format(queue)
+            running = sum(1 for _ in self.redis_client.scan_iter(
+                match=pattern, count=1000))
+            self.in_progress[queue] = running
+            self.redis_keys[queue] = waiting + running
+        self.logger.debug('Finished tallying redis keys in %s seconds.',
+                          self._clock() - start)
+        self.logger.info('In-progress or new redis keys: %s', self.redis_keys)
+        return dict(self.redis_keys)
+
+    # -- C7-C9: actuator access ------------------------------------------------
+    def get_actuator(self):
+        """The ``get_apps_v1_client``/``get_batch_v1_client`` analog."""
+        if self.actuator is None:
+            from .gpumgr import connect
+            self.actuator = connect()
+        return self.actuator
+
+    def _timed(self, what, func, *args):
+        started = self._clock()
+        try:
+            result = func(*args)
+        except ActuatorError as err:
+            self.logger.error('%s when calling `%s`: %s',
+                              type(err).__name__, what, err)
+            raise
+        self.logger.debug('%s finished in %s seconds.', what,
+                          self._clock() - started)
+        return result
+
+    def list_namespaced_deployment(self, namespace):
+        items = self._timed('list_namespaced_deployment',
+                            self.get_actuator().list_namespaced_deployment,
+                            namespace).items
+        self.logger.debug('Found %s deployments in namespace `%s`: %s',
+                          len(items), namespace,
+                          [d.metadata.name for d in items])
+        return items
+
+    def list_namespaced_job(self, namespace):
+        items = self._timed('list_namespaced_job',
+                            self.get_actuator().list_namespaced_job,
+                            namespace).items
+        self.logger.debug('Found %s jobs in namespace `%s`.', len(items),
+                          namespace)
+        return items
+
+    def patch_namespaced_deployment(self, name, namespace, body):
+        return self._timed('patch_namespaced_deployment',
+                           self.get_actuator().patch_namespaced_deployment,
+                           name, namespace, body)
+
+    def patch_namespaced_job(self, name, namespace, body):
+        return self._timed('patch_namespaced_job',
+                           self.get_actuator().patch_namespaced_job,
+                           name, namespace, body)
+
+    # -- C10 -----------------------------------------------------------------
+    def _check_type(self, resource_type):
+        if resource_type not in self.managed_resource_types:
+            raise ValueError('`resource_type` must be one of {}. Got {}.'.format(
+                self.managed_resource_types, resource_type))
+
+    def get_current_pods(self, namespace, resource_type, name,
+                         only_running=False):
+        """Declared worker count (or READY count with ``only_running``)."""
+        self._check_type(resource_type)
+        if resource_type == 'deployment':
+            items = self.list_namespaced_deployment(namespace)
+        else:
+            items = self.list_namespaced_job(namespace)
+        count = 0
+        for item in items:
+            if item.metadata.name != name:
+                continue
+            if resource_type == 'job':
+                count = item.spec.parallelism
+            elif only_running:
+                count = item.status.available_replicas
+            else:
+                count = item.spec.replicas
+            self.logger.debug('%s %s has %s pods', resource_type, name, count)
+            break
+        return int(count or 0)
+
+    # -- C11 / C12 -------------------------------------------------------------
+    def clip_pod_count(self, desired_pods, min_pods, max_pods, current_pods):
+        clipped = policies.clip_pod_count(desired_pods, min_pods, max_pods,
+                                          current_pods)
+        if clipped != desired_pods:
+            self.logger.debug('Clipped pods from %s to %s', desired_pods,
+                              clipped)
+        return clipped
+
+    def get_desired_pods(self, key, keys_per_pod, min_pods, max_pods,
+                         current_pods):
+        return self.clip_pod_count(self.redis_keys[key] // keys_per_pod,
+                                   min_pods, max_pods, current_pods)
+
+    # -- C13 -----------------------------------------------------------------
+    def scale_resource(self, desired_pods, current_pods, resource_type,
+                       namespace, name):
+        if resource_type not in self.managed_resource_types:
+            raise ValueError('Cannot scale resource type: %s' % resource_type)
+        if desired_pods == current_pods:
+            return None
+        if resource_type == 'job':
+            self.patch_namespaced_job(
+                name, namespace, {'spec': {'parallelism': desired_pods}})
+        else:
+            self.patch_namespaced_deployment(
+                name, namespace, {'spec': {'replicas': desired_pods}})
+        self.logger.info('Successfully scaled %s `%s` in namespace `%s` '
+                         'from %s to %s pods.', resource_type, name,
+                         namespace, current_pods, desired_pods)
+        self.events.emit('scale', kind=resource_type, name=name,
+                         namespace=namespace, current=current_pods,
+                         desired=desired_pods)
+        return True
+
+    # -- C14 -----------------------------------------------------------------
+    def _decide(self, min_pods, max_pods, keys_per_pod, current_pods):
+        if self.policy == 'reference':
+            desired = 0
+            for key in self.redis_keys:
+                desired += self.get_desired_pods(key, keys_per_pod, min_pods,
+                                                 max_pods, current_pods)
+            return self.clip_pod_count(desired, min_pods, max_pods,
+                                       current_pods)
+        desired = policies.decide(
+            self.redis_keys, min_pods, max_pods, keys_per_pod, current_pods,
+            policy=self.policy, busy=sum(self.in_progress.values()))
+        if desired < current_pods and self.scale_down_delay > 0:
+            now = self._clock()
+            if self._lower_since is None:
+                self._lower_since = now
+            if now - self._lower_since < self.scale_down_delay:
+                return current_pods
+        else:
+            self._lower_since = None
+        return desired
+
+    def scale(self, namespace, resource_type, name, min_pods=0, max_pods=1,
+              keys_per_pod=1):
+        """One reconcile tick.  Returns the target replica count."""
+        self.tally_queues()
+        self.logger.debug('Scaling %s `%s.%s`.', resource_type, namespace,
+                          name)
+        current_pods = self.get_current_pods(namespace, resource_type, name)
+        desired_pods = self._decide(min_pods, max_pods, keys_per_pod,
+                                    current_pods)
+        self.logger.debug('%s `%s` in namespace `%s` has a current state of '
+                          '%s pods and a desired state of %s pods.',
+                          str(resource_type).capitalize(), name, namespace,
+                          current_pods, desired_pods)
+        self.events.emit('tick', keys=dict(self.redis_keys),
+                         current=current_pods, desired=desired_pods)
+        self.last_decision = desired_pods
+        try:
+            self.scale_resource(desired_pods, current_pods, resource_type,
+                                namespace, name)
+        except ActuatorError as err:
+            self.logger.warning('Failed to scale %s `%s.%s` due to %s: %s',
+                                resource_type, namespace, name,
+                                type(err).__name__, err)
+        return desired_pods

@@ -1,0 +1,117 @@
+"""Process entry point: env config -> logging -> clients -> reconcile loop.
+
+Behaviour of the reference's ``scale.py`` (C16-C18, ``scale.py:69-106``):
+
+* logging as :func:`~kiosk_autoscaler_amd.utils.logs.initialize_logger`;
+* a sentinel-aware :class:`RedisClient` built from ``REDIS_HOST/PORT`` with
+  ``REDIS_INTERVAL`` backoff -- a connection error here crashes startup;
+* ``RESOURCE_NAME`` is required (missing -> ``UndefinedValueError``);
+* ``while True: scale(); gc.collect(); sleep(INTERVAL)`` -- the period is
+  tick time + ``INTERVAL`` (``FIXED_RATE=1`` makes it exactly ``INTERVAL``);
+* any exception -> CRITICAL ``Fatal Error: <type>: <msg>`` and exit 1.
+
+The actuator is the node-local GPU manager: embedded in this process by
+default (its workers are drained when the process exits) or a separate
+daemon (``GPUMGR=unix:PATH``; workers then survive autoscaler restarts).
+"""
+import gc
+import logging
+import signal
+import sys
+import time
+
+from . import gpumgr
+from .autoscaler import Autoscaler
+from .config import Settings
+from .redisq import RedisClient
+from .utils.events import EventLog
+from .utils.logs import initialize_logger
+
+
+class _Terminate(Exception):
+    pass
+
+
+def _on_sigterm(signum, frame):
+    raise _Terminate('signal %d' % signum)
+
+
+def build(settings=None, redis_client=None, actuator=None, events=None):
+    """Construct (client, scaler, manager) exactly as ``main`` would."""
+    settings = settings or Settings()
+    if redis_client is None:
+        redis_client = RedisClient(host=settings.REDIS_HOST,
+                                   port=settings.REDIS_PORT,
+                                   backoff=settings.REDIS_INTERVAL)
+    if events is None:
+        events = EventLog(path=settings.EVENT_LOG or None,
+                          source='autoscaler')
+    manager = None
+    if actuator is None:
+        if settings.GPUMGR.startswith('unix:'):
+            # the daemon registers the resource from its own environment
+            actuator = gpumgr.connect(settings.GPUMGR)
+        else:
+            manager = gpumgr.build_manager(settings, redis_client=redis_client,
+                                           events=events)
+            manager.start()
+            gpumgr.set_embedded(manager)
+            actuator = manager
+    scaler = Autoscaler(redis_client=redis_client, queues=settings.QUEUES,
+                        queue_delim=settings.QUEUE_DELIMITER,
+                        actuator=actuator, policy=settings.SCALE_POLICY,
+                        scale_down_delay=settings.SCALE_DOWN_DELAY,
+                        events=events)
+    return redis_client, scaler, manager
+
+
+def run_loop(scaler, settings, max_ticks=None, sleep=time.sleep,
+             clock=time.monotonic):
+    """The reconcile loop; returns after ``max_ticks`` (tests) or never."""
+    ticks = 0
+    next_tick = clock()
+    while max_ticks is None or ticks < max_ticks:
+        scaler.scale(namespace=settings.RESOURCE_NAMESPACE,
+                     resource_type=settings.RESOURCE_TYPE,
+                     name=settings.RESOURCE_NAME,
+                     min_pods=settings.MIN_PODS,
+                     max_pods=settings.MAX_PODS,
+                     keys_per_pod=settings.KEYS_PER_POD)
+        gc.collect()
+        ticks += 1
+        if max_ticks is not None and ticks >= max_ticks:
+            break
+        if settings.FIXED_RATE:
+            next_tick += settings.INTERVAL
+            sleep(max(0.0, next_tick - clock()))
+        else:
+            sleep(settings.INTERVAL)
+    return ticks
+
+
+def main(argv=None):
+    del argv
+    settings = Settings()   # missing RESOURCE_NAME raises here (fatal)
+    initialize_logger(debug_mode=settings.DEBUG, log_file=settings.LOG_FILE)
+    _logger = logging.getLogger(__file__)
+    signal.signal(signal.SIGTERM, _on_sigterm)
+    manager = None
+    try:
+        _, scaler, manager = build(settings)
+        run_loop(scaler, settings)
+    except (KeyboardInterrupt, _Terminate) as err:
+        _logger.info('Shutting down (%s).', err or 'interrupt')
+        code = 0
+    except Exception as err:  # pylint: disable=broad-except
+        _logger.critical('Fatal Error: %s: %s', type(err).__name__, err)
+        code = 1
+    else:
+        code = 0
+    finally:
+        if manager is not None:
+            manager.stop()
+    sys.exit(code)
+
+
+if __name__ == '__main__':
+    main()

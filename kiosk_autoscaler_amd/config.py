@@ -1,0 +1,176 @@
+"""Typed environment configuration (component C17).
+
+The reference reads 12 variables through python-decouple
+(``scale.py:74-92``).  decouple is not available, so this module provides a
+small equivalent: environment first, then an optional ``.env`` /
+``settings.ini`` found from the working directory upward (decouple's
+``AutoConfig`` search), then the default.  A variable with no default that
+is missing raises :class:`UndefinedValueError` -- ``RESOURCE_NAME`` keeps the
+reference's fatal-at-startup behaviour (``scale.py:88``).
+
+MI355X additions (all optional, with defaults) are listed in
+:data:`EXTRA_DEFAULTS`.
+"""
+import configparser
+import os
+
+_MISSING = object()
+
+TRUE_STRINGS = frozenset(['1', 'true', 'yes', 'y', 'on', 't'])
+FALSE_STRINGS = frozenset(['0', 'false', 'no', 'n', 'off', 'f', ''])
+
+
+class UndefinedValueError(Exception):
+    """A required configuration value is not set anywhere."""
+
+
+def cast_bool(value):
+    if isinstance(value, bool):
+        return value
+    text = str(value).strip().lower()
+    if text in TRUE_STRINGS:
+        return True
+    if text in FALSE_STRINGS:
+        return False
+    raise ValueError('Invalid truth value: %r' % value)
+
+
+def _find_upwards(start, names):
+    path = os.path.abspath(start)
+    while True:
+        for name in names:
+            candidate = os.path.join(path, name)
+            if os.path.isfile(candidate):
+                return candidate
+        parent = os.path.dirname(path)
+        if parent == path:
+            return None
+        path = parent
+
+
+def _read_env_file(path):
+    values = {}
+    with open(path) as handle:
+        for line in handle:
+            line = line.strip()
+            if not line or line.startswith('#') or '=' not in line:
+                continue
+            key, value = line.split('=', 1)
+            key = key.strip()
+            if key.startswith('export '):
+                key = key[len('export '):].strip()
+            value = value.strip()
+            if len(value) >= 2 and value[0] == value[-1] and value[0] in '"\'':
+                value = value[1:-1]
+            values[key] = value
+    return values
+
+
+def _read_ini_file(path):
+    parser = configparser.ConfigParser()
+    parser.optionxform = str
+    parser.read(path)
+    if parser.has_section('settings'):
+        return dict(parser.items('settings'))
+    return {}
+
+
+class Config(object):
+    """Lookup chain: ``environ`` -> repository file -> default."""
+
+    def __init__(self, environ=None, search_path=None, use_files=True):
+        self.environ = os.environ if environ is None else environ
+        self.file_values = {}
+        self.source = None
+        if use_files:
+            explicit = self.environ.get('ENV_FILE')
+            path = explicit or _find_upwards(search_path or os.getcwd(),
+                                             ('settings.ini', '.env'))
+            if path and os.path.isfile(path):
+                self.source = path
+                if path.endswith('.ini'):
+                    self.file_values = _read_ini_file(path)
+                else:
+                    self.file_values = _read_env_file(path)
+
+    def __call__(self, option, default=_MISSING, cast=None):
+        if option in self.environ:
+            value = self.environ[option]
+        elif option in self.file_values:
+            value = self.file_values[option]
+        elif default is not _MISSING:
+            value = default
+        else:
+            raise UndefinedValueError(
+                '%s not found. Declare it as envvar or define a default '
+                'value.' % option)
+        if cast is None or value is None:
+            return value
+        if cast is bool:
+            return cast_bool(value)
+        return cast(value)
+
+
+#: The reference's configuration surface, same names/types/defaults
+#: (``scale.py:74-92``, README table).  ``None`` default = required.
+REFERENCE_DEFAULTS = (
+    ('REDIS_HOST', str, 'redis-master'),
+    ('REDIS_PORT', int, 6379),
+    ('REDIS_INTERVAL', int, 1),
+    ('QUEUES', str, 'predict,track'),
+    ('QUEUE_DELIMITER', str, ','),
+    ('INTERVAL', int, 5),
+    ('RESOURCE_NAMESPACE', str, 'default'),
+    ('RESOURCE_TYPE', str, 'deployment'),
+    ('RESOURCE_NAME', str, _MISSING),
+    ('MIN_PODS', int, 0),
+    ('MAX_PODS', int, 1),
+    ('KEYS_PER_POD', int, 1),
+)
+
+#: MI355X-native additions (SURVEY §5.6 "New knobs").
+EXTRA_DEFAULTS = (
+    ('SCALE_POLICY', str, 'reference'),     # reference | strict
+    ('SCALE_DOWN_DELAY', float, 0.0),       # strict: idle grace seconds
+    ('FIXED_RATE', bool, False),            # tick every INTERVAL (not tick+INTERVAL)
+    ('GPU_IDS', str, ''),                   # '' = all visible GPUs
+    ('GPUMGR', str, 'embedded'),            # embedded | unix:<path>
+    ('WORKER_MODULE', str, 'kiosk_autoscaler_amd.worker.main'),
+    ('WORKER_BACKEND', str, 'auto'),        # auto | hip | cpu
+    ('WARM_POOL', int, -1),                 # standby processes (-1 = MAX_PODS)
+    ('WARM_START', bool, True),             # run the N1 warm-start kernel
+    ('FENCE', str, 'auto'),                 # auto | rccl | store | none
+    ('MODEL_DIM', int, 4096),
+    ('MODEL_HIDDEN', int, 16384),
+    ('MODEL_LAYERS', int, 4),
+    ('ROWS_PER_KEY', int, 2048),
+    ('HBM_PER_KEY_BYTES', int, 0),          # 0 = derive from the model
+    ('HBM_RESERVE_BYTES', int, 8 << 30),
+    ('EVENT_LOG', str, ''),                 # JSONL event path ('' = off)
+    ('STATE_TTL', int, 3600),
+    ('DEBUG', bool, True),
+    ('LOG_FILE', str, 'autoscaler.log'),
+)
+
+
+class Settings(object):
+    """All settings resolved once (attribute access, e.g. ``s.MAX_PODS``)."""
+
+    def __init__(self, config=None, require_resource_name=True):
+        config = config if config is not None else Config()
+        self.source = config.source
+        for name, cast, default in REFERENCE_DEFAULTS + EXTRA_DEFAULTS:
+            if default is _MISSING and not require_resource_name:
+                default = ''
+            setattr(self, name, config(name, default=default, cast=cast))
+
+    @property
+    def queues(self):
+        return self.QUEUES.split(self.QUEUE_DELIMITER)
+
+    def as_dict(self):
+        return {name: getattr(self, name)
+                for name, _, _ in REFERENCE_DEFAULTS + EXTRA_DEFAULTS}
+
+
+config = Config  # decouple-style alias: ``config()('NAME', default=..)``

@@ -1,0 +1,103 @@
+"""Node-local GPU/process manager (replaces the reference's k8s layer).
+
+``connect()`` is the ``kubernetes.config.load_incluster_config()`` +
+``AppsV1Api()`` analog (reference ``autoscaler/autoscaler.py:79-87``): it
+returns the actuator the Autoscaler talks to -- the process-wide embedded
+manager, or a client for an out-of-process daemon (``GPUMGR=unix:PATH``).
+"""
+import os
+
+from .controller import GpuManager, WorkerTemplate
+from .daemon import GpuManagerClient, ManagerServer
+from .gpus import GpuSlot, discover
+from .resources import ActuatorError, ResourceList, ResourceView
+
+_EMBEDDED = None
+
+
+def set_embedded(manager):
+    global _EMBEDDED
+    _EMBEDDED = manager
+
+
+def connect(address=None):
+    address = address or os.environ.get('GPUMGR', 'embedded')
+    if address.startswith('unix:'):
+        return GpuManagerClient(address[len('unix:'):])
+    if _EMBEDDED is None:
+        raise ActuatorError(503, 'no embedded GPU manager is running')
+    return _EMBEDDED
+
+
+def resolve_backend(requested, slots):
+    if requested in ('hip', 'cpu'):
+        return requested
+    return 'hip' if any(s.kind == 'gpu' for s in slots) else 'cpu'
+
+
+def worker_env(settings, keys_per_pod=None):
+    """Environment every worker of this autoscaler inherits."""
+    env = {
+        'REDIS_HOST': settings.REDIS_HOST, 'REDIS_PORT': settings.REDIS_PORT,
+        'REDIS_INTERVAL': settings.REDIS_INTERVAL,
+        'QUEUES': settings.QUEUES, 'QUEUE_DELIMITER': settings.QUEUE_DELIMITER,
+        'KEYS_PER_POD': keys_per_pod or settings.KEYS_PER_POD,
+        'MODEL_DIM': settings.MODEL_DIM, 'MODEL_HIDDEN': settings.MODEL_HIDDEN,
+        'MODEL_LAYERS': settings.MODEL_LAYERS,
+        'ROWS_PER_KEY': settings.ROWS_PER_KEY,
+        'WARM_START': int(settings.WARM_START), 'FENCE': settings.FENCE,
+        'RESOURCE_NAMESPACE': settings.RESOURCE_NAMESPACE,
+        'RESOURCE_NAME': settings.RESOURCE_NAME,
+    }
+    if settings.EVENT_LOG:
+        env['EVENT_LOG'] = settings.EVENT_LOG
+    for passthrough in ('PASSES_PER_KEY', 'MOCK_WORK_MS', 'WORKER_BATCH',
+                        'JOB_IDLE_EXIT_S', 'POLL_BLOCK_S', 'MODEL_SEED',
+                        'KIOSK_RCCL_LIB', 'WORKER_EVENTS'):
+        if passthrough in os.environ:
+            env[passthrough] = os.environ[passthrough]
+    return env
+
+
+def build_manager(settings, redis_client=None, events=None, slots=None,
+                  extra_env=None):
+    """Build (not start) the manager + register the configured resource."""
+    from ..utils import hbm
+    if slots is None:
+        cpu_slots = max(1, settings.MAX_PODS)
+        slots = discover(settings.GPU_IDS, cpu_slots=cpu_slots)
+    backend = resolve_backend(settings.WORKER_BACKEND, slots)
+    if backend == 'cpu':
+        slots = [s if s.kind == 'cpu' else GpuSlot(s.index, '', kind='cpu')
+                 for s in slots] or [GpuSlot(i, '', kind='cpu')
+                                     for i in range(max(1, settings.MAX_PODS))]
+    kpp = settings.KEYS_PER_POD
+    if backend == 'hip':
+        kpp = hbm.size_keys_per_pod(
+            kpp, settings.MODEL_DIM, settings.MODEL_HIDDEN,
+            settings.MODEL_LAYERS, settings.ROWS_PER_KEY,
+            reserve=settings.HBM_RESERVE_BYTES,
+            per_key=settings.HBM_PER_KEY_BYTES)
+    env = worker_env(settings, kpp)
+    env.update(extra_env or {})
+    template = WorkerTemplate(queues=settings.queues,
+                              module=settings.WORKER_MODULE,
+                              env=env, backend=backend,
+                              keys_per_pod=kpp)
+    pool = settings.WARM_POOL
+    if pool < 0:
+        pool = min(max(settings.MAX_PODS, 0), len(slots))
+    fence = settings.FENCE not in ('none', 'off')
+    manager = GpuManager(slots, redis_client=redis_client, pool_size=pool,
+                         pool_template=template, events=events, fence=fence)
+    if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
+                                                           'job'):
+        manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,
+                         settings.RESOURCE_NAME, template)
+    return manager
+
+
+__all__ = ['GpuManager', 'WorkerTemplate', 'GpuManagerClient',
+           'ManagerServer', 'GpuSlot', 'discover', 'ActuatorError',
+           'ResourceList', 'ResourceView', 'connect', 'set_embedded',
+           'build_manager', 'resolve_backend']

@@ -1,0 +1,719 @@
+"""Node-local GPU/process manager -- the Kubernetes replacement.
+
+The reference's actuator is the Kubernetes API: it reads ``spec.replicas``
+and PATCHes it, and k8s controllers create pods later
+(``autoscaler/autoscaler.py:79-195, 221-242``).  On one 8-GPU MI355X node
+this module plays API server + controller + kubelet:
+
+* **Resources** (``deployment`` / ``job``) carry a declared count; a PATCH
+  sets it and wakes the reconcile loop (no pod-scheduling round trip).
+* **Workers** are OS processes, one per GPU, pinned with
+  ``HIP_VISIBLE_DEVICES`` and CPU affinity to the GPU's NUMA-local cores.
+  The lowest free GPU index is allocated first.
+* **Warm pool**: ``pool_size`` standby processes have already imported
+  PyTorch-ROCm and the native kernel module but have *not* initialised HIP
+  (so they hold no GPU).  A scale-up hands a standby its GPU over a pipe,
+  taking the ~1.6 s interpreter/torch import off the critical path
+  (SURVEY §7.4 item 4).  Standbys do not count as replicas.
+* **READY** (``status.available_replicas``) means the worker has its
+  weights in HBM and has run the warm-start kernel.
+* **Scale-down** drains: the worker finishes its in-flight key and exits.
+  Busy workers are never chosen while an idle or not-ready one exists.
+* **Failure**: a dead worker's ``processing-<q>:<id>*`` items are pushed
+  back to their queue and a replacement is started (with backoff).
+* **Jobs** are one-shot: workers exit 0 when the queue is empty; each
+  success decrements ``spec.parallelism`` (TTL-after-finished semantics), so
+  the reference's stranded-keys case (a completed Job that is never
+  restarted) cannot occur.
+* **Membership fence**: whenever the READY set changes the manager starts a
+  fence epoch (coalesced: one in flight at a time); workers agree on the set
+  with an RCCL all-reduce over xGMI and rank 0 acknowledges.  The fenced
+  set is published to Redis (``kiosk:active:<ns>:<name>``).
+"""
+import collections
+import itertools
+import json
+import logging
+import os
+import select
+import subprocess
+import sys
+import threading
+import time
+
+from ..utils.events import NULL as NULL_EVENTS
+from .resources import ActuatorError, ResourceList, ResourceView, \
+    desired_from_body
+
+logger = logging.getLogger('GpuManager')
+
+STARTING, READY, DRAINING, EXITED = 'starting', 'ready', 'draining', 'exited'
+ACTIVE_KEY = 'kiosk:active:{ns}:{name}'
+WORKER_KEY = 'kiosk:worker:{id}'
+
+
+class WorkerTemplate(object):
+    """What to run for a resource (the pod template analog)."""
+
+    def __init__(self, queues=('predict',), module=None, env=None,
+                 python=None, backend='auto', keys_per_pod=1):
+        self.queues = list(queues)
+        self.module = module or 'kiosk_autoscaler_amd.worker.main'
+        self.env = dict(env or {})
+        self.python = python or sys.executable
+        self.backend = backend
+        self.keys_per_pod = int(keys_per_pod)
+
+    def to_dict(self):
+        return {'queues': self.queues, 'module': self.module,
+                'env': self.env, 'backend': self.backend,
+                'keys_per_pod': self.keys_per_pod}
+
+
+class _Pipe(object):
+    """Line-oriented JSON channel over a pair of pipe fds."""
+
+    def __init__(self, cmd_w, ev_r):
+        self.cmd_w = cmd_w
+        self.ev_r = ev_r
+        self._buf = b''
+        os.set_blocking(ev_r, False)
+
+    def send(self, message):
+        data = (json.dumps(message) + '\n').encode()
+        try:
+            os.write(self.cmd_w, data)
+            return True
+        except OSError:
+            return False
+
+    def read_messages(self):
+        out = []
+        while True:
+            try:
+                chunk = os.read(self.ev_r, 65536)
+            except BlockingIOError:
+                break
+            except OSError:
+                chunk = b''
+            if not chunk:
+                out.append(None)  # EOF
+                break
+            self._buf += chunk
+        while b'\n' in self._buf:
+            line, self._buf = self._buf.split(b'\n', 1)
+            if line.strip():
+                try:
+                    out.append(json.loads(line))
+                except ValueError:
+                    logger.warning('bad worker message %r', line[:200])
+        return out
+
+    def close(self):
+        for fd in (self.cmd_w, self.ev_r):
+            try:
+                os.close(fd)
+            except OSError:
+                pass
+
+
+class _Process(object):
+    """A child process (standby or worker) and its control pipe."""
+
+    _ids = itertools.count()
+
+    def __init__(self, popen, pipe, role):
+        self.popen = popen
+        self.pipe = pipe
+        self.role = role
+        self.seq = next(self._ids)
+        self.t_spawn = time.monotonic_ns()
+        self.booted = False
+        self.eof = False
+
+    @property
+    def pid(self):
+        return self.popen.pid
+
+
+class Worker(object):
+    __slots__ = ('id', 'resource', 'slot', 'proc', 'state', 'busy',
+                 't_assigned', 't_ready', 't_exit', 'exit_code', 'from_pool',
+                 'stages')
+
+    def __init__(self, wid, resource, slot, proc, from_pool):
+        self.id = wid
+        self.resource = resource
+        self.slot = slot
+        self.proc = proc
+        self.state = STARTING
+        self.busy = False
+        self.t_assigned = time.monotonic_ns()
+        self.t_ready = None
+        self.t_exit = None
+        self.exit_code = None
+        self.from_pool = from_pool
+        self.stages = {}
+
+    def summary(self):
+        return {'id': self.id, 'gpu': self.slot.index, 'pid': self.proc.pid,
+                'state': self.state, 'busy': self.busy,
+                'from_pool': self.from_pool, 't_assigned': self.t_assigned,
+                't_ready': self.t_ready, 'stages': dict(self.stages)}
+
+
+class Resource(object):
+    def __init__(self, kind, namespace, name, template):
+        self.kind = kind
+        self.namespace = namespace
+        self.name = name
+        self.template = template
+        self.declared = 0
+        self.generation = 0
+        self.workers = collections.OrderedDict()
+        self.succeeded = 0
+        self.failed = 0
+        self.restart_backoff_until = 0.0
+        self.consecutive_failures = 0
+        # fence bookkeeping
+        self.epoch = 0
+        self.fenced_epoch = 0
+        self.fenced_members = []
+        self.fence_inflight = None   # (epoch, members, t_start)
+        self.fence_wanted = False
+        self.fence_fresh = False     # force re-init after a failed epoch
+
+    @property
+    def key(self):
+        return (self.kind, self.namespace, self.name)
+
+    def live(self):
+        return [w for w in self.workers.values() if w.state in (STARTING,
+                                                                READY)]
+
+    def ready(self):
+        return [w for w in self.workers.values() if w.state == READY]
+
+    def view(self):
+        live = self.live()
+        return ResourceView.build(
+            self.kind, self.namespace, self.name, self.declared,
+            ready=len([w for w in live if w.state == READY]),
+            active=len(live), succeeded=self.succeeded, failed=self.failed,
+            generation=self.generation, epoch=self.fenced_epoch,
+            gpus=[w.slot.index for w in live])
+
+
+class GpuManager(object):
+    """In-process manager.  Thread-safe; ``start()`` runs its event loop.
+
+    Args:
+        slots: :class:`~.gpus.GpuSlot` list this manager may use.
+        redis_client: used to requeue a dead worker's items and to publish
+            worker/active-set state (optional for pure unit tests).
+        pool_size: warm standby processes to keep (0 disables the pool).
+        pool_template: template used to boot standbys (backend/module/env).
+        events: :class:`~kiosk_autoscaler_amd.utils.EventLog`.
+        fence: run membership fences on READY-set changes.
+        fence_timeout: seconds before an unacknowledged fence is abandoned.
+    """
+
+    def __init__(self, slots, redis_client=None, pool_size=0,
+                 pool_template=None, events=None, fence=True,
+                 fence_timeout=60.0, max_restart_backoff=10.0):
+        self.slots = list(slots)
+        self.redis = redis_client
+        self.pool_size = max(0, int(pool_size))
+        self.pool_template = pool_template
+        self.events = events if events is not None else NULL_EVENTS
+        self.fence_enabled = fence
+        self.fence_timeout = fence_timeout
+        self.max_restart_backoff = max_restart_backoff
+        self.resources = collections.OrderedDict()
+        self.standbys = []
+        self.lock = threading.RLock()
+        self._thread = None
+        self._stop = threading.Event()
+        self._wake_r, self._wake_w = os.pipe()
+        os.set_blocking(self._wake_r, False)
+        self._worker_seq = itertools.count()
+        self._stopping = False
+        self.history = []   # exited workers, for accounting
+
+    # ------------------------------------------------------------------
+    # API (the kubernetes AppsV1Api / BatchV1Api analogs)
+    # ------------------------------------------------------------------
+    def register(self, kind, namespace, name, template):
+        if kind not in ('deployment', 'job'):
+            raise ValueError('kind must be deployment or job, got %r' % kind)
+        with self.lock:
+            key = (kind, namespace, name)
+            if key not in self.resources:
+                self.resources[key] = Resource(kind, namespace, name, template)
+            else:
+                self.resources[key].template = template
+            return self.resources[key].view()
+
+    def _list(self, kind, namespace):
+        with self.lock:
+            return ResourceList(items=[
+                r.view() for r in self.resources.values()
+                if r.kind == kind and r.namespace == namespace])
+
+    def list_namespaced_deployment(self, namespace):
+        return self._list('deployment', namespace)
+
+    def list_namespaced_job(self, namespace):
+        return self._list('job', namespace)
+
+    def _patch(self, kind, name, namespace, body):
+        declared = desired_from_body(kind, body)
+        with self.lock:
+            resource = self.resources.get((kind, namespace, name))
+            if resource is None:
+                raise ActuatorError(404, '%s "%s" not found in namespace "%s"'
+                                    % (kind, name, namespace))
+            if declared > len(self.slots):
+                logger.warning('%s %s asks for %d workers but only %d GPU '
+                               'slots exist; the rest stay pending', kind,
+                               name, declared, len(self.slots))
+            resource.declared = declared
+            resource.generation += 1
+            self.events.emit('patch', kind=kind, name=name, declared=declared)
+            self._reconcile(resource)
+            view = resource.view()
+        self._wake()
+        return view
+
+    def patch_namespaced_deployment(self, name, namespace, body):
+        return self._patch('deployment', name, namespace, body)
+
+    def patch_namespaced_job(self, name, namespace, body):
+        return self._patch('job', name, namespace, body)
+
+    def status(self):
+        with self.lock:
+            return {
+                'slots': [s.to_dict() for s in self.slots],
+                'standbys': [{'pid': p.pid, 'booted': p.booted}
+                             for p in self.standbys],
+                'resources': [dict(r.view().to_dict(), workers=[
+                    w.summary() for w in r.workers.values()])
+                    for r in self.resources.values()],
+            }
+
+    # ------------------------------------------------------------------
+    # lifecycle
+    # ------------------------------------------------------------------
+    def start(self):
+        if self._thread is None:
+            with self.lock:
+                self._refill_pool()
+            self._thread = threading.Thread(target=self._loop,
+                                            name='gpumgr', daemon=True)
+            self._thread.start()
+        return self
+
+    def _wake(self):
+        try:
+            os.write(self._wake_w, b'x')
+        except OSError:
+            pass
+
+    def _loop(self):
+        while not self._stop.is_set():
+            self.poll(0.05)
+
+    def stop(self, timeout=10.0):
+        """Drain every worker, stop standbys, join the loop."""
+        with self.lock:
+            self._stopping = True
+            for resource in self.resources.values():
+                resource.declared = 0
+                self._reconcile(resource)
+            for proc in self.standbys:
+                proc.pipe.send({'cmd': 'exit'})
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            with self.lock:
+                alive = [w for r in self.resources.values()
+                         for w in r.workers.values() if w.state != EXITED]
+                alive += [p for p in self.standbys if p.popen.poll() is None]
+            if not alive:
+                break
+            if self._thread is None:
+                self.poll(0.05)
+            else:
+                time.sleep(0.05)
+        with self.lock:
+            for resource in self.resources.values():
+                for worker in resource.workers.values():
+                    if worker.proc.popen.poll() is None:
+                        worker.proc.popen.kill()
+            for proc in self.standbys:
+                if proc.popen.poll() is None:
+                    proc.popen.kill()
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=5)
+            self._thread = None
+        with self.lock:
+            self._reap_all()
+
+    # ------------------------------------------------------------------
+    # event loop body
+    # ------------------------------------------------------------------
+    def poll(self, timeout=0.05):
+        with self.lock:
+            fds = {self._wake_r: None}
+            for proc in self.standbys:
+                if not proc.eof:
+                    fds[proc.pipe.ev_r] = proc
+            for resource in self.resources.values():
+                for worker in resource.workers.values():
+                    if worker.state != EXITED and not worker.proc.eof:
+                        fds[worker.proc.pipe.ev_r] = worker
+        try:
+            ready, _, _ = select.select(list(fds), [], [], timeout)
+        except (OSError, ValueError):
+            ready = []
+        with self.lock:
+            for fd in ready:
+                owner = fds.get(fd)
+                if owner is None:
+                    try:
+                        os.read(self._wake_r, 4096)
+                    except OSError:
+                        pass
+                elif isinstance(owner, _Process):
+                    self._on_standby_messages(owner)
+                else:
+                    self._on_worker_messages(owner)
+            self._reap_all()
+            for resource in self.resources.values():
+                self._reconcile(resource)
+                self._maybe_fence(resource)
+            self._refill_pool()
+
+    # ------------------------------------------------------------------
+    # process management
+    # ------------------------------------------------------------------
+    def _spawn(self, template, role, assign=None):
+        cmd_r, cmd_w = os.pipe()
+        ev_r, ev_w = os.pipe()
+        argv = [template.python, '-m', template.module,
+                '--cmd-fd', str(cmd_r), '--ev-fd', str(ev_w),
+                '--backend', template.backend]
+        if assign is not None:
+            argv += ['--assign', json.dumps(assign)]
+        env = dict(os.environ)
+        env.update({k: str(v) for k, v in template.env.items()})
+        env['PYTHONUNBUFFERED'] = '1'
+        root = os.path.dirname(os.path.dirname(os.path.dirname(
+            os.path.abspath(__file__))))
+        env['PYTHONPATH'] = os.pathsep.join(
+            [root] + [p for p in env.get('PYTHONPATH', '').split(os.pathsep)
+                      if p])
+        try:
+            popen = subprocess.Popen(argv, env=env, pass_fds=(cmd_r, ev_w),
+                                     close_fds=True, start_new_session=True)
+        finally:
+            os.close(cmd_r)
+            os.close(ev_w)
+        proc = _Process(popen, _Pipe(cmd_w, ev_r), role)
+        self.events.emit('process_spawn', role=role, pid=popen.pid)
+        return proc
+
+    def _refill_pool(self):
+        if not self.pool_size or self.pool_template is None or \
+                self._stopping:
+            return
+        self.standbys = [p for p in self.standbys if p.popen.poll() is None]
+        while len(self.standbys) < self.pool_size:
+            self.standbys.append(self._spawn(self.pool_template, 'standby'))
+
+    def _take_standby(self, template):
+        if self.pool_template is None or \
+                template.module != self.pool_template.module or \
+                template.backend != self.pool_template.backend:
+            return None
+        booted = [p for p in self.standbys if p.booted and
+                  p.popen.poll() is None]
+        if not booted:
+            return None
+        proc = booted[0]
+        self.standbys.remove(proc)
+        return proc
+
+    def _on_standby_messages(self, proc):
+        for message in proc.pipe.read_messages():
+            if message is None:
+                proc.eof = True
+                continue
+            if message.get('ev') == 'standby':
+                proc.booted = True
+                self.events.emit('standby_ready', pid=proc.pid,
+                                 boot_s=(time.monotonic_ns() - proc.t_spawn)
+                                 / 1e9)
+
+    def _free_slots(self):
+        used = set()
+        for resource in self.resources.values():
+            for worker in resource.workers.values():
+                if worker.state != EXITED:
+                    used.add(worker.slot.index)
+        return [s for s in self.slots if s.index not in used]
+
+    def _start_worker(self, resource, slot):
+        wid = '%s-g%d-%d' % (resource.name, slot.index,
+                             next(self._worker_seq))
+        assign = {
+            'cmd': 'assign', 'worker_id': wid, 'gpu': slot.visible_id,
+            'slot': slot.index, 'cpus': slot.cpus, 'kind': resource.kind,
+            'namespace': resource.namespace, 'resource': resource.name,
+            'template': resource.template.to_dict(),
+            't_assign': time.monotonic_ns(),
+        }
+        proc = self._take_standby(resource.template)
+        from_pool = proc is not None
+        if from_pool:
+            if not proc.pipe.send(assign):
+                proc.popen.kill()
+                proc = None
+                from_pool = False
+        if proc is None:
+            proc = self._spawn(resource.template, 'worker', assign=assign)
+        proc.role = 'worker'
+        worker = Worker(wid, resource, slot, proc, from_pool)
+        resource.workers[wid] = worker
+        self.events.emit('worker_assigned', worker=wid, gpu=slot.index,
+                         pid=proc.pid, from_pool=from_pool,
+                         resource=resource.name)
+        logger.info('Started worker %s on GPU %s (pid %d, %s).', wid,
+                    slot.visible_id or slot.index, proc.pid,
+                    'warm pool' if from_pool else 'cold spawn')
+        return worker
+
+    def _drain(self, worker, reason):
+        if worker.state in (DRAINING, EXITED):
+            return
+        worker.state = DRAINING
+        worker.proc.pipe.send({'cmd': 'drain', 'reason': reason})
+        self.events.emit('worker_drain', worker=worker.id, reason=reason)
+        logger.info('Draining worker %s (%s).', worker.id, reason)
+
+    def _reconcile(self, resource):
+        live = resource.live()
+        if len(live) < resource.declared and not self._stopping:
+            if time.monotonic() < resource.restart_backoff_until:
+                return
+            free = self._free_slots()
+            for slot in free[:resource.declared - len(live)]:
+                self._start_worker(resource, slot)
+        elif len(live) > resource.declared:
+            excess = len(live) - resource.declared
+            # victims: not-ready first, then idle; newest first; busy last
+            order = sorted(live, key=lambda w: (
+                w.state == READY, w.busy, -w.t_assigned))
+            for worker in order:
+                if excess == 0:
+                    break
+                if worker.busy and any(not w.busy for w in order
+                                       if w.state != DRAINING):
+                    continue
+                self._drain(worker, 'scale-down')
+                excess -= 1
+
+    def _on_worker_messages(self, worker):
+        for message in worker.proc.pipe.read_messages():
+            if message is None:
+                worker.proc.eof = True
+                continue
+            kind = message.get('ev')
+            if kind == 'stage':
+                worker.stages[message.get('stage')] = message.get('t')
+            elif kind == 'ready':
+                if worker.state == STARTING:
+                    worker.state = READY
+                worker.t_ready = message.get('t', time.monotonic_ns())
+                worker.stages.update(message.get('stages', {}))
+                worker.resource.fence_wanted = True
+                worker.resource.consecutive_failures = 0
+                self._publish_worker(worker)
+                logger.info('Worker %s READY on GPU %s after %.3f s.',
+                            worker.id, worker.slot.index,
+                            (worker.t_ready - worker.t_assigned) / 1e9)
+            elif kind == 'busy':
+                worker.busy = True
+            elif kind == 'idle':
+                worker.busy = False
+            elif kind == 'fenced':
+                self._on_fenced(worker.resource, message)
+            elif kind == 'error':
+                logger.error('Worker %s reported: %s', worker.id,
+                             message.get('message'))
+
+    def _reap_all(self):
+        for resource in self.resources.values():
+            for worker in list(resource.workers.values()):
+                if worker.state == EXITED:
+                    continue
+                code = worker.proc.popen.poll()
+                if code is None:
+                    continue
+                # drain remaining messages (the READY/exit of a short job)
+                self._on_worker_messages(worker)
+                self._on_exit(resource, worker, code)
+        for proc in list(self.standbys):
+            if proc.popen.poll() is not None:
+                proc.pipe.close()
+                self.standbys.remove(proc)
+
+    def _on_exit(self, resource, worker, code):
+        was_ready = worker.state in (READY, DRAINING) and worker.t_ready
+        drained = worker.state == DRAINING
+        worker.state = EXITED
+        worker.exit_code = code
+        worker.t_exit = time.monotonic_ns()
+        worker.proc.pipe.close()
+        del resource.workers[worker.id]
+        self.history.append(worker.summary())
+        self.events.emit('worker_exit', worker=worker.id, code=code,
+                         gpu=worker.slot.index)
+        requeued = self._requeue(resource, worker)
+        if resource.kind == 'job' and code == 0 and not drained:
+            resource.succeeded += 1
+            resource.declared = max(0, resource.declared - 1)
+        elif code != 0 and not drained:
+            resource.failed += 1
+            resource.consecutive_failures += 1
+            delay = min(self.max_restart_backoff,
+                        0.1 * (2 ** min(resource.consecutive_failures, 10)))
+            resource.restart_backoff_until = time.monotonic() + delay
+            logger.warning('Worker %s exited with code %s (requeued %d '
+                           'items); restarting in %.1f s.', worker.id, code,
+                           requeued, delay)
+        if was_ready:
+            resource.fence_wanted = True
+        if self.redis is not None:
+            try:
+                self.redis.delete(WORKER_KEY.format(id=worker.id))
+            except Exception:  # pylint: disable=broad-except
+                pass
+
+    def _requeue(self, resource, worker):
+        """Push a dead worker's in-flight items back to their queues."""
+        if self.redis is None:
+            return 0
+        moved = 0
+        for queue in resource.template.queues:
+            # exact key plus the per-slot keys of a batched pull; never a
+            # bare prefix (worker 1 must not claim worker 12's items)
+            exact = 'processing-%s:%s' % (queue, worker.id)
+            try:
+                keys = list(self.redis.scan_iter(match=exact + '.*',
+                                                 count=1000))
+                if self.redis.exists(exact):
+                    keys.append(exact)
+                for key in keys:
+                    while self.redis.rpoplpush(key, queue) is not None:
+                        moved += 1
+                    self.redis.delete(key)
+            except Exception as err:  # pylint: disable=broad-except
+                logger.error('requeue of %s failed: %s', worker.id, err)
+        if moved:
+            self.events.emit('requeue', worker=worker.id, items=moved)
+        return moved
+
+    def _publish_worker(self, worker):
+        if self.redis is None:
+            return
+        try:
+            self.redis.hset(WORKER_KEY.format(id=worker.id), mapping={
+                'gpu': worker.slot.index, 'pid': worker.proc.pid,
+                'state': worker.state, 'ready_ns': worker.t_ready or 0,
+                'resource': worker.resource.name})
+        except Exception:  # pylint: disable=broad-except
+            pass
+
+    # ------------------------------------------------------------------
+    # membership fence orchestration
+    # ------------------------------------------------------------------
+    def _maybe_fence(self, resource):
+        if not self.fence_enabled:
+            return
+        inflight = resource.fence_inflight
+        if inflight is not None:
+            epoch, members, started = inflight
+            dead = [m for m in members if m not in resource.workers or
+                    resource.workers[m].state == EXITED]
+            if dead or time.monotonic() - started > self.fence_timeout:
+                logger.warning('Fence epoch %d abandoned (%s).', epoch,
+                               'member exited' if dead else 'timeout')
+                for wid in members:
+                    w = resource.workers.get(wid)
+                    if w is not None and w.state != EXITED:
+                        w.proc.pipe.send({'cmd': 'fence_abort',
+                                          'epoch': epoch})
+                resource.fence_inflight = None
+                resource.fence_wanted = True
+                resource.fence_fresh = True
+            else:
+                return
+        if not resource.fence_wanted:
+            return
+        members = sorted((w.id for w in resource.ready()),
+                         key=lambda wid: resource.workers[wid].slot.index)
+        resource.fence_wanted = False
+        if members == resource.fenced_members:
+            return
+        if not members:
+            resource.fenced_members = []
+            resource.fenced_epoch = resource.epoch
+            self._publish_active(resource)
+            return
+        resource.epoch += 1
+        epoch = resource.epoch
+        previous = list(resource.fenced_members)
+        for rank, wid in enumerate(members):
+            resource.workers[wid].proc.pipe.send({
+                'cmd': 'fence', 'epoch': epoch, 'rank': rank,
+                'members': members, 'previous': previous,
+                'slots': [resource.workers[m].slot.index for m in members],
+                'fresh': resource.fence_fresh,
+                'group': '%s/%s' % (resource.namespace, resource.name)})
+        resource.fence_inflight = (epoch, members, time.monotonic())
+        self.events.emit('fence_start', epoch=epoch, members=members)
+
+    def _on_fenced(self, resource, message):
+        inflight = resource.fence_inflight
+        if inflight is None or message.get('epoch') != inflight[0]:
+            return
+        epoch, members, started = inflight
+        resource.fence_inflight = None
+        if not message.get('ok', False):
+            logger.warning('Fence epoch %d failed: %s', epoch,
+                           message.get('detail'))
+            resource.fence_wanted = True
+            resource.fence_fresh = True
+            return
+        resource.fence_fresh = False
+        resource.fenced_epoch = epoch
+        resource.fenced_members = members
+        self.events.emit('fence_done', epoch=epoch, members=members,
+                         wall_s=time.monotonic() - started,
+                         transport=message.get('transport'),
+                         allreduce_us=message.get('allreduce_us'),
+                         init_ms=message.get('init_ms'))
+        self._publish_active(resource)
+
+    def _publish_active(self, resource):
+        if self.redis is None:
+            return
+        try:
+            self.redis.set(ACTIVE_KEY.format(ns=resource.namespace,
+                                             name=resource.name),
+                           json.dumps({'epoch': resource.fenced_epoch,
+                                       'members': resource.fenced_members}))
+        except Exception:  # pylint: disable=broad-except
+            pass

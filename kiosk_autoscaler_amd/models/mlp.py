@@ -1,0 +1,135 @@
+"""The worker's model: a stack of bf16 residual MLP blocks on random weights.
+
+BASELINE.json asks for "random-init worker weights"; SURVEY §2.4 N2 fixes
+the shape: ``[B x d] . [d x 4d] -> act -> [4d x d]``.  One block is
+
+    h = gelu_tanh(x @ W1^T + b1)          (bf16 out, fp32 accumulate)
+    y = h @ W2^T + b2 + x                 (bf16 out, residual)
+
+with ``W1: [H, D]`` and ``W2: [D, H]`` stored K-contiguous (the layout both
+MFMA operand fragments read along K).  Layers chain ``x <- y``.
+
+Engines:
+
+* :class:`HipMlpEngine` -- the MI355X path: weights generated *on device*
+  by the native init kernel (no host RNG / H2D of a GB of weights on the
+  scale-up critical path), the N1 warm-start kernel, and the forward as one
+  captured hipGraph (first inference after READY = one graph launch).
+* :class:`CpuMlpEngine` -- the mock worker of BASELINE config 1 (plumbing
+  on a machine without a GPU): numpy at toy size plus an optional sleep.
+* :func:`torch_reference` -- fp32 PyTorch reference used by the numerics
+  tests.
+"""
+import time
+
+import numpy as np
+
+GELU_C = 0.7978845608028654  # sqrt(2/pi)
+
+
+def init_bound(fan_in):
+    return 1.0 / np.sqrt(fan_in)
+
+
+def gelu_tanh_np(x):
+    return 0.5 * x * (1.0 + np.tanh(GELU_C * (x + 0.044715 * x ** 3)))
+
+
+def torch_reference(x, w1, b1, w2, b2, residual=True):
+    """fp32 reference of one block (inputs may be bf16 tensors)."""
+    import torch
+    xf = x.float()
+    h = torch.nn.functional.linear(xf, w1.float(), b1.float())
+    h = 0.5 * h * (1.0 + torch.tanh(GELU_C * (h + 0.044715 * h ** 3)))
+    h = h.to(torch.bfloat16).float()   # the kernel stores h as bf16
+    y = torch.nn.functional.linear(h, w2.float(), b2.float())
+    if residual:
+        y = y + xf
+    return y
+
+
+class CpuMlpEngine(object):
+    """Mock CPU engine: real (tiny) math plus a configurable service time."""
+
+    name = 'cpu'
+
+    def __init__(self, cfg, stage=None, dim=64, hidden=256):
+        self.cfg = cfg
+        rng = np.random.default_rng(cfg.seed)
+        self.layers = []
+        for _ in range(max(1, min(cfg.layers, 4))):
+            self.layers.append((
+                rng.uniform(-init_bound(dim), init_bound(dim),
+                            (hidden, dim)).astype(np.float32),
+                np.zeros(hidden, np.float32),
+                rng.uniform(-init_bound(hidden), init_bound(hidden),
+                            (dim, hidden)).astype(np.float32),
+                np.zeros(dim, np.float32)))
+        self.dim = dim
+        if stage:
+            stage('device_ready')
+
+    def warmstart(self):
+        self.forward(8, 1, 0)
+        return {'backend': 'cpu', 'cus_touched': 0}
+
+    def forward(self, rows, passes, seed):
+        t0 = time.perf_counter()
+        rng = np.random.default_rng(seed)
+        x = rng.standard_normal((min(rows, 256), self.dim)).astype(np.float32)
+        for _ in range(max(1, passes)):
+            for w1, b1, w2, b2 in self.layers:
+                x = gelu_tanh_np(x @ w1.T + b1) @ w2.T + b2 + x
+        if self.cfg.mock_work_ms > 0:
+            remaining = self.cfg.mock_work_ms * max(1, passes) / 1000.0 - (
+                time.perf_counter() - t0)
+            if remaining > 0:
+                time.sleep(remaining)
+        return {'ms': (time.perf_counter() - t0) * 1e3,
+                'checksum': float(x.sum())}
+
+    def close(self):
+        self.layers = []
+
+
+class HipMlpEngine(object):
+    """MI355X engine backed by the native ``_kiosk_hip`` module."""
+
+    name = 'hip'
+
+    def __init__(self, cfg, stage=None):
+        from ..ops import native
+        mod = native.load()
+        if stage:
+            stage('native_loaded')
+        self.cfg = cfg
+        self.engine = mod.Engine(0, cfg.dim, cfg.hidden, cfg.layers,
+                                 max(cfg.rows * cfg.batch, 256), cfg.seed)
+        if stage:
+            for name, t in sorted(self.engine.stage_times().items(),
+                                  key=lambda kv: kv[1]):
+                stage(name)
+
+    def warmstart(self):
+        info = dict(self.engine.warmstart())
+        # pre-capture the default-shape forward so the first key is a
+        # single graph launch
+        self.engine.prepare(self.cfg.rows)
+        return info
+
+    def forward(self, rows, passes, seed):
+        return dict(self.engine.forward(int(rows), int(max(1, passes)),
+                                        int(seed)))
+
+    def close(self):
+        if self.engine is not None:
+            self.engine.close()
+            self.engine = None
+
+
+def create_engine(backend, cfg, stage=None):
+    if backend == 'hip':
+        return HipMlpEngine(cfg, stage)
+    if backend == 'cpu':
+        return CpuMlpEngine(cfg, stage)
+    raise ValueError('unknown worker backend %r' % backend)

@@ -1,0 +1,63 @@
+"""Loader for the in-tree native module ``_kiosk_hip`` (HIP/gfx950 + RCCL).
+
+Load order matters: PyTorch-ROCm bundles its own ``libamdhip64.so`` (SONAME
+``libamdhip64.so.7``).  Importing torch first makes the extension's
+``libamdhip64.so.7`` dependency resolve to that already-loaded runtime, so
+one HIP runtime serves both (two runtimes in one process would each own the
+device).  RCCL is *not* a link-time dependency: the fence code ``dlopen``s a
+full RCCL (``KIOSK_RCCL_LIB``, default ROCm's, which has
+``ncclCommShrink``) with ``RTLD_LOCAL``.
+
+There is no silent fallback: on a machine with a GPU a missing or stale
+extension raises :class:`NativeUnavailable` with the build command.
+"""
+import glob
+import importlib
+import os
+import sys
+
+_MOD = None
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD_HINT = ('build it with `python tools/build_native.py` '
+              '(or `python -c "import __graft_entry__ as g; g.build()"`)')
+
+
+class NativeUnavailable(ImportError):
+    pass
+
+
+def extension_candidates():
+    return sorted(glob.glob(os.path.join(HERE, '_kiosk_hip*.so')))
+
+
+def load():
+    """Import and return the native module (cached)."""
+    global _MOD
+    if _MOD is not None:
+        return _MOD
+    if not extension_candidates():
+        raise NativeUnavailable('native module _kiosk_hip is not built; '
+                                + BUILD_HINT)
+    try:
+        import torch  # noqa: F401  -- must precede the extension (see above)
+    except ImportError:
+        pass
+    try:
+        _MOD = importlib.import_module('kiosk_autoscaler_amd.ops._kiosk_hip')
+    except ImportError as err:
+        raise NativeUnavailable('cannot import _kiosk_hip (%s); %s' % (
+            err, BUILD_HINT))
+    return _MOD
+
+
+def available():
+    try:
+        load()
+        return True
+    except NativeUnavailable:
+        return False
+
+
+def loaded_path():
+    mod = sys.modules.get('kiosk_autoscaler_amd.ops._kiosk_hip')
+    return getattr(mod, '__file__', None)

@@ -1,0 +1,106 @@
+"""Worker process entry point: ``python -m kiosk_autoscaler_amd.worker.main``.
+
+Two start modes (both spawned by :mod:`kiosk_autoscaler_amd.gpumgr`):
+
+* **standby** (no ``--assign``): import PyTorch-ROCm and the native kernel
+  module, report ``standby`` and block on the command pipe.  No HIP call is
+  made, so the process holds no GPU and may later be pinned to any one.
+* **cold** (``--assign JSON``): the same, but start immediately.
+
+After assignment the process pins itself (``HIP_VISIBLE_DEVICES`` + CPU
+affinity), builds the engine and runs :class:`WorkerRuntime`.
+"""
+import argparse
+import logging
+import os
+import sys
+import time
+
+
+def _preload(backend):
+    """Import everything heavy *without* touching the GPU."""
+    t0 = time.monotonic_ns()
+    if backend == 'hip':
+        import torch  # noqa: F401  -- shares libamdhip64 with the extension
+        from ..ops import native
+        native.load()
+    else:
+        import numpy  # noqa: F401
+    return time.monotonic_ns() - t0
+
+
+def _build_fence_factory(config):
+    if config.fence in ('none', 'off', '0'):
+        return None
+    from ..parallel.fence import make_agent_factory
+    return make_agent_factory(config)
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser(description=__doc__)
+    parser.add_argument('--cmd-fd', type=int, default=None)
+    parser.add_argument('--ev-fd', type=int, default=None)
+    parser.add_argument('--backend', default='auto')
+    parser.add_argument('--assign', default=None)
+    args = parser.parse_args(argv)
+
+    logging.basicConfig(
+        level=logging.INFO, stream=sys.stderr,
+        format='[%(asctime)s]:[%(levelname)s]:[%(name)s]: %(message)s')
+
+    from .channel import Channel
+    from .runtime import (WorkerConfig, WorkerRuntime, apply_assignment_env,
+                          parse_assignment)
+    channel = Channel(args.cmd_fd, args.ev_fd)
+
+    backend = args.backend
+    if backend == 'auto':
+        backend = 'cpu'
+        if args.assign:
+            if parse_assignment(args.assign).get('gpu') not in (None, ''):
+                backend = 'hip'
+    preload_ns = _preload(backend)
+
+    if args.assign:
+        assignment = parse_assignment(args.assign)
+    else:
+        channel.emit('standby', preload_ns=preload_ns, backend=backend)
+        while True:
+            assignment = channel.read_command()
+            if assignment is None or assignment.get('cmd') == 'exit':
+                return 0
+            if assignment.get('cmd') == 'assign':
+                break
+    apply_assignment_env(assignment)
+    config = WorkerConfig(os.environ, assignment)
+
+    from ..models.mlp import create_engine
+    from ..redisq import RedisClient
+    from ..utils.events import EventLog
+
+    def redis_factory():
+        # sentinel-aware and retrying, like the autoscaler's own client
+        return RedisClient(host=config.redis_host, port=config.redis_port,
+                           backoff=float(os.environ.get('REDIS_INTERVAL', 1)))
+
+    events = None
+    if config.record_events:
+        events = EventLog(path=os.environ.get('EVENT_LOG') or None,
+                          redis_client=redis_factory(),
+                          source=config.worker_id)
+
+    def engine_factory(cfg, stage):
+        return create_engine(backend, cfg, stage)
+
+    runtime = WorkerRuntime(config, engine_factory, channel, redis_factory,
+                            fence_factory=_build_fence_factory(config),
+                            event_log=events)
+    code = runtime.run()
+    if events is not None:
+        events.emit('worker_exit_self', worker=config.worker_id,
+                    keys_done=runtime.keys_done)
+    return code
+
+
+if __name__ == '__main__':
+    sys.exit(main())

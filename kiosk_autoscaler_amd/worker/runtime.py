@@ -1,0 +1,288 @@
+"""Worker runtime: GPU attach -> weights -> warm-start -> READY -> consume.
+
+Replaces the out-of-repo GPU pod of the reference.  The
+queue protocol is the one the reference's tally assumes
+(``autoscaler/autoscaler.py:64-73``): a consumer atomically moves an item
+from ``<q>`` into its own ``processing-<q>:<worker-id>`` list (``LMOVE ...
+RIGHT LEFT`` = FIFO with producers that ``LPUSH``), processes it, then
+deletes the processing key.  While the key exists the tally counts it as
+in-progress work.
+
+Items are job-hash keys (the kiosk convention); the hash may carry
+``rows`` / ``passes`` / ``seed`` for the inference and receives ``status``,
+timings and a checksum of the output.  A plain string item is processed
+with the configured defaults.
+"""
+import json
+import logging
+import os
+import queue as queue_mod
+import time
+
+from ..redisq import exceptions as redis_errors
+
+logger = logging.getLogger('Worker')
+
+
+def _env_int(env, name, default):
+    try:
+        return int(env.get(name, default))
+    except (TypeError, ValueError):
+        return default
+
+
+def _env_float(env, name, default):
+    try:
+        return float(env.get(name, default))
+    except (TypeError, ValueError):
+        return default
+
+
+class WorkerConfig(object):
+    def __init__(self, env, assignment):
+        template = assignment.get('template', {})
+        self.worker_id = assignment['worker_id']
+        self.kind = assignment.get('kind', 'deployment')
+        self.slot = assignment.get('slot', 0)
+        self.gpu = assignment.get('gpu', '')
+        self.queues = template.get('queues') or env.get(
+            'QUEUES', 'predict').split(env.get('QUEUE_DELIMITER', ','))
+        self.redis_host = env.get('REDIS_HOST', '127.0.0.1')
+        self.redis_port = _env_int(env, 'REDIS_PORT', 6379)
+        self.keys_per_pod = max(1, int(template.get(
+            'keys_per_pod', _env_int(env, 'KEYS_PER_POD', 1))))
+        batch_default = self.keys_per_pod if self.kind == 'job' else 1
+        self.batch = max(1, _env_int(env, 'WORKER_BATCH', batch_default))
+        self.dim = _env_int(env, 'MODEL_DIM', 4096)
+        self.hidden = _env_int(env, 'MODEL_HIDDEN', 16384)
+        self.layers = _env_int(env, 'MODEL_LAYERS', 4)
+        self.rows = _env_int(env, 'ROWS_PER_KEY', 2048)
+        self.passes = _env_int(env, 'PASSES_PER_KEY', 1)
+        self.seed = _env_int(env, 'MODEL_SEED', 1234)
+        self.warm_start = env.get('WARM_START', '1').lower() not in (
+            '0', 'false', 'no', 'off')
+        self.fence = env.get('FENCE', 'auto')
+        self.poll_block = _env_float(env, 'POLL_BLOCK_S', 0.1)
+        self.job_idle_exit = _env_float(env, 'JOB_IDLE_EXIT_S', 1.0)
+        self.mock_work_ms = _env_float(env, 'MOCK_WORK_MS', 0.0)
+        self.record_events = env.get('WORKER_EVENTS', '1') not in ('0', '')
+
+
+class QueueConsumer(object):
+    """Moves items into per-worker processing keys and back out."""
+
+    def __init__(self, redis, worker_id, queues, poll_block=0.1):
+        self.redis = redis
+        self.worker_id = worker_id
+        self.queues = list(queues)
+        self.poll_block = poll_block
+        self._rotate = 0
+
+    def processing_key(self, queue, slot=0):
+        suffix = '' if slot == 0 else '.%d' % slot
+        return 'processing-%s:%s%s' % (queue, self.worker_id, suffix)
+
+    def pull(self, limit=1, block=True):
+        """Return up to ``limit`` ``(queue, item, processing_key)`` tuples.
+
+        Sweeps every queue with non-blocking ``LMOVE`` first; when all are
+        empty, blocks on one queue (rotating) for ``poll_block`` seconds --
+        or indefinitely-short 1 s chunks with a single queue, where
+        ``BLMOVE`` wakes the instant a key lands."""
+        taken = []
+        for queue in self.queues:
+            while len(taken) < limit:
+                pkey = self.processing_key(queue, len(taken))
+                item = self.redis.lmove(queue, pkey, 'RIGHT', 'LEFT')
+                if item is None:
+                    break
+                taken.append((queue, item, pkey))
+        if taken or not block:
+            return taken
+        queue = self.queues[self._rotate % len(self.queues)]
+        self._rotate += 1
+        timeout = 1.0 if len(self.queues) == 1 else self.poll_block
+        pkey = self.processing_key(queue, 0)
+        item = self.redis.blmove(queue, pkey, timeout, 'RIGHT', 'LEFT')
+        if item is not None:
+            taken.append((queue, item, pkey))
+        return taken
+
+    def queues_empty(self):
+        return all(self.redis.llen(q) == 0 for q in self.queues)
+
+    def complete(self, pkey):
+        self.redis.delete(pkey)
+
+
+class WorkerRuntime(object):
+    """Runs one assigned worker to completion.  Returns the exit code."""
+
+    def __init__(self, config, engine_factory, channel, redis_factory,
+                 fence_factory=None, event_log=None):
+        self.config = config
+        self.engine_factory = engine_factory
+        self.channel = channel
+        self.redis_factory = redis_factory
+        self.fence_factory = fence_factory
+        self.events = event_log
+        self.engine = None
+        self.fence_agent = None
+        self.draining = False
+        self.stages = {}
+        self.keys_done = 0
+
+    def _stage(self, name):
+        t = time.monotonic_ns()
+        self.stages[name] = t
+        self.channel.emit('stage', stage=name, t=t)
+        return t
+
+    def _emit_event(self, kind, **fields):
+        if self.events is not None:
+            fields.setdefault('worker', self.config.worker_id)
+            self.events.emit(kind, **fields)
+
+    def _handle_commands(self):
+        while True:
+            try:
+                message = self.channel.commands.get_nowait()
+            except queue_mod.Empty:
+                return
+            cmd = message.get('cmd')
+            if cmd in ('drain', 'exit', 'eof'):
+                self.draining = True
+            elif cmd in ('fence', 'fence_abort') and self.fence_agent:
+                self.fence_agent.submit(message)
+
+    def start(self):
+        cfg = self.config
+        self._stage('assigned_recv')
+        self.redis = self.redis_factory()
+        self.engine = self.engine_factory(cfg, self._stage)
+        self._stage('weights_ready')
+        if cfg.warm_start:
+            info = self.engine.warmstart()
+            self._stage('warmstart_done')
+            self._emit_event('warmstart', **{k: v for k, v in info.items()
+                                             if k != 'cu_mask'})
+        t_ready = self._stage('ready')
+        self.channel.emit('ready', t=t_ready, stages=self.stages)
+        self._emit_event('worker_ready', gpu=cfg.slot, t_ns=t_ready,
+                         stages=self.stages)
+        if self.fence_factory is not None:
+            self.fence_agent = self.fence_factory(self)
+
+    def run(self):
+        cfg = self.config
+        self.channel.start_reader()
+        try:
+            self.start()
+        except Exception as err:  # pylint: disable=broad-except
+            logger.exception('worker %s failed to start', cfg.worker_id)
+            self.channel.emit('error', message='%s: %s' % (
+                type(err).__name__, err))
+            return 3
+        consumer = QueueConsumer(self.redis, cfg.worker_id, cfg.queues,
+                                 cfg.poll_block)
+        idle_since = time.monotonic()
+        busy = False
+        try:
+            while True:
+                self._handle_commands()
+                if self.draining:
+                    break
+                try:
+                    items = consumer.pull(limit=cfg.batch)
+                except redis_errors.ConnectionError as err:
+                    logger.warning('redis unavailable (%s); retrying', err)
+                    time.sleep(0.5)
+                    continue
+                if not items:
+                    if busy:
+                        busy = False
+                        self.channel.emit('idle')
+                    if cfg.kind == 'job' and (
+                            time.monotonic() - idle_since >= cfg.job_idle_exit
+                            and consumer.queues_empty()):
+                        logger.info('job worker %s: queue empty, exiting',
+                                    cfg.worker_id)
+                        break
+                    continue
+                if not busy:
+                    busy = True
+                    self.channel.emit('busy')
+                self._process(consumer, items)
+                idle_since = time.monotonic()
+        finally:
+            if self.fence_agent is not None:
+                self.fence_agent.close()
+            if self.engine is not None:
+                self.engine.close()
+        return 0
+
+    def _job_params(self, item):
+        params = {'rows': self.config.rows, 'passes': self.config.passes,
+                  'seed': self.config.seed}
+        try:
+            fields = self.redis.hgetall(item)
+        except redis_errors.ResponseError:
+            fields = {}  # item is not a hash key
+        for name in ('rows', 'passes', 'seed'):
+            if name in fields:
+                try:
+                    params[name] = int(fields[name])
+                except ValueError:
+                    pass
+        return params, fields
+
+    def _process(self, consumer, items):
+        cfg = self.config
+        t_start = time.monotonic_ns()
+        jobs = []
+        for queue, item, pkey in items:
+            params, fields = self._job_params(item)
+            jobs.append((queue, item, pkey, params, fields))
+            self._emit_event('key_start', item=item, queue=queue, t_ns=t_start,
+                             gpu=cfg.slot)
+        rows = sum(p['rows'] for _, _, _, p, _ in jobs)
+        passes = max(p['passes'] for _, _, _, p, _ in jobs)
+        result = self.engine.forward(rows, passes, jobs[0][3]['seed'])
+        t_done = time.monotonic_ns()
+        for queue, item, pkey, params, fields in jobs:
+            if fields:
+                self.redis.hset(item, mapping={
+                    'status': 'done', 'worker': cfg.worker_id,
+                    'gpu': cfg.slot, 'compute_ms': '%.3f' % result['ms'],
+                    'checksum': '%.6e' % result.get('checksum', 0.0),
+                    'started_ns': t_start, 'finished_ns': t_done})
+            consumer.complete(pkey)
+            self.keys_done += 1
+            self._emit_event('key_done', item=item, queue=queue, t_ns=t_done,
+                             gpu=cfg.slot, compute_ms=result['ms'],
+                             batch=len(jobs))
+
+
+def parse_assignment(text):
+    return json.loads(text) if isinstance(text, str) else text
+
+
+def apply_assignment_env(assignment, env=None):
+    """Put the template env and the GPU pin into ``os.environ``.
+
+    Must run before anything initialises HIP: the runtime reads
+    ``HIP_VISIBLE_DEVICES`` once, at init."""
+    env = os.environ if env is None else env
+    template = assignment.get('template', {})
+    for key, value in template.get('env', {}).items():
+        env[key] = str(value)
+    gpu = assignment.get('gpu')
+    if gpu not in (None, ''):
+        env['HIP_VISIBLE_DEVICES'] = str(gpu)
+    cpus = assignment.get('cpus') or []
+    if cpus and hasattr(os, 'sched_setaffinity'):
+        try:
+            os.sched_setaffinity(0, set(int(c) for c in cpus))
+        except OSError:
+            pass
+    return env

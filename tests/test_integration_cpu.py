@@ -1,0 +1,140 @@
+"""End-to-end plumbing on CPU (BASELINE config 1): RESP server + GPU manager
+with mock CPU workers + reconcile loop.  Keys in -> scale 0->1 -> processed
+-> scale 1->0; job mode; crash requeue; fence over the store transport."""
+import json
+import os
+import signal
+import time
+
+import pytest
+
+from kiosk_autoscaler_amd import Autoscaler, gpumgr
+from kiosk_autoscaler_amd.config import Config, Settings
+from kiosk_autoscaler_amd.redisq import RedisClient, StrictRedis
+from kiosk_autoscaler_amd.utils.events import EventLog
+
+pytestmark = pytest.mark.slow
+
+
+def wait_for(predicate, timeout=30.0, step=0.05):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        value = predicate()
+        if value:
+            return value
+        time.sleep(step)
+    raise AssertionError('condition not met within %.1fs' % timeout)
+
+
+def settings_for(server, **overrides):
+    env = {'REDIS_HOST': server.host, 'REDIS_PORT': str(server.port),
+           'QUEUES': 'predict', 'RESOURCE_NAME': 'worker',
+           'MAX_PODS': '1', 'WORKER_BACKEND': 'cpu', 'WARM_POOL': '1',
+           'FENCE': 'store', 'INTERVAL': '1', 'REDIS_INTERVAL': '0'}
+    env.update({k: str(v) for k, v in overrides.items()})
+    return Settings(Config(environ=env, use_files=False))
+
+
+@pytest.fixture
+def stack(resp_server):
+    made = []
+
+    def build(extra_env=None, **overrides):
+        settings = settings_for(resp_server, **overrides)
+        plain = StrictRedis(host=resp_server.host, port=resp_server.port,
+                            decode_responses=True)
+        events = EventLog(source='test')
+        events.keep = True
+        manager = gpumgr.build_manager(settings, redis_client=plain,
+                                       events=events,
+                                       extra_env=extra_env).start()
+        made.append(manager)
+        proxy = RedisClient(host=resp_server.host, port=resp_server.port,
+                            backoff=0)
+        scaler = Autoscaler(proxy, settings.QUEUES, actuator=manager,
+                            policy=settings.SCALE_POLICY)
+        return settings, plain, manager, scaler, events
+    yield build
+    for manager in made:
+        manager.stop(timeout=15)
+
+
+def enqueue(client, n, queue='predict', **fields):
+    for i in range(n):
+        key = '%s:job%d' % (queue, i)
+        client.hset(key, mapping=dict({'status': 'new', 'rows': 8}, **fields))
+        client.lpush(queue, key)
+
+
+def tick(scaler, s):
+    return scaler.scale(s.RESOURCE_NAMESPACE, s.RESOURCE_TYPE,
+                        s.RESOURCE_NAME, s.MIN_PODS, s.MAX_PODS,
+                        s.KEYS_PER_POD)
+
+
+def test_scale_up_process_scale_down(stack):
+    s, client, manager, scaler, events = stack()
+    wait_for(lambda: all(p.booted for p in manager.standbys)
+             and manager.standbys)
+    enqueue(client, 3)
+    assert tick(scaler, s) == 1
+    wait_for(lambda: all(client.hget('predict:job%d' % i, 'status') == 'done'
+                         for i in range(3)))
+    assert client.llen('predict') == 0
+    assert not list(client.scan_iter(match='processing-predict:*'))
+    view = manager.list_namespaced_deployment('default').items[0]
+    assert view.spec.replicas == 1 and view.status.available_replicas == 1
+    workers = [r for r in manager.status()['resources']][0]['workers']
+    assert workers[0]['from_pool'] is True
+    # fence for the 1-member set completes and is published
+    wait_for(lambda: client.get('kiosk:active:default:worker'))
+    active = json.loads(client.get('kiosk:active:default:worker'))
+    assert active['members'] == [workers[0]['id']]
+    assert tick(scaler, s) == 0
+    wait_for(lambda: not manager.status()['resources'][0]['workers'])
+    kinds = [e['ev'] for e in events.records]
+    assert 'worker_assigned' in kinds and 'worker_exit' in kinds
+    assert 'fence_done' in kinds
+
+
+def test_job_mode_one_shot(stack):
+    s, client, manager, scaler, events = stack(RESOURCE_TYPE='job',
+                                               KEYS_PER_POD='2',
+                                               MAX_PODS='2',
+                                               extra_env={
+                                                   'JOB_IDLE_EXIT_S': '0.2'})
+    enqueue(client, 4)
+    assert tick(scaler, s) == 2
+    wait_for(lambda: all(client.hget('predict:job%d' % i, 'status') == 'done'
+                         for i in range(4)))
+    # one-shot workers exit on an empty queue and release their GPUs;
+    # parallelism drops to the still-running count (no stranded job)
+    wait_for(lambda: manager.list_namespaced_job('default').items[0]
+             .spec.parallelism == 0, timeout=30)
+    view = manager.list_namespaced_job('default').items[0]
+    assert view.status.succeeded == 2
+    enqueue(client, 2)
+    assert tick(scaler, s) == 1          # new generation from zero
+    wait_for(lambda: all(client.hget('predict:job%d' % i, 'status') == 'done'
+                         for i in range(2)))
+
+
+def test_worker_crash_requeues(stack):
+    s, client, manager, scaler, events = stack(
+        extra_env={'MOCK_WORK_MS': '3000'}, WARM_POOL='0')
+    enqueue(client, 1)
+    assert tick(scaler, s) == 1
+    key = wait_for(lambda: list(client.scan_iter(
+        match='processing-predict:*')))[0]
+    assert client.lrange(key, 0, -1) == ['predict:job0']
+    worker = manager.status()['resources'][0]['workers'][0]
+    os.kill(worker['pid'], signal.SIGKILL)
+    # the item goes back to the queue and a replacement worker takes it
+    wait_for(lambda: any(e['ev'] == 'requeue' for e in events.records))
+    wait_for(lambda: len(manager.status()['resources'][0]['workers']) == 1
+             and manager.status()['resources'][0]['workers'][0]['pid']
+             != worker['pid'], timeout=30)
+    view = manager.list_namespaced_deployment('default').items[0]
+    assert view.status.restarts == 1
+    wait_for(lambda: client.hget('predict:job0', 'status') == 'done',
+             timeout=30)

@@ -1,0 +1,136 @@
+"""RESP codec, client reply callbacks, in-proc engine and socket servers."""
+import threading
+import time
+
+import pytest
+
+from kiosk_autoscaler_amd.fakes import FakeRedis, RedisEngine, glob_match
+from kiosk_autoscaler_amd.redisq import StrictRedis, exceptions
+from kiosk_autoscaler_amd.redisq.resp import (NOT_READY, ReplyError,
+                                              RespParser, encode_command,
+                                              encode_reply)
+
+
+def test_encode_command():
+    assert encode_command('LLEN', 'q') == b'*2\r\n$4\r\nLLEN\r\n$1\r\nq\r\n'
+    assert encode_command('SET', 'k', 12) == \
+        b'*3\r\n$3\r\nSET\r\n$1\r\nk\r\n$2\r\n12\r\n'
+    with pytest.raises(exceptions.DataError):
+        encode_command('SET', 'k', True)
+
+
+def test_parser_incremental_and_nested():
+    data = encode_reply([1, b'ab', None, [b'x', ReplyError('ERR no')]])
+    parser = RespParser(decode=True)
+    for i in range(len(data) - 1):   # byte by byte: never a partial reply
+        parser.feed(data[i:i + 1])
+        assert parser.gets() is NOT_READY
+    parser.feed(data[-1:])
+    reply = parser.gets()
+    assert reply[:3] == [1, 'ab', None]
+    assert reply[3][0] == 'x' and isinstance(reply[3][1], ReplyError)
+    assert parser.gets() is NOT_READY
+
+
+def test_glob():
+    assert glob_match(b'processing-predict:*', b'processing-predict:h1')
+    assert not glob_match(b'processing-predict:*', b'processing-predict')
+    assert glob_match(b'a?c', b'abc') and glob_match(b'[ab]x', b'bx')
+
+
+def _exercise(client):
+    assert client.ping() is True
+    assert client.lpush('q', 'a', 'b', 'c') == 3
+    assert client.llen('q') == 3
+    assert client.lrange('q', 0, -1) == ['c', 'b', 'a']
+    assert client.lmove('q', 'processing-q:w1', 'RIGHT', 'LEFT') == 'a'
+    assert client.rpoplpush('q', 'processing-q:w2') == 'b'
+    assert sorted(client.scan_iter(match='processing-q:*', count=1)) == [
+        'processing-q:w1', 'processing-q:w2']
+    assert client.delete('processing-q:w1', 'nope') == 1
+    assert client.hset('job', mapping={'rows': 4, 'status': 'new'}) == 2
+    assert client.hgetall('job') == {'rows': '4', 'status': 'new'}
+    assert client.hmset('job', {'status': 'done'}) is True
+    assert client.hget('job', 'status') == 'done'
+    assert client.set('k', 'v', ex=10) is True
+    assert 0 < client.ttl('k') <= 10
+    assert client.get('k') == 'v'
+    assert client.type('job') == 'hash'
+    assert client.exists('k', 'job', 'zz') == 2
+    assert client.incr('n') == 1 and client.incr('n', 5) == 6
+    info = client.info()
+    assert 'redis_version' in info
+    with pytest.raises(exceptions.ResponseError):
+        client.lpush('k', 'x')          # WRONGTYPE
+    with pytest.raises(exceptions.ResponseError):
+        client.sentinel_masters()       # plain redis: unknown command
+    pipe = client.pipeline()
+    pipe.llen('q').lpush('q', 'z').llen('q')
+    assert pipe.execute() == [1, 2, 2]
+    assert client.blmove('empty', 'dst', 0.05) is None
+    assert client.blpop(['empty'], timeout=0.05) is None
+
+
+def test_fake_client(redis_client):
+    _exercise(redis_client)
+
+
+def test_python_server(resp_server):
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    _exercise(client)
+
+
+def test_native_server(kredis_server):
+    client = StrictRedis(host=kredis_server.host, port=kredis_server.port,
+                         decode_responses=True)
+    client.flushall()
+    _exercise(client)
+
+
+def test_blocking_move_wakes(resp_server):
+    host, port = resp_server.host, resp_server.port
+    consumer = StrictRedis(host=host, port=port, decode_responses=True)
+    producer = StrictRedis(host=host, port=port, decode_responses=True)
+    got = {}
+
+    def consume():
+        t0 = time.monotonic()
+        got['item'] = consumer.blmove('jobs', 'processing-jobs:w', 5,
+                                      'RIGHT', 'LEFT')
+        got['dt'] = time.monotonic() - t0
+    thread = threading.Thread(target=consume)
+    thread.start()
+    time.sleep(0.1)
+    producer.lpush('jobs', 'j1')
+    thread.join(5)
+    assert got['item'] == 'j1'
+    assert got['dt'] < 1.0
+    assert producer.lrange('processing-jobs:w', 0, -1) == ['j1']
+
+
+def test_connection_refused():
+    client = StrictRedis(host='127.0.0.1', port=1, socket_connect_timeout=0.5)
+    with pytest.raises(exceptions.ConnectionError):
+        client.ping()
+
+
+def test_fault_injection_engine():
+    engine = RedisEngine()
+    client = FakeRedis(engine=engine)
+    engine.inject_fault('LLEN', 'connection')
+    with pytest.raises(exceptions.ConnectionError):
+        client.llen('q')
+    assert client.llen('q') == 0                 # one-shot
+    engine.inject_fault('LLEN', 'busy')
+    with pytest.raises(exceptions.ResponseError) as info:
+        client.llen('q')
+    assert 'BUSY' in str(info.value) and 'SCRIPT KILL' in str(info.value)
+
+
+def test_expiry_and_scan_type(redis_client):
+    redis_client.set('short', '1', px=30)
+    redis_client.rpush('l', 'x')
+    time.sleep(0.06)
+    assert redis_client.get('short') is None
+    assert list(redis_client.scan_iter(_type='list')) == ['l']
