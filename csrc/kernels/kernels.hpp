@@ -1,0 +1,57 @@
+// Host-side launchers for the gfx950 kernels in csrc/kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace kiosk {
+
+enum Epilogue {
+  EPI_NONE = 0,           // C = A.B^T
+  EPI_BIAS_GELU = 1,      // C = gelu_tanh(A.B^T + bias)
+  EPI_BIAS_RESIDUAL = 2,  // C = A.B^T + bias + R
+};
+
+// GEMM tile geometry (shared with the warm-start kernel, which
+// pre-allocates and zeroes the same LDS footprint).
+constexpr int kGemmBM = 128;
+constexpr int kGemmBN = 128;
+constexpr int kGemmBK = 64;
+constexpr int kGemmThreads = 256;
+constexpr int kGemmLdsBytes = 2 * 2 * kGemmBM * kGemmBK * 2;  // 64 KiB
+constexpr int kGemmBlocksPerCU = 2;
+
+// C[M,N] (bf16) = epilogue(A[M,K] . B[N,K]^T); fp32 accumulate.
+// Requires N % 128 == 0, K % 64 == 0; any M >= 1.
+hipError_t launch_gemm(const uint16_t* A, const uint16_t* B, uint16_t* C,
+                       const float* bias, const uint16_t* R, int M, int N,
+                       int K, int epilogue, hipStream_t stream);
+bool gemm_shape_ok(int M, int N, int K);
+hipError_t gemm_prepare();  // call once before launching / capturing
+
+// Uniform [lo, hi) init, counter-based (reproducible for a seed).
+hipError_t launch_init_uniform_bf16(uint16_t* p, size_t n, uint64_t seed,
+                                    float lo, float hi, hipStream_t stream);
+hipError_t launch_init_uniform_f32(float* p, size_t n, uint64_t seed,
+                                   float lo, float hi, hipStream_t stream);
+// Same, but the seed is read from device memory (graph-capturable).
+hipError_t launch_init_uniform_bf16_devseed(uint16_t* p, size_t n,
+                                            const uint64_t* seed, float lo,
+                                            float hi, hipStream_t stream);
+
+// Deterministic fp32 partial sums of a bf16 buffer (one per block).
+constexpr int kSumBlocks = 1024;
+hipError_t launch_partial_sums(const uint16_t* p, size_t n, float* partials,
+                               hipStream_t stream);
+
+// N1 warm-start: one workgroup per CU (LDS request > half the CU's LDS
+// keeps two from sharing a CU); zeroes `lds_bytes` of LDS, streams a slice
+// of `w` (n elements), runs `iters` MFMA steps and records per-WG
+// {HW_ID, XCC_ID, t0, t1, checksum bits, ...} into record[8 * wg].
+constexpr int kWarmRecordWords = 8;
+hipError_t launch_warmstart(const uint16_t* w, size_t n, uint32_t* record,
+                            int nblocks, int iters, int lds_bytes,
+                            hipStream_t stream);
+
+}  // namespace kiosk

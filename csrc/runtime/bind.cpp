@@ -1,0 +1,210 @@
+// Python bindings for the native module `_kiosk_hip`.
+//
+// Raw-pointer entry points (gemm, init, sums) let tests drive the kernels
+// on torch-allocated tensors (tensor.data_ptr(), the current stream);
+// Engine / Fence are the runtime objects the worker uses.  Every
+// long-running call releases the GIL.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../kernels/kernels.hpp"
+#include "engine.hpp"
+#include "fence.hpp"
+
+namespace py = pybind11;
+using kiosk::check_hip;
+
+namespace {
+
+template <typename T>
+T* ptr(unsigned long long p) {
+  return reinterpret_cast<T*>(static_cast<uintptr_t>(p));
+}
+
+hipStream_t stream_of(unsigned long long s) {
+  return reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(s));
+}
+
+py::dict warm_to_dict(const kiosk::WarmStartResult& r) {
+  py::dict d;
+  d["blocks"] = r.blocks;
+  d["cus_touched"] = r.distinct_cus;
+  d["xccs_touched"] = r.distinct_xccs;
+  d["iters"] = r.iters;
+  d["lds_bytes"] = r.lds_bytes;
+  d["kernel_us"] = r.kernel_us;
+  d["span_us"] = r.span_us;
+  d["wall_us"] = r.wall_us;
+  d["checksum"] = r.checksum;
+  d["cu_mask"] = r.cu_keys;
+  return d;
+}
+
+py::dict fwd_to_dict(const kiosk::ForwardResult& r) {
+  py::dict d;
+  d["ms"] = r.ms;
+  d["gpu_ms"] = r.gpu_ms;
+  d["checksum"] = r.checksum;
+  d["rows"] = r.rows;
+  d["passes"] = r.passes;
+  d["graph"] = r.graph;
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_kiosk_hip, m) {
+  m.doc() = "MI355X (gfx950) kernels + runtime for kiosk_autoscaler_amd";
+  m.attr("arch") = "gfx950";
+  m.attr("gemm_tile") = py::make_tuple(kiosk::kGemmBM, kiosk::kGemmBN,
+                                       kiosk::kGemmBK);
+  m.attr("gemm_lds_bytes") = kiosk::kGemmLdsBytes;
+  m.attr("sum_blocks") = kiosk::kSumBlocks;
+
+  m.def("gemm_shape_ok", &kiosk::gemm_shape_ok);
+  m.def(
+      "gemm",
+      [](unsigned long long a, unsigned long long b, unsigned long long c,
+         unsigned long long bias, unsigned long long res, int M, int N, int K,
+         int epilogue, unsigned long long stream) {
+        check_hip(kiosk::gemm_prepare(), "gemm_prepare");
+        check_hip(kiosk::launch_gemm(ptr<const uint16_t>(a),
+                                     ptr<const uint16_t>(b), ptr<uint16_t>(c),
+                                     ptr<const float>(bias),
+                                     ptr<const uint16_t>(res), M, N, K,
+                                     epilogue, stream_of(stream)),
+                  "launch_gemm");
+      },
+      py::arg("a"), py::arg("b"), py::arg("c"), py::arg("bias") = 0,
+      py::arg("res") = 0, py::arg("M"), py::arg("N"), py::arg("K"),
+      py::arg("epilogue") = 0, py::arg("stream") = 0,
+      py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "init_uniform_bf16",
+      [](unsigned long long p, size_t n, unsigned long long seed, float lo,
+         float hi, unsigned long long stream) {
+        check_hip(kiosk::launch_init_uniform_bf16(ptr<uint16_t>(p), n, seed,
+                                                  lo, hi, stream_of(stream)),
+                  "init_uniform_bf16");
+      },
+      py::arg("ptr"), py::arg("n"), py::arg("seed"), py::arg("lo") = -1.0f,
+      py::arg("hi") = 1.0f, py::arg("stream") = 0,
+      py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "init_uniform_f32",
+      [](unsigned long long p, size_t n, unsigned long long seed, float lo,
+         float hi, unsigned long long stream) {
+        check_hip(kiosk::launch_init_uniform_f32(ptr<float>(p), n, seed, lo,
+                                                 hi, stream_of(stream)),
+                  "init_uniform_f32");
+      },
+      py::arg("ptr"), py::arg("n"), py::arg("seed"), py::arg("lo") = -1.0f,
+      py::arg("hi") = 1.0f, py::arg("stream") = 0,
+      py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "partial_sums",
+      [](unsigned long long p, size_t n, unsigned long long out,
+         unsigned long long stream) {
+        check_hip(kiosk::launch_partial_sums(ptr<const uint16_t>(p), n,
+                                             ptr<float>(out),
+                                             stream_of(stream)),
+                  "partial_sums");
+      },
+      py::arg("ptr"), py::arg("n"), py::arg("out"), py::arg("stream") = 0,
+      py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "warmstart_raw",
+      [](unsigned long long w, size_t n, unsigned long long record,
+         int nblocks, int iters, int lds_bytes, unsigned long long stream) {
+        check_hip(kiosk::launch_warmstart(ptr<const uint16_t>(w), n,
+                                          ptr<uint32_t>(record), nblocks,
+                                          iters, lds_bytes, stream_of(stream)),
+                  "launch_warmstart");
+      },
+      py::arg("w"), py::arg("n"), py::arg("record"), py::arg("nblocks"),
+      py::arg("iters"), py::arg("lds_bytes"), py::arg("stream") = 0,
+      py::call_guard<py::gil_scoped_release>());
+  m.def("synchronize", [] { check_hip(hipDeviceSynchronize(), "sync"); },
+        py::call_guard<py::gil_scoped_release>());
+
+  py::class_<kiosk::Engine>(m, "Engine")
+      .def(py::init<int, int, int, int, int, unsigned long long>(),
+           py::arg("device"), py::arg("dim"), py::arg("hidden"),
+           py::arg("layers"), py::arg("max_rows"), py::arg("seed"),
+           py::call_guard<py::gil_scoped_release>())
+      .def(
+          "warmstart",
+          [](kiosk::Engine& e, int iters, int lds_bytes) {
+            kiosk::WarmStartResult r;
+            {
+              py::gil_scoped_release release;
+              r = e.warmstart(iters, lds_bytes);
+            }
+            return warm_to_dict(r);
+          },
+          py::arg("iters") = 4096,
+          py::arg("lds_bytes") = 2 * kiosk::kGemmLdsBytes)
+      .def("prepare", &kiosk::Engine::prepare, py::arg("rows"),
+           py::call_guard<py::gil_scoped_release>())
+      .def(
+          "forward",
+          [](kiosk::Engine& e, int rows, int passes,
+             unsigned long long seed) {
+            kiosk::ForwardResult r;
+            {
+              py::gil_scoped_release release;
+              r = e.forward(rows, passes, seed);
+            }
+            return fwd_to_dict(r);
+          },
+          py::arg("rows"), py::arg("passes") = 1, py::arg("seed") = 0)
+      .def("close", &kiosk::Engine::close,
+           py::call_guard<py::gil_scoped_release>())
+      .def("stage_times",
+           [](const kiosk::Engine& e) {
+             py::dict d;
+             for (const auto& kv : e.stages()) d[py::str(kv.first)] = kv.second;
+             return d;
+           })
+      .def("info", &kiosk::Engine::info)
+      .def("weight_ptr", &kiosk::Engine::weight_ptr)
+      .def("act_ptr", &kiosk::Engine::act_ptr)
+      .def_property_readonly("stream", &kiosk::Engine::stream_handle)
+      .def_property_readonly("dim", &kiosk::Engine::dim)
+      .def_property_readonly("hidden", &kiosk::Engine::hidden)
+      .def_property_readonly("layers", &kiosk::Engine::layers)
+      .def_property_readonly("max_rows", &kiosk::Engine::max_rows);
+
+  m.def("rccl_library", &kiosk::rccl_library);
+  m.def("rccl_version", &kiosk::rccl_version);
+  m.def("fence_can_shrink", &kiosk::rccl_can_shrink);
+  m.def("fence_unique_id",
+        [] { return py::bytes(kiosk::rccl_unique_id()); });
+
+  py::class_<kiosk::Fence>(m, "Fence")
+      .def(py::init([](py::bytes uid, int nranks, int rank, double timeout) {
+             std::string id = uid;
+             py::gil_scoped_release release;
+             return new kiosk::Fence(id, nranks, rank, timeout);
+           }),
+           py::arg("unique_id"), py::arg("nranks"), py::arg("rank"),
+           py::arg("timeout") = 60.0)
+      .def("allreduce", &kiosk::Fence::allreduce,
+           py::call_guard<py::gil_scoped_release>())
+      .def(
+          "shrink",
+          [](kiosk::Fence& f, const std::vector<int>& excluded,
+             double timeout) -> kiosk::Fence& {
+            py::gil_scoped_release release;
+            f.shrink(excluded, timeout);
+            return f;
+          },
+          py::arg("excluded"), py::arg("timeout") = 60.0,
+          py::return_value_policy::reference)
+      .def("destroy", &kiosk::Fence::destroy,
+           py::call_guard<py::gil_scoped_release>())
+      .def("abort", &kiosk::Fence::abort,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("nranks", &kiosk::Fence::nranks)
+      .def_property_readonly("rank", &kiosk::Fence::rank);
+}

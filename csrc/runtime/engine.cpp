@@ -1,0 +1,332 @@
+// Worker inference engine (see engine.hpp).
+#include "engine.hpp"
+
+#include <time.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <set>
+
+#include "../kernels/kernels.hpp"
+
+namespace kiosk {
+
+void check_hip(hipError_t err, const char* what) {
+  if (err != hipSuccess) {
+    throw std::runtime_error(std::string(what) + ": " +
+                             hipGetErrorString(err));
+  }
+}
+
+long long monotonic_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<long long>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+
+namespace {
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+}  // namespace
+
+void Engine::stage(const char* name) {
+  stages_.emplace_back(name, monotonic_ns());
+}
+
+void Engine::launch_or_throw(hipError_t err, const char* what) {
+  check_hip(err, what);
+}
+
+Engine::Engine(int device, int dim, int hidden, int layers, int max_rows,
+               unsigned long long seed)
+    : device_(device), dim_(dim), hidden_(hidden), layers_(layers),
+      max_rows_(max_rows) {
+  if (!gemm_shape_ok(1, hidden, dim) || !gemm_shape_ok(1, dim, hidden)) {
+    throw std::invalid_argument(
+        "model dims must be multiples of 128 (dim and hidden)");
+  }
+  if (layers < 1 || max_rows < 1) {
+    throw std::invalid_argument("layers and max_rows must be >= 1");
+  }
+  stage("engine_enter");
+  check_hip(hipSetDevice(device), "hipSetDevice");
+  check_hip(hipFree(nullptr), "hip context init");
+  stage("hip_context");
+  check_hip(hipDeviceGetAttribute(&cu_count_, hipDeviceAttributeMultiprocessorCount,
+                                  device),
+            "hipDeviceGetAttribute");
+  check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking),
+            "hipStreamCreate");
+  check_hip(hipEventCreate(&ev0_), "hipEventCreate");
+  check_hip(hipEventCreate(&ev1_), "hipEventCreate");
+  check_hip(gemm_prepare(), "gemm_prepare");
+  stage("stream_ready");
+
+  // One arena: per-layer W1 [H,D], b1 [H], W2 [D,H], b2 [D]; then x, y, h,
+  // partial sums and the device-side seed.
+  const size_t A = 256;
+  std::vector<size_t> offsets;
+  size_t off = 0;
+  for (int l = 0; l < layers; ++l) {
+    offsets.push_back(off); off = align_up(off + size_t(hidden) * dim * 2, A);
+    offsets.push_back(off); off = align_up(off + size_t(hidden) * 4, A);
+    offsets.push_back(off); off = align_up(off + size_t(dim) * hidden * 2, A);
+    offsets.push_back(off); off = align_up(off + size_t(dim) * 4, A);
+  }
+  const size_t x_off = off; off = align_up(off + size_t(max_rows) * dim * 2, A);
+  const size_t y_off = off; off = align_up(off + size_t(max_rows) * dim * 2, A);
+  const size_t h_off = off; off = align_up(off + size_t(max_rows) * hidden * 2, A);
+  const size_t p_off = off; off = align_up(off + kSumBlocks * 4, A);
+  const size_t s_off = off; off = align_up(off + 8, A);
+  arena_bytes_ = off;
+  check_hip(hipMalloc(reinterpret_cast<void**>(&arena_), arena_bytes_),
+            "hipMalloc(arena)");
+  for (int l = 0; l < layers; ++l) {
+    w1_.push_back(reinterpret_cast<uint16_t*>(arena_ + offsets[4 * l + 0]));
+    b1_.push_back(reinterpret_cast<float*>(arena_ + offsets[4 * l + 1]));
+    w2_.push_back(reinterpret_cast<uint16_t*>(arena_ + offsets[4 * l + 2]));
+    b2_.push_back(reinterpret_cast<float*>(arena_ + offsets[4 * l + 3]));
+  }
+  x_ = reinterpret_cast<uint16_t*>(arena_ + x_off);
+  y_ = reinterpret_cast<uint16_t*>(arena_ + y_off);
+  h_ = reinterpret_cast<uint16_t*>(arena_ + h_off);
+  partials_ = reinterpret_cast<float*>(arena_ + p_off);
+  seed_dev_ = reinterpret_cast<unsigned long long*>(arena_ + s_off);
+  check_hip(hipHostMalloc(reinterpret_cast<void**>(&seed_host_), 8),
+            "hipHostMalloc(seed)");
+  check_hip(hipHostMalloc(reinterpret_cast<void**>(&partials_host_),
+                          kSumBlocks * 4),
+            "hipHostMalloc(partials)");
+  stage("hbm_alloc");
+
+  // Random-init weights on the device (PyTorch nn.Linear-style bounds).
+  const float bd = 1.0f / std::sqrt(static_cast<float>(dim));
+  const float bh = 1.0f / std::sqrt(static_cast<float>(hidden));
+  for (int l = 0; l < layers; ++l) {
+    const unsigned long long s = seed * 1000003ull + 16ull * l;
+    launch_or_throw(launch_init_uniform_bf16(w1_[l], size_t(hidden) * dim,
+                                             s + 1, -bd, bd, stream_),
+                    "init W1");
+    launch_or_throw(launch_init_uniform_f32(b1_[l], hidden, s + 2, -bd, bd,
+                                            stream_),
+                    "init b1");
+    launch_or_throw(launch_init_uniform_bf16(w2_[l], size_t(dim) * hidden,
+                                             s + 3, -bh, bh, stream_),
+                    "init W2");
+    launch_or_throw(launch_init_uniform_f32(b2_[l], dim, s + 4, -bh, bh,
+                                            stream_),
+                    "init b2");
+  }
+  check_hip(hipStreamSynchronize(stream_), "weights init sync");
+  stage("weights_init");
+}
+
+Engine::~Engine() {
+  try {
+    close();
+  } catch (...) {
+  }
+}
+
+void Engine::close() {
+  if (closed_) return;
+  closed_ = true;
+  for (auto& kv : graphs_) {
+    hipGraphExecDestroy(kv.second.second);
+    hipGraphDestroy(kv.second.first);
+  }
+  graphs_.clear();
+  if (stream_) hipStreamSynchronize(stream_);
+  if (arena_) hipFree(arena_);
+  if (seed_host_) hipHostFree(seed_host_);
+  if (partials_host_) hipHostFree(partials_host_);
+  if (ev0_) hipEventDestroy(ev0_);
+  if (ev1_) hipEventDestroy(ev1_);
+  if (stream_) hipStreamDestroy(stream_);
+  arena_ = nullptr;
+  seed_host_ = nullptr;
+  partials_host_ = nullptr;
+  stream_ = nullptr;
+  ev0_ = ev1_ = nullptr;
+}
+
+WarmStartResult Engine::warmstart(int iters, int lds_bytes) {
+  if (closed_) throw std::runtime_error("engine closed");
+  WarmStartResult r;
+  r.blocks = cu_count_;
+  r.iters = iters;
+  r.lds_bytes = lds_bytes;
+  const long long t0 = monotonic_ns();
+  uint32_t* rec = nullptr;
+  const size_t words = size_t(r.blocks) * kWarmRecordWords;
+  check_hip(hipMalloc(reinterpret_cast<void**>(&rec), words * 4),
+            "hipMalloc(warm record)");
+  check_hip(hipMemsetAsync(rec, 0, words * 4, stream_), "memset record");
+  check_hip(hipEventRecord(ev0_, stream_), "event");
+  hipError_t err = launch_warmstart(w1_[0], size_t(hidden_) * dim_, rec,
+                                    r.blocks, iters, lds_bytes, stream_);
+  if (err != hipSuccess) {
+    hipFree(rec);
+    check_hip(err, "launch_warmstart");
+  }
+  check_hip(hipEventRecord(ev1_, stream_), "event");
+  std::vector<uint32_t> host(words);
+  check_hip(hipMemcpyAsync(host.data(), rec, words * 4, hipMemcpyDeviceToHost,
+                           stream_),
+            "copy record");
+  check_hip(hipStreamSynchronize(stream_), "warmstart sync");
+  hipFree(rec);
+  float ms = 0;
+  hipEventElapsedTime(&ms, ev0_, ev1_);
+  r.kernel_us = ms * 1e3;
+  r.wall_us = (monotonic_ns() - t0) / 1e3;
+  std::set<unsigned> cus, xccs;
+  unsigned long long tmin = ~0ull, tmax = 0;
+  double checksum = 0;
+  for (int b = 0; b < r.blocks; ++b) {
+    const uint32_t* w = &host[size_t(b) * kWarmRecordWords];
+    const unsigned hw = w[0], xcc = w[1] & 0xf;
+    const unsigned cu = (hw >> 8) & 0xf, sh = (hw >> 12) & 0x1,
+                   se = (hw >> 13) & 0x7;
+    cus.insert((xcc << 16) | (se << 8) | (sh << 4) | cu);
+    xccs.insert(xcc);
+    const unsigned long long a = (static_cast<unsigned long long>(w[3]) << 32) | w[2];
+    const unsigned long long z = (static_cast<unsigned long long>(w[5]) << 32) | w[4];
+    if (a) tmin = std::min(tmin, a);
+    tmax = std::max(tmax, z);
+    float f;
+    std::memcpy(&f, &w[6], 4);
+    checksum += f;
+  }
+  r.distinct_cus = static_cast<int>(cus.size());
+  r.distinct_xccs = static_cast<int>(xccs.size());
+  r.span_us = tmax > tmin ? (tmax - tmin) / 100.0 : 0.0;  // 100 MHz clock
+  r.checksum = checksum;
+  r.cu_keys.assign(cus.begin(), cus.end());
+  stage("warmstart");
+  return r;
+}
+
+void Engine::enqueue_forward(int rows) {
+  launch_or_throw(launch_init_uniform_bf16_devseed(
+                      x_, size_t(rows) * dim_,
+                      reinterpret_cast<const uint64_t*>(seed_dev_), -1.0f,
+                      1.0f, stream_),
+                  "input init");
+  uint16_t* cur = x_;
+  uint16_t* nxt = y_;
+  for (int l = 0; l < layers_; ++l) {
+    launch_or_throw(launch_gemm(cur, w1_[l], h_, b1_[l], nullptr, rows,
+                                hidden_, dim_, EPI_BIAS_GELU, stream_),
+                    "gemm1");
+    launch_or_throw(launch_gemm(h_, w2_[l], nxt, b2_[l], cur, rows, dim_,
+                                hidden_, EPI_BIAS_RESIDUAL, stream_),
+                    "gemm2");
+    std::swap(cur, nxt);
+  }
+  launch_or_throw(launch_partial_sums(cur, size_t(rows) * dim_, partials_,
+                                      stream_),
+                  "partial sums");
+}
+
+void Engine::prepare(int rows) {
+  if (closed_) throw std::runtime_error("engine closed");
+  if (rows < 1 || rows > max_rows_) {
+    throw std::invalid_argument("rows out of range for this engine");
+  }
+  if (graphs_.count(rows)) return;
+  if (graphs_.size() >= 16) {
+    auto victim = graphs_.begin();
+    hipGraphExecDestroy(victim->second.second);
+    hipGraphDestroy(victim->second.first);
+    graphs_.erase(victim);
+  }
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  check_hip(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal),
+            "begin capture");
+  try {
+    enqueue_forward(rows);
+  } catch (...) {
+    hipStreamEndCapture(stream_, &graph);
+    if (graph) hipGraphDestroy(graph);
+    throw;
+  }
+  check_hip(hipStreamEndCapture(stream_, &graph), "end capture");
+  check_hip(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0),
+            "graph instantiate");
+  graphs_[rows] = std::make_pair(graph, exec);
+  stage("graph_ready");
+}
+
+ForwardResult Engine::forward(int rows, int passes, unsigned long long seed) {
+  if (closed_) throw std::runtime_error("engine closed");
+  if (rows < 1 || rows > max_rows_) {
+    throw std::invalid_argument("rows exceeds the engine's max_rows");
+  }
+  ForwardResult r;
+  r.rows = rows;
+  r.passes = std::max(1, passes);
+  const long long t0 = monotonic_ns();
+  prepare(rows);
+  auto exec = graphs_[rows].second;
+  *seed_host_ = seed;
+  check_hip(hipMemcpyAsync(seed_dev_, seed_host_, 8, hipMemcpyHostToDevice,
+                           stream_),
+            "seed upload");
+  check_hip(hipEventRecord(ev0_, stream_), "event");
+  for (int p = 0; p < r.passes; ++p) {
+    check_hip(hipGraphLaunch(exec, stream_), "graph launch");
+  }
+  check_hip(hipEventRecord(ev1_, stream_), "event");
+  check_hip(hipMemcpyAsync(partials_host_, partials_, kSumBlocks * 4,
+                           hipMemcpyDeviceToHost, stream_),
+            "partials download");
+  check_hip(hipStreamSynchronize(stream_), "forward sync");
+  float ms = 0;
+  hipEventElapsedTime(&ms, ev0_, ev1_);
+  double sum = 0;
+  for (int b = 0; b < kSumBlocks; ++b) sum += partials_host_[b];
+  r.checksum = sum;
+  r.gpu_ms = ms;
+  r.ms = (monotonic_ns() - t0) / 1e6;
+  r.graph = true;
+  return r;
+}
+
+std::map<std::string, double> Engine::info() const {
+  std::map<std::string, double> out;
+  size_t free_b = 0, total_b = 0;
+  hipMemGetInfo(&free_b, &total_b);
+  out["cu_count"] = cu_count_;
+  out["hbm_free_bytes"] = static_cast<double>(free_b);
+  out["hbm_total_bytes"] = static_cast<double>(total_b);
+  out["arena_bytes"] = static_cast<double>(arena_bytes_);
+  out["graphs"] = static_cast<double>(graphs_.size());
+  int clock_khz = 0;
+  hipDeviceGetAttribute(&clock_khz, hipDeviceAttributeClockRate, device_);
+  out["clock_khz"] = clock_khz;
+  return out;
+}
+
+unsigned long long Engine::weight_ptr(int layer, int which) const {
+  if (layer < 0 || layer >= layers_) throw std::out_of_range("layer");
+  switch (which) {
+    case 0: return reinterpret_cast<unsigned long long>(w1_[layer]);
+    case 1: return reinterpret_cast<unsigned long long>(b1_[layer]);
+    case 2: return reinterpret_cast<unsigned long long>(w2_[layer]);
+    case 3: return reinterpret_cast<unsigned long long>(b2_[layer]);
+    default: throw std::out_of_range("which");
+  }
+}
+
+unsigned long long Engine::act_ptr(int which) const {
+  switch (which) {
+    case 0: return reinterpret_cast<unsigned long long>(x_);
+    case 1: return reinterpret_cast<unsigned long long>(y_);
+    case 2: return reinterpret_cast<unsigned long long>(h_);
+    default: throw std::out_of_range("which");
+  }
+}
+
+}  // namespace kiosk

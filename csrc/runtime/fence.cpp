@@ -1,0 +1,270 @@
+// RCCL membership fence (see fence.hpp).
+#include "fence.hpp"
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <thread>
+
+#include "engine.hpp"
+
+namespace kiosk {
+
+struct RcclApi {
+  void* handle = nullptr;
+  std::string path;
+  decltype(&::ncclGetVersion) GetVersion = nullptr;
+  decltype(&::ncclGetUniqueId) GetUniqueId = nullptr;
+  decltype(&::ncclCommInitRankConfig) CommInitRankConfig = nullptr;
+  decltype(&::ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+  decltype(&::ncclCommAbort) CommAbort = nullptr;
+  decltype(&::ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&::ncclCommFinalize) CommFinalize = nullptr;
+  decltype(&::ncclAllReduce) AllReduce = nullptr;
+  decltype(&::ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&::ncclCommShrink) CommShrink = nullptr;   // optional
+};
+
+namespace {
+
+template <typename T>
+void bind(void* handle, const char* name, T& slot, bool required) {
+  slot = reinterpret_cast<T>(dlsym(handle, name));
+  if (!slot && required) {
+    throw std::runtime_error(std::string("RCCL symbol missing: ") + name);
+  }
+}
+
+RcclApi* load_rccl() {
+  std::vector<std::string> candidates;
+  if (const char* env = std::getenv("KIOSK_RCCL_LIB")) candidates.push_back(env);
+  candidates.push_back("/opt/rocm/lib/librccl.so.1");
+  candidates.push_back("librccl.so.1");
+  std::string errors;
+  for (const auto& path : candidates) {
+    void* handle = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!handle) {
+      const char* e = dlerror();
+      errors += path + ": " + (e ? e : "?") + "; ";
+      continue;
+    }
+    auto* api = new RcclApi();
+    api->handle = handle;
+    api->path = path;
+    try {
+      bind(handle, "ncclGetVersion", api->GetVersion, true);
+      bind(handle, "ncclGetUniqueId", api->GetUniqueId, true);
+      bind(handle, "ncclCommInitRankConfig", api->CommInitRankConfig, true);
+      bind(handle, "ncclCommGetAsyncError", api->CommGetAsyncError, true);
+      bind(handle, "ncclCommAbort", api->CommAbort, true);
+      bind(handle, "ncclCommDestroy", api->CommDestroy, true);
+      bind(handle, "ncclCommFinalize", api->CommFinalize, true);
+      bind(handle, "ncclAllReduce", api->AllReduce, true);
+      bind(handle, "ncclGetErrorString", api->GetErrorString, true);
+      bind(handle, "ncclCommShrink", api->CommShrink, false);
+    } catch (const std::exception& e) {
+      errors += path + ": " + e.what() + "; ";
+      delete api;
+      continue;
+    }
+    return api;
+  }
+  throw std::runtime_error("no usable RCCL library: " + errors);
+}
+
+std::once_flag g_once;
+RcclApi* g_api = nullptr;
+std::string g_error;
+
+void check_nccl(ncclResult_t res, const char* what) {
+  if (res != ncclSuccess && res != ncclInProgress) {
+    throw std::runtime_error(std::string(what) + ": " +
+                             rccl().GetErrorString(res));
+  }
+}
+
+double now_s() {
+  return std::chrono::duration<double>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+}  // namespace
+
+const RcclApi& rccl() {
+  std::call_once(g_once, [] {
+    try {
+      g_api = load_rccl();
+    } catch (const std::exception& e) {
+      g_error = e.what();
+    }
+  });
+  if (!g_api) throw std::runtime_error(g_error);
+  return *g_api;
+}
+
+std::string rccl_library() { return rccl().path; }
+
+int rccl_version() {
+  int v = 0;
+  check_nccl(rccl().GetVersion(&v), "ncclGetVersion");
+  return v;
+}
+
+bool rccl_can_shrink() { return rccl().CommShrink != nullptr; }
+
+std::string rccl_unique_id() {
+  ncclUniqueId id;
+  check_nccl(rccl().GetUniqueId(&id), "ncclGetUniqueId");
+  return std::string(id.internal, sizeof(id.internal));
+}
+
+void Fence::wait_ready(void* comm, double timeout_s, const char* what) {
+  const double deadline = now_s() + timeout_s;
+  while (true) {
+    ncclResult_t state = ncclSuccess;
+    ncclResult_t res = rccl().CommGetAsyncError(
+        static_cast<ncclComm_t>(comm), &state);
+    if (res != ncclSuccess) state = res;
+    if (state == ncclSuccess) return;
+    if (state != ncclInProgress) {
+      rccl().CommAbort(static_cast<ncclComm_t>(comm));
+      throw std::runtime_error(std::string(what) + " failed: " +
+                               rccl().GetErrorString(state));
+    }
+    if (now_s() > deadline) {
+      rccl().CommAbort(static_cast<ncclComm_t>(comm));
+      throw std::runtime_error(std::string(what) + " timed out");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+Fence::Fence(const std::string& unique_id, int nranks, int rank,
+             double timeout_s)
+    : nranks_(nranks), rank_(rank), timeout_s_(timeout_s) {
+  if (unique_id.size() != sizeof(ncclUniqueId)) {
+    throw std::invalid_argument("unique id must be 128 bytes");
+  }
+  if (nranks < 1 || rank < 0 || rank >= nranks) {
+    throw std::invalid_argument("bad rank / nranks");
+  }
+  const RcclApi& api = rccl();
+  check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking),
+            "fence stream");
+  check_hip(hipMalloc(reinterpret_cast<void**>(&dev_), 128 * sizeof(long long)),
+            "fence buffers");
+  check_hip(hipHostMalloc(reinterpret_cast<void**>(&host_),
+                          64 * sizeof(long long)),
+            "fence pinned");
+  ncclUniqueId id;
+  std::memcpy(id.internal, unique_id.data(), sizeof(id.internal));
+  ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+  config.blocking = 0;   // init must be abortable on timeout
+  ncclComm_t comm = nullptr;
+  check_nccl(api.CommInitRankConfig(&comm, nranks, id, rank, &config),
+             "ncclCommInitRankConfig");
+  comm_ = comm;
+  wait_ready(comm_, timeout_s, "ncclCommInitRank");
+}
+
+Fence::~Fence() {
+  try {
+    destroy();
+  } catch (...) {
+  }
+}
+
+std::pair<std::vector<long long>, double> Fence::allreduce(
+    const std::vector<long long>& values) {
+  if (!comm_) throw std::runtime_error("fence communicator is closed");
+  if (values.empty() || values.size() > 64) {
+    throw std::invalid_argument("fence vector must have 1..64 entries");
+  }
+  const size_t n = values.size();
+  const double t0 = now_s();
+  std::memcpy(host_, values.data(), n * sizeof(long long));
+  check_hip(hipMemcpyAsync(dev_, host_, n * sizeof(long long),
+                           hipMemcpyHostToDevice, stream_),
+            "fence upload");
+  check_nccl(rccl().AllReduce(dev_, dev_ + 64, n, ncclInt64, ncclSum,
+                              static_cast<ncclComm_t>(comm_), stream_),
+             "ncclAllReduce");
+  wait_ready(comm_, timeout_s_, "ncclAllReduce enqueue");
+  check_hip(hipMemcpyAsync(host_, dev_ + 64, n * sizeof(long long),
+                           hipMemcpyDeviceToHost, stream_),
+            "fence download");
+  // bounded wait: a dead peer must not hang the worker forever
+  const double deadline = now_s() + timeout_s_;
+  while (hipStreamQuery(stream_) == hipErrorNotReady) {
+    if (now_s() > deadline) {
+      abort();
+      throw std::runtime_error("fence all-reduce timed out");
+    }
+    std::this_thread::yield();
+  }
+  check_hip(hipStreamSynchronize(stream_), "fence sync");
+  std::vector<long long> out(host_, host_ + n);
+  return {out, (now_s() - t0) * 1e6};
+}
+
+void Fence::shrink(const std::vector<int>& excluded, double timeout_s) {
+  if (!comm_) throw std::runtime_error("fence communicator is closed");
+  if (!rccl().CommShrink) {
+    throw std::runtime_error("this RCCL has no ncclCommShrink");
+  }
+  std::vector<int> ex(excluded);
+  ncclComm_t next = nullptr;
+  check_nccl(rccl().CommShrink(static_cast<ncclComm_t>(comm_), ex.data(),
+                               static_cast<int>(ex.size()), &next, nullptr,
+                               NCCL_SHRINK_DEFAULT),
+             "ncclCommShrink");
+  wait_ready(next, timeout_s, "ncclCommShrink");
+  void* old = comm_;
+  comm_ = next;
+  int below = 0;
+  for (int r : excluded) below += (r < rank_);
+  rank_ -= below;
+  nranks_ -= static_cast<int>(excluded.size());
+  rccl().CommDestroy(static_cast<ncclComm_t>(old));
+}
+
+void Fence::abort() {
+  if (comm_) {
+    rccl().CommAbort(static_cast<ncclComm_t>(comm_));
+    comm_ = nullptr;
+  }
+}
+
+void Fence::destroy() {
+  if (comm_) {
+    rccl().CommFinalize(static_cast<ncclComm_t>(comm_));
+    try {
+      wait_ready(comm_, timeout_s_, "ncclCommFinalize");
+    } catch (...) {
+      comm_ = nullptr;   // already aborted by wait_ready
+    }
+    if (comm_) rccl().CommDestroy(static_cast<ncclComm_t>(comm_));
+    comm_ = nullptr;
+  }
+  if (stream_) {
+    hipStreamSynchronize(stream_);
+    hipStreamDestroy(stream_);
+    stream_ = nullptr;
+  }
+  if (dev_) {
+    hipFree(dev_);
+    dev_ = nullptr;
+  }
+  if (host_) {
+    hipHostFree(host_);
+    host_ = nullptr;
+  }
+}
+
+}  // namespace kiosk

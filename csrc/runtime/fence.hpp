@@ -1,0 +1,54 @@
+// RCCL membership fence.  RCCL is dlopen'ed, not linked:
+// PyTorch-ROCm ships an older RCCL without ncclCommShrink and loads it into
+// every process that imports torch; binding our own symbols through an
+// RTLD_LOCAL handle of ROCm's RCCL 2.27 keeps the two apart while sharing
+// the one HIP runtime.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace kiosk {
+
+struct RcclApi;
+const RcclApi& rccl();            // throws if no usable RCCL is found
+std::string rccl_library();       // path actually loaded
+int rccl_version();
+bool rccl_can_shrink();
+std::string rccl_unique_id();     // 128 raw bytes
+
+class Fence {
+ public:
+  // Collective: every rank calls it with the same id and nranks.
+  Fence(const std::string& unique_id, int nranks, int rank, double timeout_s);
+  ~Fence();
+  Fence(const Fence&) = delete;
+  Fence& operator=(const Fence&) = delete;
+
+  // Sum-all-reduce of small int64 vectors (the 72-B membership vector).
+  // Returns the result and the host-observed latency in microseconds.
+  std::pair<std::vector<long long>, double> allreduce(
+      const std::vector<long long>& values);
+  // Collective over the surviving ranks: drop `excluded` (old rank ids).
+  void shrink(const std::vector<int>& excluded, double timeout_s);
+  void destroy();
+  void abort();
+  int nranks() const { return nranks_; }
+  int rank() const { return rank_; }
+
+ private:
+  void wait_ready(void* comm, double timeout_s, const char* what);
+
+  void* comm_ = nullptr;        // ncclComm_t
+  hipStream_t stream_ = nullptr;
+  long long* dev_ = nullptr;    // send [64] + recv [64]
+  long long* host_ = nullptr;   // pinned [64]
+  int nranks_ = 0;
+  int rank_ = 0;
+  double timeout_s_ = 60.0;
+};
+
+}  // namespace kiosk

@@ -1,0 +1,124 @@
+"""torch-tensor front end for the native gfx950 kernels.
+
+Every function here launches a hand-written HIP kernel from ``_kiosk_hip``
+on the current PyTorch stream; none falls back to a PyTorch op.  The
+``reference_*`` helpers are the plain fp32 PyTorch references the numerics
+tests compare against.
+"""
+import math
+
+from . import native
+
+EPILOGUES = {'none': 0, 'gelu': 1, 'bias_gelu': 1, 'residual': 2,
+             'bias_residual': 2}
+
+
+def _stream():
+    import torch
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check_bf16(t, name):
+    import torch
+    if t.dtype != torch.bfloat16 or not t.is_cuda or not t.is_contiguous():
+        raise ValueError('%s must be a contiguous bf16 CUDA tensor' % name)
+
+
+def gemm(a, b, bias=None, residual=None, epilogue='none', out=None):
+    """``epi(a @ b.T)`` with a: [M, K], b: [N, K] (bf16) -> [M, N] bf16.
+
+    ``epilogue``: ``'none'``, ``'gelu'`` (``gelu_tanh(a@b.T + bias)``) or
+    ``'residual'`` (``a@b.T + bias + residual``)."""
+    import torch
+    mod = native.load()
+    _check_bf16(a, 'a')
+    _check_bf16(b, 'b')
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2:
+        raise ValueError('inner dimensions differ: %d vs %d' % (K, K2))
+    if not mod.gemm_shape_ok(M, N, K):
+        raise ValueError('unsupported GEMM shape M=%d N=%d K=%d (need N %% 128'
+                         ' == 0, K %% 64 == 0)' % (M, N, K))
+    epi = EPILOGUES[epilogue]
+    if epi and (bias is None or bias.dtype != torch.float32
+                or bias.numel() != N or not bias.is_contiguous()):
+        raise ValueError('epilogue %r needs an fp32 bias of %d' % (epilogue, N))
+    if epi == 2:
+        _check_bf16(residual, 'residual')
+        if tuple(residual.shape) != (M, N):
+            raise ValueError('residual must be [M, N]')
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    mod.gemm(a.data_ptr(), b.data_ptr(), out.data_ptr(),
+             bias.data_ptr() if bias is not None else 0,
+             residual.data_ptr() if residual is not None else 0,
+             M, N, K, epi, _stream())
+    return out
+
+
+def init_uniform_(t, seed, lo=-1.0, hi=1.0):
+    """Fill a bf16 or fp32 CUDA tensor with the on-device generator."""
+    import torch
+    mod = native.load()
+    if not t.is_contiguous() or not t.is_cuda:
+        raise ValueError('tensor must be contiguous on the GPU')
+    if t.dtype == torch.bfloat16:
+        mod.init_uniform_bf16(t.data_ptr(), t.numel(), int(seed), lo, hi,
+                              _stream())
+    elif t.dtype == torch.float32:
+        mod.init_uniform_f32(t.data_ptr(), t.numel(), int(seed), lo, hi,
+                             _stream())
+    else:
+        raise ValueError('init_uniform_ supports bf16 / fp32')
+    return t
+
+
+def checksum(t):
+    """fp32 sum of a bf16 tensor via the deterministic partial-sum kernel."""
+    import torch
+    mod = native.load()
+    _check_bf16(t, 't')
+    partials = torch.empty(mod.sum_blocks, dtype=torch.float32,
+                           device=t.device)
+    mod.partial_sums(t.data_ptr(), t.numel(), partials.data_ptr(), _stream())
+    return float(partials.double().sum().item())
+
+
+def model_weights(dim, hidden, layers, seed, device='cuda'):
+    """Regenerate the Engine's weights (same seeds and bounds) as tensors."""
+    import torch
+    bd, bh = 1.0 / math.sqrt(dim), 1.0 / math.sqrt(hidden)
+    weights = []
+    for layer in range(layers):
+        s = seed * 1000003 + 16 * layer
+        w1 = torch.empty((hidden, dim), dtype=torch.bfloat16, device=device)
+        b1 = torch.empty(hidden, dtype=torch.float32, device=device)
+        w2 = torch.empty((dim, hidden), dtype=torch.bfloat16, device=device)
+        b2 = torch.empty(dim, dtype=torch.float32, device=device)
+        init_uniform_(w1, s + 1, -bd, bd)
+        init_uniform_(b1, s + 2, -bd, bd)
+        init_uniform_(w2, s + 3, -bh, bh)
+        init_uniform_(b2, s + 4, -bh, bh)
+        weights.append((w1, b1, w2, b2))
+    return weights
+
+
+def reference_forward(x, weights):
+    """fp32 PyTorch reference of the worker model with the kernels' bf16
+    storage points (hidden activation and every layer output)."""
+    import torch
+    from ..models.mlp import torch_reference
+    for w1, b1, w2, b2 in weights:
+        x = torch_reference(x, w1, b1, w2, b2).to(torch.bfloat16)
+    return x
+
+
+def reference_forward_checksum(dim, hidden, layers, rows, model_seed,
+                               input_seed):
+    import torch
+    weights = model_weights(dim, hidden, layers, model_seed)
+    x = torch.empty((rows, dim), dtype=torch.bfloat16, device='cuda')
+    init_uniform_(x, input_seed, -1.0, 1.0)
+    y = reference_forward(x, weights)
+    return float(y.double().sum().item())

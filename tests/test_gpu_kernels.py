@@ -1,0 +1,161 @@
+"""Numerics of the gfx950 kernels against plain PyTorch fp32 references.
+
+Runs on an MI355X only (``-m gpu``); every kernel call goes through the
+native extension (there is no PyTorch fallback to pass silently)."""
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def mod():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from kiosk_autoscaler_amd.ops import native
+    return native.load()
+
+
+def rand_bf16(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device='cuda').manual_seed(seed)
+    return ((torch.rand(*shape, generator=g, device='cuda') * 2 - 1)
+            * scale).to(torch.bfloat16)
+
+
+def gelu_tanh(x):
+    return 0.5 * x * (1 + torch.tanh(0.7978845608028654 *
+                                     (x + 0.044715 * x ** 3)))
+
+
+@pytest.mark.parametrize('M,N,K', [(128, 128, 64), (256, 384, 512),
+                                   (100, 256, 192), (1, 128, 64),
+                                   (2048, 1024, 4096)])
+def test_gemm_plain(mod, M, N, K):
+    from kiosk_autoscaler_amd.ops import kernels
+    a = rand_bf16(M, K, seed=1)
+    b = rand_bf16(N, K, seed=2)
+    c = kernels.gemm(a, b)
+    ref = a.float() @ b.float().t()
+    err = (c.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
+
+
+def test_gemm_identity_asymmetric(mod):
+    """A = I with an asymmetric B catches a transposed C-write exactly."""
+    from kiosk_autoscaler_amd.ops import kernels
+    M = K = 256
+    N = 384
+    a = torch.eye(M, K, device='cuda', dtype=torch.bfloat16)
+    b = (torch.arange(N * K, device='cuda', dtype=torch.float32)
+         .reshape(N, K) % 251 - 125).to(torch.bfloat16)
+    c = kernels.gemm(a, b)
+    assert torch.equal(c, b.t().contiguous()[:M])
+
+
+def test_gemm_bias_gelu(mod):
+    from kiosk_autoscaler_amd.ops import kernels
+    M, N, K = 192, 512, 256
+    a, b = rand_bf16(M, K, seed=3), rand_bf16(N, K, scale=0.1, seed=4)
+    bias = torch.randn(N, device='cuda')
+    c = kernels.gemm(a, b, bias=bias, epilogue='gelu')
+    ref = gelu_tanh(a.float() @ b.float().t() + bias)
+    torch.testing.assert_close(c.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_gemm_bias_residual(mod):
+    from kiosk_autoscaler_amd.ops import kernels
+    M, N, K = 130, 256, 512
+    a, b = rand_bf16(M, K, seed=5), rand_bf16(N, K, scale=0.05, seed=6)
+    bias = torch.randn(N, device='cuda')
+    res = rand_bf16(M, N, seed=7)
+    c = kernels.gemm(a, b, bias=bias, residual=res, epilogue='residual')
+    ref = a.float() @ b.float().t() + bias + res.float()
+    torch.testing.assert_close(c.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+def test_gemm_rejects_bad_shapes(mod):
+    from kiosk_autoscaler_amd.ops import kernels
+    with pytest.raises(ValueError):
+        kernels.gemm(rand_bf16(64, 64), rand_bf16(100, 64))
+
+
+def test_init_uniform_and_checksum(mod):
+    from kiosk_autoscaler_amd.ops import kernels
+    t = torch.empty(1 << 20, device='cuda', dtype=torch.bfloat16)
+    kernels.init_uniform_(t, 42, -0.5, 0.5)
+    f = t.float()
+    assert f.min().item() >= -0.5 and f.max().item() <= 0.5
+    assert abs(f.mean().item()) < 5e-3
+    assert abs(f.std().item() - 1 / (12 ** 0.5)) < 5e-3
+    u = torch.empty_like(t)
+    kernels.init_uniform_(u, 42, -0.5, 0.5)
+    assert torch.equal(t, u)                        # reproducible
+    kernels.init_uniform_(u, 43, -0.5, 0.5)
+    assert not torch.equal(t, u)
+    assert abs(kernels.checksum(t) - f.double().sum().item()) < 1e-2
+    odd = torch.empty(1001, device='cuda', dtype=torch.bfloat16)
+    kernels.init_uniform_(odd, 1)
+    assert abs(kernels.checksum(odd) - odd.double().sum().item()) < 1e-3
+
+
+def test_engine_matches_reference(mod):
+    from kiosk_autoscaler_amd.ops import kernels
+    dim, hidden, layers, rows = 256, 1024, 3, 200
+    engine = mod.Engine(0, dim, hidden, layers, 256, 5)
+    try:
+        out = engine.forward(rows, 1, 99)
+        ref = kernels.reference_forward_checksum(dim, hidden, layers, rows, 5,
+                                                 99)
+        assert abs(out['checksum'] - ref) <= 1e-2 * max(1.0, abs(ref)), \
+            (out, ref)
+        again = engine.forward(rows, 2, 99)        # graph replay, same input
+        assert again['graph'] and again['passes'] == 2
+        assert abs(again['checksum'] - out['checksum']) < 1e-6
+        other = engine.forward(rows, 1, 100)
+        assert other['checksum'] != out['checksum']
+        stages = engine.stage_times()
+        assert list(stages)[:2] == ['engine_enter', 'hip_context']
+    finally:
+        engine.close()
+
+
+def test_warmstart_touches_every_cu(mod):
+    engine = mod.Engine(0, 256, 512, 1, 64, 1)
+    try:
+        info = engine.warmstart(512)
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        assert info['blocks'] == cus
+        assert info['cus_touched'] == cus, info['cus_touched']
+        assert info['xccs_touched'] == 8
+        assert info['kernel_us'] > 0 and info['span_us'] > 0
+    finally:
+        engine.close()
+
+
+def test_fence_world_size_one(mod):
+    uid = mod.fence_unique_id()
+    assert len(uid) == 128
+    fence = mod.Fence(uid, 1, 0, 30.0)
+    try:
+        vec = [7, 0, 1, 0, 0, 0, 0, 0, 0]
+        out, us = fence.allreduce(vec)
+        assert out == vec and us > 0
+    finally:
+        fence.destroy()
+
+
+def test_fence_agent_rccl_transport(mod):
+    from kiosk_autoscaler_amd.fakes import FakeRedis
+    from kiosk_autoscaler_amd.parallel import FenceAgent, RcclTransport
+    transport = RcclTransport(FakeRedis(), 'ns/w', timeout=30.0, native=mod)
+    agent = FenceAgent('w-g0-0', 0, transport)
+    try:
+        r1 = agent.run_epoch({'epoch': 1, 'members': ['w-g0-0'],
+                              'slots': [0]})
+        assert r1['ok'] and r1['mode'] == 'init'
+        r2 = agent.run_epoch({'epoch': 2, 'members': ['w-g0-0'],
+                              'slots': [0], 'previous': ['w-g0-0']})
+        assert r2['ok'] and r2['mode'] == 'reuse'
+    finally:
+        agent.close()

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""GEMM microbenchmark: native gfx950 kernel vs torch.matmul (hipBLASLt).
+
+Interleaves the two in one process (cdna_hip_programming.md rule 24) on
+random data (rule 25) at the worker's shapes and prints one JSON line per
+shape with TFLOP/s for each.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    from kiosk_autoscaler_amd.ops import kernels
+    parser = argparse.ArgumentParser()
+    parser.add_argument('--iters', type=int, default=20)
+    parser.add_argument('--rounds', type=int, default=5)
+    parser.add_argument('--shapes', default='2048x16384x4096,2048x4096x16384,'
+                        '8192x16384x4096,4096x4096x4096')
+    args = parser.parse_args()
+    for spec in args.shapes.split(','):
+        M, N, K = (int(v) for v in spec.split('x'))
+        a = (torch.rand(M, K, device='cuda') * 2 - 1).to(torch.bfloat16)
+        b = ((torch.rand(N, K, device='cuda') * 2 - 1) * 0.05).to(torch.bfloat16)
+        bias = torch.randn(N, device='cuda')
+        out = torch.empty(M, N, device='cuda', dtype=torch.bfloat16)
+
+        def ours():
+            kernels.gemm(a, b, bias=bias, epilogue='gelu', out=out)
+
+        def ours_plain():
+            kernels.gemm(a, b, out=out)
+
+        def theirs():
+            torch.nn.functional.gelu(torch.addmm(bias.to(torch.bfloat16), a,
+                                                 b.t()), approximate='tanh')
+
+        def theirs_plain():
+            torch.matmul(a, b.t(), out=out)
+
+        fns = {'native_gelu': ours, 'native': ours_plain,
+               'torch_gelu': theirs, 'torch': theirs_plain}
+        results = {k: [] for k in fns}
+        for fn in fns.values():
+            fn()
+        torch.cuda.synchronize()
+        for _ in range(args.rounds):
+            for name, fn in fns.items():
+                start = torch.cuda.Event(enable_timing=True)
+                end = torch.cuda.Event(enable_timing=True)
+                start.record()
+                for _ in range(args.iters):
+                    fn()
+                end.record()
+                end.synchronize()
+                ms = start.elapsed_time(end) / args.iters
+                results[name].append(2.0 * M * N * K / (ms * 1e-3) / 1e12)
+        ref = (a.float() @ b.float().t())
+        ours_plain()
+        torch.cuda.synchronize()
+        err = (out.float() - ref).abs().max().item()
+        summary = {'shape': [M, N, K], 'max_abs_err': err}
+        for name, vals in results.items():
+            vals.sort()
+            summary[name + '_tflops_median'] = round(vals[len(vals) // 2], 1)
+            summary[name + '_tflops_max'] = round(vals[-1], 1)
+        print(json.dumps(summary), flush=True)
+
+
+if __name__ == '__main__':
+    main()

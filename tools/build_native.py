@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""Build every native component in-tree (no JIT cache, no pip install).
+
+* ``kiosk_autoscaler_amd/ops/_kiosk_hip<ext>`` -- gfx950 kernels
+  (csrc/kernels/*.hip) + runtime (csrc/runtime/*.cpp: engine, RCCL fence,
+  pybind11 bindings), compiled with ``hipcc --offload-arch=gfx950`` and
+  linked ``-shared -fPIC``.  RCCL is dlopen'ed at run time (see fence.hpp).
+* ``build/kredis-server`` -- the native RESP server (csrc/kredis), g++.
+
+Objects are cached by source mtime under ``build/obj``; ``--clean`` rebuilds.
+"""
+import argparse
+import concurrent.futures
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD = os.path.join(ROOT, 'build')
+OBJ = os.path.join(BUILD, 'obj')
+ARCH = os.environ.get('KIOSK_OFFLOAD_ARCH', 'gfx950')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+EXT = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
+EXT_PATH = os.path.join(ROOT, 'kiosk_autoscaler_amd', 'ops', '_kiosk_hip' + EXT)
+KREDIS = os.path.join(BUILD, 'kredis-server')
+
+
+def _includes():
+    import pybind11
+    return ['-I' + pybind11.get_include(),
+            '-I' + sysconfig.get_paths()['include'],
+            '-I' + os.path.join(ROOT, 'csrc')]
+
+
+def _headers(directory):
+    out = []
+    for base, _, files in os.walk(directory):
+        out += [os.path.join(base, f) for f in files
+                if f.endswith(('.hpp', '.h'))]
+    return out
+
+
+def _stale(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(' '.join(cmd), flush=True)
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                          text=True)
+    if proc.returncode != 0:
+        sys.stderr.write(proc.stdout)
+        raise RuntimeError('command failed: %s' % ' '.join(cmd[:3]))
+    return proc.stdout
+
+
+def compile_units(verbose=False, jobs=4):
+    os.makedirs(OBJ, exist_ok=True)
+    headers = _headers(os.path.join(ROOT, 'csrc'))
+    units = []
+    for sub in ('kernels', 'runtime'):
+        d = os.path.join(ROOT, 'csrc', sub)
+        for name in sorted(os.listdir(d)):
+            if name.endswith(('.hip', '.cpp')):
+                units.append(os.path.join(d, name))
+    flags = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH,
+             '-Wall', '-Wno-unused-result', '-Wno-unused-function',
+             '-fvisibility=hidden'] + _includes()
+    jobs_list = []
+    for src in units:
+        obj = os.path.join(OBJ, os.path.basename(src) + '.o')
+        if _stale(obj, [src] + headers):
+            cmd = [HIPCC] + flags + ['-c', src, '-o', obj]
+            if src.endswith('.cpp'):
+                cmd = [HIPCC] + flags + ['-x', 'hip', '-c', src, '-o', obj]
+            jobs_list.append(cmd)
+        units_obj = obj
+        del units_obj
+    with concurrent.futures.ThreadPoolExecutor(max_workers=jobs) as pool:
+        list(pool.map(lambda c: _run(c, verbose), jobs_list))
+    return [os.path.join(OBJ, os.path.basename(s) + '.o') for s in units]
+
+
+def link_extension(objects, verbose=False):
+    if not _stale(EXT_PATH, objects):
+        return EXT_PATH
+    cmd = [HIPCC, '-shared', '-fPIC', '--offload-arch=' + ARCH] + objects + \
+        ['-o', EXT_PATH, '-ldl']
+    _run(cmd, verbose)
+    return EXT_PATH
+
+
+def build_kredis(verbose=False):
+    src_dir = os.path.join(ROOT, 'csrc', 'kredis')
+    if not os.path.isdir(src_dir):
+        return None
+    sources = [os.path.join(src_dir, f) for f in sorted(os.listdir(src_dir))
+               if f.endswith('.cpp')]
+    if not sources:
+        return None
+    os.makedirs(BUILD, exist_ok=True)
+    if _stale(KREDIS, sources + _headers(src_dir)):
+        cxx = shutil.which('g++') or 'c++'
+        _run([cxx, '-O2', '-std=c++17', '-Wall', '-pthread'] + sources +
+             ['-o', KREDIS], verbose)
+    return KREDIS
+
+
+def build(verbose=False, clean=False, jobs=4, kernels=True):
+    if clean and os.path.isdir(BUILD):
+        shutil.rmtree(BUILD)
+    out = {'kredis': build_kredis(verbose)}
+    if kernels:
+        objects = compile_units(verbose, jobs)
+        out['extension'] = link_extension(objects, verbose)
+    return out
+
+
+def main():
+    parser = argparse.ArgumentParser(description=__doc__)
+    parser.add_argument('-v', '--verbose', action='store_true')
+    parser.add_argument('--clean', action='store_true')
+    parser.add_argument('-j', '--jobs', type=int, default=4)
+    parser.add_argument('--no-kernels', action='store_true')
+    args = parser.parse_args()
+    out = build(args.verbose, args.clean, args.jobs, not args.no_kernels)
+    for key, value in out.items():
+        print('%s: %s' % (key, value))
+
+
+if __name__ == '__main__':
+    main()
