@@ -1,0 +1,182 @@
+"""Benchmark metrics from the lifecycle event stream.
+
+Definitions (shared with :mod:`.sim`):
+
+* **scale-up latency** = first key of an episode enqueued (no worker alive)
+  -> first worker READY (weights in HBM + warm-start kernel done);
+  decomposed into *decision* (enqueue -> the tick that scaled) and
+  *actuation* (that tick -> READY);
+* **first result** = first key enqueued -> that key's result written;
+* **GPU-idle %** = sum over workers of (alive - busy) / sum(alive); alive
+  spans GPU assignment -> process exit, busy is the union of key-in-flight
+  intervals (batched keys overlap).
+"""
+import collections
+
+
+def _mean(values):
+    values = [v for v in values if v is not None]
+    return sum(values) / len(values) if values else None
+
+
+def _pct(values, q):
+    values = sorted(v for v in values if v is not None)
+    if not values:
+        return None
+    idx = min(len(values) - 1, max(0, int(round(q * (len(values) - 1)))))
+    return values[idx]
+
+
+def _union_length(intervals):
+    total = 0
+    end = None
+    start = None
+    for a, b in sorted(intervals):
+        if end is None or a > end:
+            if end is not None:
+                total += end - start
+            start, end = a, b
+        else:
+            end = max(end, b)
+    if end is not None:
+        total += end - start
+    return total
+
+
+def cold_starts(events, keys, t_lo, t_hi):
+    """Every cold start in [t_lo, t_hi]: a key enqueued while no worker is
+    alive (assigned and not draining) -> the next worker READY.  Same
+    definition as :func:`kiosk_autoscaler_amd.bench.sim.simulate`."""
+    timeline = []
+    for e in events:
+        if e['ev'] in ('worker_assigned', 'worker_drain', 'worker_exit',
+                       'worker_ready'):
+            timeline.append((e['t'], e['ev'], e.get('worker')))
+    for _, _, t in keys:
+        timeline.append((t, 'key', None))
+    timeline.sort(key=lambda x: x[0])
+    alive = set()
+    drained = set()
+    pending = None
+    out = []
+    for t, kind, worker in timeline:
+        if kind == 'worker_assigned':
+            alive.add(worker)
+        elif kind in ('worker_drain', 'worker_exit'):
+            alive.discard(worker)
+            drained.add(worker)
+        elif kind == 'worker_ready':
+            if pending is not None and worker not in drained:
+                if t_lo <= pending <= t_hi:
+                    out.append((pending, t))
+                pending = None
+        elif kind == 'key' and not alive and pending is None:
+            pending = t
+    return out
+
+
+def episode_metrics(events, episode):
+    """Latency decomposition for one episode dict
+    (``t_first``, ``t_end``, ``keys``: [(item, queue, t_enq)])."""
+    t0, t_end = episode['t_first'], episode['t_end']
+    in_window = [e for e in events if t0 <= e.get('t', 0) <= t_end]
+    ready = sorted(e['t'] for e in in_window if e['ev'] == 'worker_ready')
+    scale = sorted(e['t'] for e in in_window
+                   if e['ev'] == 'scale' and e.get('desired', 0) >
+                   e.get('current', 0))
+    first_item = episode['keys'][0][0] if episode['keys'] else None
+    done = {e.get('item'): e['t'] for e in in_window if e['ev'] == 'key_done'}
+    start = {e.get('item'): e['t'] for e in in_window
+             if e['ev'] == 'key_start'}
+    waits = [(start[item] - t) / 1e9 for item, _, t in episode['keys']
+             if item in start]
+    colds = cold_starts(events, episode['keys'], t0, t_end)
+    out = {
+        'latency_s': (ready[0] - t0) / 1e9 if ready else None,
+        'cold_starts_s': [(b - a) / 1e9 for a, b in colds],
+        'decision_s': (scale[0] - t0) / 1e9 if scale else None,
+        'actuation_s': ((ready[0] - scale[0]) / 1e9
+                        if ready and scale and ready[0] >= scale[0] else None),
+        'first_result_s': ((done[first_item] - t0) / 1e9
+                           if first_item in done else None),
+        'all_ready_s': (ready[-1] - t0) / 1e9 if ready else None,
+        'workers_ready': len(ready),
+        'keys': len(episode['keys']),
+        'keys_done': sum(1 for item, _, _ in episode['keys'] if item in done),
+        'queue_wait_mean_s': _mean(waits),
+    }
+    readies = [e for e in in_window if e['ev'] == 'worker_ready']
+    if readies:
+        first = min(readies, key=lambda e: e['t'])
+        assigned = [e['t'] for e in in_window if e['ev'] == 'worker_assigned'
+                    and e.get('worker') == first.get('worker')]
+        stages = first.get('stages') or {}
+        base = assigned[0] if assigned else None
+        if base is not None:
+            out['stages_ms'] = {k: round((v - base) / 1e6, 3)
+                                for k, v in sorted(stages.items(),
+                                                   key=lambda kv: kv[1])}
+            out['from_pool'] = any(
+                e.get('from_pool') for e in in_window
+                if e['ev'] == 'worker_assigned'
+                and e.get('worker') == first.get('worker'))
+    return out
+
+
+def gpu_idle(events, t_lo, t_hi):
+    """GPU-idle % over workers assigned within [t_lo, t_hi]."""
+    assigned = {}
+    exited = {}
+    busy = collections.defaultdict(list)
+    starts = {}
+    for e in sorted(events, key=lambda e: e.get('t', 0)):
+        ev = e['ev']
+        worker = e.get('worker')
+        if ev == 'worker_assigned' and t_lo <= e['t'] <= t_hi:
+            assigned[worker] = e['t']
+        elif ev == 'worker_exit':
+            exited[worker] = e['t']
+        elif ev == 'key_start':
+            starts[(worker, e.get('item'))] = e['t']
+        elif ev == 'key_done':
+            begin = starts.pop((worker, e.get('item')), None)
+            if begin is not None:
+                busy[worker].append((begin, e['t']))
+    alive_total = busy_total = 0
+    for worker, t_a in assigned.items():
+        t_x = exited.get(worker, t_hi)
+        alive = max(0, t_x - t_a)
+        intervals = [(max(a, t_a), min(b, t_x)) for a, b in busy[worker]
+                     if b > t_a and a < t_x]
+        alive_total += alive
+        busy_total += _union_length(intervals)
+    if alive_total <= 0:
+        return None, 0.0, 0.0
+    return (100.0 * (alive_total - busy_total) / alive_total,
+            alive_total / 1e9, busy_total / 1e9)
+
+
+def summarize(events, episodes):
+    per = [episode_metrics(events, ep) for ep in episodes]
+    lat = [v for p in per for v in p['cold_starts_s']]
+    first = [p['latency_s'] for p in per]
+    idle, alive_s, busy_s = gpu_idle(
+        events, episodes[0]['t_first'] if episodes else 0,
+        episodes[-1]['t_end'] if episodes else 0)
+    return {
+        'latency_mean_s': _mean(lat),
+        'cold_starts': len(lat),
+        'first_key_latency_mean_s': _mean(first),
+        'latency_p50_s': _pct(lat, 0.5),
+        'latency_max_s': max([v for v in lat if v is not None], default=None),
+        'decision_mean_s': _mean([p['decision_s'] for p in per]),
+        'actuation_mean_s': _mean([p['actuation_s'] for p in per]),
+        'first_result_mean_s': _mean([p['first_result_s'] for p in per]),
+        'queue_wait_mean_s': _mean([p['queue_wait_mean_s'] for p in per]),
+        'gpu_idle_pct': idle,
+        'gpu_alive_s': alive_s,
+        'gpu_busy_s': busy_s,
+        'keys': sum(p['keys'] for p in per),
+        'keys_done': sum(p['keys_done'] for p in per),
+        'episodes': per,
+    }

@@ -1,0 +1,192 @@
+"""Discrete-event simulation of an INTERVAL-driven autoscaler.
+
+Reproduces the method behind BASELINE.md §3 (the only obtainable baseline:
+the reference publishes no numbers): the reference's decision logic
+(:func:`kiosk_autoscaler_amd.policy.decide`, bit-compatible ``reference``
+policy) drives an ideal actuator.  Workers become ready ``ready_delay``
+seconds after being declared, serve one key at a time for ``service_s``
+seconds (FIFO across queues), in-progress keys count in the tally (the
+``processing-<q>:*`` convention), and the loop period is
+``tick_s + interval`` (sleep-after, ``scale.py:94-103``).
+
+Metrics use the same definitions as the live benchmark
+(:mod:`kiosk_autoscaler_amd.bench.metrics`):
+
+* cold start = first key enqueued while no worker is ready *or declared*
+  -> first worker ready;
+* GPU-idle % = sum(alive - busy) / sum(alive) over workers, alive from
+  declaration to removal.
+"""
+import collections
+import math
+import random
+
+from .. import policy as policies
+
+
+def poisson_on_off(rate, on_s, off_s, duration_s, seed, queues=('predict',),
+                   start=0.0):
+    """Arrival times (and queue) of a Poisson on/off process."""
+    rng = random.Random(seed)
+    arrivals = []
+    period = on_s + off_s
+    t = start
+    end = start + duration_s
+    while t < end:
+        phase = (t - start) % period
+        if phase >= on_s:
+            t += period - phase
+            continue
+        gap = rng.expovariate(rate)
+        if phase + gap >= on_s:
+            t += period - phase   # the on-window closed before the next key
+            continue
+        t += gap
+        if t < end:
+            arrivals.append((t, rng.choice(list(queues))))
+    return arrivals
+
+
+class _Worker(object):
+    __slots__ = ('born', 'ready_at', 'busy_until', 'busy_total', 'removed',
+                 'current')
+
+    def __init__(self, born, ready_at):
+        self.born = born
+        self.ready_at = ready_at
+        self.busy_until = None
+        self.busy_total = 0.0
+        self.removed = None
+        self.current = None
+
+
+def simulate(arrivals, interval=5.0, service_s=1.0, ready_delay=0.0,
+             min_pods=0, max_pods=1, keys_per_pod=1, queues=('predict',),
+             policy='reference', tick_s=0.0, horizon=None, dt=0.01,
+             first_tick=0.0):
+    """Run the simulation; returns a metrics dict."""
+    queues = list(queues)
+    pending = {q: collections.deque() for q in queues}
+    arrivals = sorted(arrivals)
+    horizon = horizon if horizon is not None else (
+        (arrivals[-1][0] if arrivals else 0.0) + 300.0)
+    workers = []
+    next_arrival = 0
+    next_tick = first_tick
+    cold_starts = []
+    waits = []
+    cold_pending = None  # arrival time of the key that found no worker
+    t = 0.0
+    steps = int(math.ceil(horizon / dt))
+    for step in range(steps + 1):
+        t = step * dt
+        # arrivals
+        while next_arrival < len(arrivals) and arrivals[next_arrival][0] <= t:
+            at, q = arrivals[next_arrival]
+            pending[q].append(at)
+            live = [w for w in workers if w.removed is None]
+            if not live and cold_pending is None:
+                cold_pending = at
+            next_arrival += 1
+        # workers finish / pick up work
+        for w in workers:
+            if w.removed is not None or w.ready_at > t:
+                continue
+            if cold_pending is not None and w.ready_at <= t:
+                cold_starts.append(w.ready_at - cold_pending)
+                cold_pending = None
+            if w.busy_until is not None and w.busy_until <= t:
+                w.busy_until = None
+                w.current = None
+            if w.busy_until is None:
+                for q in queues:
+                    if pending[q]:
+                        at = pending[q].popleft()
+                        start = max(t, w.ready_at)
+                        waits.append(start - at)
+                        w.busy_until = start + service_s
+                        w.busy_total += service_s
+                        w.current = q
+                        break
+        # reconcile tick
+        if t >= next_tick:
+            keys = {q: len(pending[q]) for q in queues}
+            for w in workers:
+                if w.removed is None and w.current is not None:
+                    keys[w.current] += 1
+            live = [w for w in workers if w.removed is None]
+            current = len(live)
+            busy = sum(1 for w in live if w.current is not None)
+            desired = policies.decide(keys, min_pods, max_pods, keys_per_pod,
+                                      current, policy=policy, busy=busy)
+            if desired > current:
+                for _ in range(desired - current):
+                    workers.append(_Worker(t, t + ready_delay))
+            elif desired < current:
+                # remove idle / not-ready workers first, never busy ones
+                order = sorted(live, key=lambda w: (w.current is not None,
+                                                    -w.born))
+                for w in order[:current - desired]:
+                    if w.current is None:
+                        w.removed = t
+            next_tick = t + tick_s + interval
+        if (next_arrival >= len(arrivals) and not any(pending.values())
+                and all(w.removed is not None for w in workers)
+                and t > (arrivals[-1][0] if arrivals else 0)):
+            break
+    end = t
+    alive = busy = 0.0
+    for w in workers:
+        stop = w.removed if w.removed is not None else end
+        alive += stop - w.born
+        busy += min(w.busy_total, stop - w.born)
+    return {
+        'cold_start_mean_s': _mean(cold_starts),
+        'cold_start_max_s': max(cold_starts) if cold_starts else None,
+        'cold_starts': len(cold_starts),
+        'queue_wait_mean_s': _mean(waits),
+        'gpu_idle_pct': 100.0 * (alive - busy) / alive if alive else None,
+        'keys': len(arrivals),
+        'workers_started': len(workers),
+    }
+
+
+def _mean(values):
+    return sum(values) / len(values) if values else None
+
+
+def baseline_table(seeds=(0, 1, 2, 3, 4), duration=1200.0, on=60.0,
+                   off=60.0):
+    """Re-derive BASELINE.md §3 rows (means over seeds)."""
+    rows = [
+        ('predict MAX=1 lam=0.5', dict(queues=('predict',), max_pods=1),
+         0.5, {}),
+        ('predict MAX=8 KPP=1 lam=2', dict(queues=('predict',), max_pods=8),
+         2.0, {}),
+        ('predict,track MAX=8 KPP=1 lam=2',
+         dict(queues=('predict', 'track'), max_pods=8), 2.0, {}),
+        ('predict MAX=8 KPP=4 lam=2',
+         dict(queues=('predict',), max_pods=8, keys_per_pod=4), 2.0, {}),
+        ('predict MAX=8 lam=2 D=10', dict(queues=('predict',), max_pods=8,
+                                          ready_delay=10.0), 2.0, {}),
+        ('predict MAX=8 lam=2 INTERVAL=1', dict(queues=('predict',),
+                                                max_pods=8, interval=1.0),
+         2.0, {}),
+    ]
+    out = {}
+    for name, kwargs, lam, _ in rows:
+        results = []
+        for seed in seeds:
+            arrivals = poisson_on_off(lam, on, off, duration, seed,
+                                      kwargs.get('queues', ('predict',)))
+            results.append(simulate(arrivals, **kwargs))
+        out[name] = {key: _mean([r[key] for r in results
+                                 if r[key] is not None])
+                     for key in ('cold_start_mean_s', 'cold_start_max_s',
+                                 'queue_wait_mean_s', 'gpu_idle_pct')}
+    return out
+
+
+if __name__ == '__main__':
+    import json
+    print(json.dumps(baseline_table(), indent=1))

@@ -44,8 +44,11 @@ def build(settings=None, redis_client=None, actuator=None, events=None):
                                    port=settings.REDIS_PORT,
                                    backoff=settings.REDIS_INTERVAL)
     if events is None:
-        events = EventLog(path=settings.EVENT_LOG or None,
-                          source='autoscaler')
+        if settings.EVENT_LOG == 'redis':
+            events = EventLog(redis_client=redis_client, source='autoscaler')
+        else:
+            events = EventLog(path=settings.EVENT_LOG or None,
+                              source='autoscaler')
     manager = None
     if actuator is None:
         if settings.GPUMGR.startswith('unix:'):
@@ -70,7 +73,9 @@ def run_loop(scaler, settings, max_ticks=None, sleep=time.sleep,
     """The reconcile loop; returns after ``max_ticks`` (tests) or never."""
     ticks = 0
     next_tick = clock()
+    tick_key = getattr(settings, 'TICK_KEY', '')
     while max_ticks is None or ticks < max_ticks:
+        started = time.monotonic_ns()
         scaler.scale(namespace=settings.RESOURCE_NAMESPACE,
                      resource_type=settings.RESOURCE_TYPE,
                      name=settings.RESOURCE_NAME,
@@ -78,6 +83,10 @@ def run_loop(scaler, settings, max_ticks=None, sleep=time.sleep,
                      max_pods=settings.MAX_PODS,
                      keys_per_pod=settings.KEYS_PER_POD)
         gc.collect()
+        if tick_key:
+            # observability hook for the benchmark's phase control
+            scaler.redis_client.set(tick_key, '%d %d %d' % (
+                started, time.monotonic_ns(), ticks))
         ticks += 1
         if max_ticks is not None and ticks >= max_ticks:
             break

@@ -35,6 +35,15 @@ def cast_bool(value):
     raise ValueError('Invalid truth value: %r' % value)
 
 
+def number(value):
+    """``int`` like the reference (``'5'`` -> 5), but accepts fractional
+    values (``'0.5'``) so sub-second loops can be configured for tests."""
+    try:
+        return int(value)
+    except ValueError:
+        return float(value)
+
+
 def _find_upwards(start, names):
     path = os.path.abspath(start)
     while True:
@@ -119,7 +128,7 @@ REFERENCE_DEFAULTS = (
     ('REDIS_INTERVAL', int, 1),
     ('QUEUES', str, 'predict,track'),
     ('QUEUE_DELIMITER', str, ','),
-    ('INTERVAL', int, 5),
+    ('INTERVAL', number, 5),
     ('RESOURCE_NAMESPACE', str, 'default'),
     ('RESOURCE_TYPE', str, 'deployment'),
     ('RESOURCE_NAME', str, _MISSING),
@@ -146,7 +155,8 @@ EXTRA_DEFAULTS = (
     ('ROWS_PER_KEY', int, 2048),
     ('HBM_PER_KEY_BYTES', int, 0),          # 0 = derive from the model
     ('HBM_RESERVE_BYTES', int, 8 << 30),
-    ('EVENT_LOG', str, ''),                 # JSONL event path ('' = off)
+    ('EVENT_LOG', str, ''),                 # JSONL path | 'redis' | '' (off)
+    ('TICK_KEY', str, ''),                  # publish tick times to this key
     ('STATE_TTL', int, 3600),
     ('DEBUG', bool, True),
     ('LOG_FILE', str, 'autoscaler.log'),

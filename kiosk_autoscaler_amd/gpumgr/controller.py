@@ -50,6 +50,7 @@ logger = logging.getLogger('GpuManager')
 STARTING, READY, DRAINING, EXITED = 'starting', 'ready', 'draining', 'exited'
 ACTIVE_KEY = 'kiosk:active:{ns}:{name}'
 WORKER_KEY = 'kiosk:worker:{id}'
+POOL_KEY = 'kiosk:pool'
 
 
 class WorkerTemplate(object):
@@ -443,7 +444,17 @@ class GpuManager(object):
             return None
         proc = booted[0]
         self.standbys.remove(proc)
+        self._publish_pool()
         return proc
+
+    def _publish_pool(self):
+        if self.redis is None:
+            return
+        try:
+            self.redis.set(POOL_KEY, '%d %d' % (
+                sum(1 for p in self.standbys if p.booted), len(self.standbys)))
+        except Exception:  # pylint: disable=broad-except
+            pass
 
     def _on_standby_messages(self, proc):
         for message in proc.pipe.read_messages():
@@ -452,6 +463,7 @@ class GpuManager(object):
                 continue
             if message.get('ev') == 'standby':
                 proc.booted = True
+                self._publish_pool()
                 self.events.emit('standby_ready', pid=proc.pid,
                                  boot_s=(time.monotonic_ns() - proc.t_spawn)
                                  / 1e9)

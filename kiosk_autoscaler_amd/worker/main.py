@@ -17,6 +17,17 @@ import sys
 import time
 
 
+def _die_with_parent():
+    """PR_SET_PDEATHSIG: a worker must not outlive its manager."""
+    try:
+        import ctypes
+        import signal
+        libc = ctypes.CDLL(None, use_errno=True)
+        libc.prctl(1, int(signal.SIGTERM), 0, 0, 0)   # PR_SET_PDEATHSIG
+    except (OSError, AttributeError):
+        pass
+
+
 def _preload(backend):
     """Import everything heavy *without* touching the GPU."""
     t0 = time.monotonic_ns()
@@ -43,6 +54,7 @@ def main(argv=None):
     parser.add_argument('--backend', default='auto')
     parser.add_argument('--assign', default=None)
     args = parser.parse_args(argv)
+    _die_with_parent()
 
     logging.basicConfig(
         level=logging.INFO, stream=sys.stderr,
@@ -85,7 +97,8 @@ def main(argv=None):
 
     events = None
     if config.record_events:
-        events = EventLog(path=os.environ.get('EVENT_LOG') or None,
+        path = os.environ.get('EVENT_LOG') or None
+        events = EventLog(path=None if path == 'redis' else path,
                           redis_client=redis_factory(),
                           source=config.worker_id)
 
