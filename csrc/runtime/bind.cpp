@@ -124,6 +124,19 @@ PYBIND11_MODULE(_kiosk_hip, m) {
       py::arg("w"), py::arg("n"), py::arg("record"), py::arg("nblocks"),
       py::arg("iters"), py::arg("lds_bytes"), py::arg("stream") = 0,
       py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "preinit_device",
+      [](int device) {
+        std::vector<std::pair<std::string, long long>> stages;
+        {
+          py::gil_scoped_release release;
+          stages = kiosk::preinit_device(device);
+        }
+        py::dict d;
+        for (const auto& kv : stages) d[py::str(kv.first)] = kv.second;
+        return d;
+      },
+      py::arg("device") = 0);
   m.def("synchronize", [] { check_hip(hipDeviceSynchronize(), "sync"); },
         py::call_guard<py::gil_scoped_release>());
 
@@ -175,11 +188,24 @@ PYBIND11_MODULE(_kiosk_hip, m) {
       .def_property_readonly("layers", &kiosk::Engine::layers)
       .def_property_readonly("max_rows", &kiosk::Engine::max_rows);
 
-  m.def("rccl_library", &kiosk::rccl_library);
-  m.def("rccl_version", &kiosk::rccl_version);
-  m.def("fence_can_shrink", &kiosk::rccl_can_shrink);
-  m.def("fence_unique_id",
-        [] { return py::bytes(kiosk::rccl_unique_id()); });
+  // every RCCL entry point releases the GIL: the first call initialises
+  // the library (seconds) and must not stall the worker's serving thread
+  m.def("rccl_library", &kiosk::rccl_library,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("rccl_version", &kiosk::rccl_version,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("fence_can_shrink", &kiosk::rccl_can_shrink,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("fence_warmup", &kiosk::rccl_warmup, py::arg("timeout") = 60.0,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("fence_unique_id", [] {
+    std::string id;
+    {
+      py::gil_scoped_release release;
+      id = kiosk::rccl_unique_id();
+    }
+    return py::bytes(id);
+  });
 
   py::class_<kiosk::Fence>(m, "Fence")
       .def(py::init([](py::bytes uid, int nranks, int rank, double timeout) {

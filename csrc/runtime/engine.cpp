@@ -29,6 +29,47 @@ namespace {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 }  // namespace
 
+std::vector<std::pair<std::string, long long>> preinit_device(int device) {
+  std::vector<std::pair<std::string, long long>> stages;
+  stages.emplace_back("preinit_enter", monotonic_ns());
+  check_hip(hipSetDevice(device), "hipSetDevice");
+  check_hip(hipFree(nullptr), "hip context init");
+  stages.emplace_back("preinit_context", monotonic_ns());
+  check_hip(gemm_prepare(), "gemm_prepare");
+  hipStream_t stream = nullptr;
+  check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking),
+            "hipStreamCreate");
+  // 128x128 operands + bias + output + sums + warm-start record
+  const size_t elems = 128 * 128;
+  char* scratch = nullptr;
+  const size_t bytes = 4 * elems * 2 + 128 * 4 + kSumBlocks * 4 + 4096;
+  check_hip(hipMalloc(reinterpret_cast<void**>(&scratch), bytes),
+            "hipMalloc(preinit)");
+  uint16_t* a = reinterpret_cast<uint16_t*>(scratch);
+  uint16_t* b = a + elems;
+  uint16_t* c = b + elems;
+  uint16_t* r = c + elems;
+  float* bias = reinterpret_cast<float*>(r + elems);
+  float* sums = bias + 128;
+  uint32_t* rec = reinterpret_cast<uint32_t*>(sums + kSumBlocks);
+  check_hip(launch_init_uniform_bf16(a, 4 * elems, 1, -1.f, 1.f, stream),
+            "preinit init");
+  check_hip(launch_init_uniform_f32(bias, 128, 2, -1.f, 1.f, stream),
+            "preinit init f32");
+  for (int epi = 0; epi < 3; ++epi) {
+    check_hip(launch_gemm(a, b, c, bias, r, 128, 128, 128, epi, stream),
+              "preinit gemm");
+  }
+  check_hip(launch_partial_sums(c, elems, sums, stream), "preinit sums");
+  check_hip(launch_warmstart(a, elems, rec, 1, 1, 2 * kGemmLdsBytes, stream),
+            "preinit warmstart");
+  check_hip(hipStreamSynchronize(stream), "preinit sync");
+  check_hip(hipFree(scratch), "hipFree(preinit)");
+  check_hip(hipStreamDestroy(stream), "hipStreamDestroy");
+  stages.emplace_back("preinit_done", monotonic_ns());
+  return stages;
+}
+
 void Engine::stage(const char* name) {
   stages_.emplace_back(name, monotonic_ns());
 }

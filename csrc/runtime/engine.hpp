@@ -15,6 +15,13 @@ namespace kiosk {
 void check_hip(hipError_t err, const char* what);
 long long monotonic_ns();
 
+// Standby pre-initialisation on the (already pinned) device: create the
+// HIP context and load every kernel code object by launching each kernel
+// once on a tiny scratch buffer, then free it.  Leaves no HBM allocated
+// and nothing running; the later Engine ctor then skips ~150 ms of
+// runtime init + code-object loading.  Returns stage timestamps.
+std::vector<std::pair<std::string, long long>> preinit_device(int device);
+
 struct WarmStartResult {
   int blocks = 0;
   int distinct_cus = 0;

@@ -124,6 +124,14 @@ std::string rccl_unique_id() {
   return std::string(id.internal, sizeof(id.internal));
 }
 
+double rccl_warmup(double timeout_s) {
+  const double t0 = now_s();
+  Fence fence(rccl_unique_id(), 1, 0, timeout_s);
+  fence.allreduce(std::vector<long long>{1});
+  fence.destroy();
+  return (now_s() - t0) * 1e3;
+}
+
 void Fence::wait_ready(void* comm, double timeout_s, const char* what) {
   const double deadline = now_s() + timeout_s;
   while (true) {

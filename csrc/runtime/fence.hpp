@@ -19,6 +19,10 @@ std::string rccl_library();       // path actually loaded
 int rccl_version();
 bool rccl_can_shrink();
 std::string rccl_unique_id();     // 128 raw bytes
+// One-time RCCL initialisation off the critical path (standby boot):
+// loads the library, builds and destroys a 1-rank communicator on the
+// current device (RCCL device code + proxy setup), returns elapsed ms.
+double rccl_warmup(double timeout_s);
 
 class Fence {
  public:

@@ -147,6 +147,7 @@ EXTRA_DEFAULTS = (
     ('WORKER_MODULE', str, 'kiosk_autoscaler_amd.worker.main'),
     ('WORKER_BACKEND', str, 'auto'),        # auto | hip | cpu
     ('WARM_POOL', int, -1),                 # standby processes (-1 = MAX_PODS)
+    ('WARM_POOL_MODE', str, 'device'),      # device (HIP ctx preinit) | import
     ('WARM_START', bool, True),             # run the N1 warm-start kernel
     ('FENCE', str, 'auto'),                 # auto | rccl | store | none
     ('MODEL_DIM', int, 4096),

@@ -221,17 +221,19 @@ class GpuManager(object):
 
     def __init__(self, slots, redis_client=None, pool_size=0,
                  pool_template=None, events=None, fence=True,
+                 pool_mode='device',
                  fence_timeout=60.0, max_restart_backoff=10.0):
         self.slots = list(slots)
         self.redis = redis_client
         self.pool_size = max(0, int(pool_size))
         self.pool_template = pool_template
+        self.pool_mode = pool_mode
         self.events = events if events is not None else NULL_EVENTS
         self.fence_enabled = fence
         self.fence_timeout = fence_timeout
         self.max_restart_backoff = max_restart_backoff
         self.resources = collections.OrderedDict()
-        self.standbys = []
+        self.standbys = collections.OrderedDict()   # slot index -> _Process
         self.lock = threading.RLock()
         self._thread = None
         self._stop = threading.Event()
@@ -296,8 +298,9 @@ class GpuManager(object):
         with self.lock:
             return {
                 'slots': [s.to_dict() for s in self.slots],
-                'standbys': [{'pid': p.pid, 'booted': p.booted}
-                             for p in self.standbys],
+                'standbys': [{'pid': p.pid, 'booted': p.booted,
+                              'slot': index}
+                             for index, p in self.standbys.items()],
                 'resources': [dict(r.view().to_dict(), workers=[
                     w.summary() for w in r.workers.values()])
                     for r in self.resources.values()],
@@ -332,14 +335,15 @@ class GpuManager(object):
             for resource in self.resources.values():
                 resource.declared = 0
                 self._reconcile(resource)
-            for proc in self.standbys:
+            for proc in self.standbys.values():
                 proc.pipe.send({'cmd': 'exit'})
         deadline = time.monotonic() + timeout
         while time.monotonic() < deadline:
             with self.lock:
                 alive = [w for r in self.resources.values()
                          for w in r.workers.values() if w.state != EXITED]
-                alive += [p for p in self.standbys if p.popen.poll() is None]
+                alive += [p for p in self.standbys.values()
+                          if p.popen.poll() is None]
             if not alive:
                 break
             if self._thread is None:
@@ -351,7 +355,7 @@ class GpuManager(object):
                 for worker in resource.workers.values():
                     if worker.proc.popen.poll() is None:
                         worker.proc.popen.kill()
-            for proc in self.standbys:
+            for proc in self.standbys.values():
                 if proc.popen.poll() is None:
                     proc.popen.kill()
         self._stop.set()
@@ -367,7 +371,7 @@ class GpuManager(object):
     def poll(self, timeout=0.05):
         with self.lock:
             fds = {self._wake_r: None}
-            for proc in self.standbys:
+            for proc in self.standbys.values():
                 if not proc.eof:
                     fds[proc.pipe.ev_r] = proc
             for resource in self.resources.values():
@@ -399,7 +403,7 @@ class GpuManager(object):
     # ------------------------------------------------------------------
     # process management
     # ------------------------------------------------------------------
-    def _spawn(self, template, role, assign=None):
+    def _spawn(self, template, role, assign=None, slot=None):
         cmd_r, cmd_w = os.pipe()
         ev_r, ev_w = os.pipe()
         argv = [template.python, '-m', template.module,
@@ -407,6 +411,10 @@ class GpuManager(object):
                 '--backend', template.backend]
         if assign is not None:
             argv += ['--assign', json.dumps(assign)]
+        elif slot is not None:
+            argv += ['--pin', json.dumps({
+                'gpu': slot.visible_id, 'slot': slot.index, 'cpus': slot.cpus,
+                'preinit': self.pool_mode})]
         env = dict(os.environ)
         env.update({k: str(v) for k, v in template.env.items()})
         env['PYTHONUNBUFFERED'] = '1'
@@ -422,28 +430,42 @@ class GpuManager(object):
             os.close(cmd_r)
             os.close(ev_w)
         proc = _Process(popen, _Pipe(cmd_w, ev_r), role)
-        self.events.emit('process_spawn', role=role, pid=popen.pid)
+        proc.slot = slot.index if slot is not None else None
+        self.events.emit('process_spawn', role=role, pid=popen.pid,
+                         slot=proc.slot)
         return proc
 
     def _refill_pool(self):
+        """Keep one standby pinned to each of the lowest ``pool_size`` free
+        GPUs (the slots the next scale-up will take)."""
         if not self.pool_size or self.pool_template is None or \
                 self._stopping:
             return
-        self.standbys = [p for p in self.standbys if p.popen.poll() is None]
-        while len(self.standbys) < self.pool_size:
-            self.standbys.append(self._spawn(self.pool_template, 'standby'))
+        changed = False
+        for index, proc in list(self.standbys.items()):
+            if proc.popen.poll() is not None:
+                proc.pipe.close()
+                del self.standbys[index]
+                changed = True
+        for slot in self._free_slots()[:self.pool_size]:
+            if slot.index not in self.standbys:
+                self.standbys[slot.index] = self._spawn(
+                    self.pool_template, 'standby', slot=slot)
+                changed = True
+        if changed:
+            self._publish_pool()
 
-    def _take_standby(self, template):
+    def _take_standby(self, template, slot):
+        """The standby pinned to ``slot`` (booted or still booting: it
+        reads the assignment as soon as its imports finish)."""
         if self.pool_template is None or \
                 template.module != self.pool_template.module or \
                 template.backend != self.pool_template.backend:
             return None
-        booted = [p for p in self.standbys if p.booted and
-                  p.popen.poll() is None]
-        if not booted:
+        proc = self.standbys.get(slot.index)
+        if proc is None or proc.popen.poll() is not None:
             return None
-        proc = booted[0]
-        self.standbys.remove(proc)
+        del self.standbys[slot.index]
         self._publish_pool()
         return proc
 
@@ -452,7 +474,8 @@ class GpuManager(object):
             return
         try:
             self.redis.set(POOL_KEY, '%d %d' % (
-                sum(1 for p in self.standbys if p.booted), len(self.standbys)))
+                sum(1 for p in self.standbys.values() if p.booted),
+                len(self.standbys)))
         except Exception:  # pylint: disable=broad-except
             pass
 
@@ -465,8 +488,9 @@ class GpuManager(object):
                 proc.booted = True
                 self._publish_pool()
                 self.events.emit('standby_ready', pid=proc.pid,
+                                 slot=proc.slot,
                                  boot_s=(time.monotonic_ns() - proc.t_spawn)
-                                 / 1e9)
+                                 / 1e9, preinit=message.get('preinit'))
 
     def _free_slots(self):
         used = set()
@@ -486,7 +510,7 @@ class GpuManager(object):
             'template': resource.template.to_dict(),
             't_assign': time.monotonic_ns(),
         }
-        proc = self._take_standby(resource.template)
+        proc = self._take_standby(resource.template, slot)
         from_pool = proc is not None
         if from_pool:
             if not proc.pipe.send(assign):
@@ -494,7 +518,8 @@ class GpuManager(object):
                 proc = None
                 from_pool = False
         if proc is None:
-            proc = self._spawn(resource.template, 'worker', assign=assign)
+            proc = self._spawn(resource.template, 'worker', assign=assign,
+                               slot=slot)
         proc.role = 'worker'
         worker = Worker(wid, resource, slot, proc, from_pool)
         resource.workers[wid] = worker
@@ -576,10 +601,10 @@ class GpuManager(object):
                 # drain remaining messages (the READY/exit of a short job)
                 self._on_worker_messages(worker)
                 self._on_exit(resource, worker, code)
-        for proc in list(self.standbys):
+        for index, proc in list(self.standbys.items()):
             if proc.popen.poll() is not None:
                 proc.pipe.close()
-                self.standbys.remove(proc)
+                del self.standbys[index]
 
     def _on_exit(self, resource, worker, code):
         was_ready = worker.state in (READY, DRAINING) and worker.t_ready

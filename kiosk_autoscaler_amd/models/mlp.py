@@ -89,11 +89,10 @@ class CpuMlpEngine(object):
         return {'ms': (time.perf_counter() - t0) * 1e3,
                 'checksum': float(x.sum())}
 
-    def passes_for(self, service_ms, rows):
+    def forward_for(self, rows, service_ms, seed):
         # the mock has no real pass time: sleep the requested service time
         self._service_ms = float(service_ms)
-        unit = self.cfg.mock_work_ms or float(service_ms)
-        return max(1, int(round(service_ms / unit)))
+        return self.forward(rows, 1, seed)
 
     def close(self):
         self.layers = []
@@ -116,7 +115,7 @@ class HipMlpEngine(object):
         if stage:
             for name, t in sorted(self.engine.stage_times().items(),
                                   key=lambda kv: kv[1]):
-                stage(name)
+                stage(name, t)   # native CLOCK_MONOTONIC stamps
 
     def warmstart(self):
         info = dict(self.engine.warmstart())
@@ -133,13 +132,30 @@ class HipMlpEngine(object):
         self.pass_ms[rows] = max(out['gpu_ms'] / passes, 1e-3)
         return self.pass_ms[rows]
 
-    def passes_for(self, service_ms, rows):
-        ms = self.pass_ms.get(rows) or self.measure(rows)
-        return max(1, int(round(service_ms / ms)))
 
     def forward(self, rows, passes, seed):
         return dict(self.engine.forward(int(rows), int(max(1, passes)),
                                         int(seed)))
+
+    def forward_for(self, rows, service_ms, seed, chunk_ms=25.0):
+        """Run real forward passes until ``service_ms`` of wall time is
+        spent (chunks of ~``chunk_ms``; the per-pass estimate adapts)."""
+        t0 = time.perf_counter()
+        total = {'ms': 0.0, 'gpu_ms': 0.0, 'checksum': 0.0, 'passes': 0}
+        per_pass = self.pass_ms.get(rows) or self.measure(rows)
+        while True:
+            left = service_ms - (time.perf_counter() - t0) * 1e3
+            if left <= per_pass * 0.5:
+                break
+            n = max(1, int(min(left, chunk_ms) / per_pass))
+            out = self.engine.forward(int(rows), n, int(seed))
+            per_pass = 0.7 * per_pass + 0.3 * (out['gpu_ms'] / n)
+            total['gpu_ms'] += out['gpu_ms']
+            total['passes'] += n
+            total['checksum'] = out['checksum']
+        self.pass_ms[rows] = per_pass
+        total['ms'] = (time.perf_counter() - t0) * 1e3
+        return total
 
     def close(self):
         if self.engine is not None:

@@ -53,6 +53,8 @@ def main(argv=None):
     parser.add_argument('--ev-fd', type=int, default=None)
     parser.add_argument('--backend', default='auto')
     parser.add_argument('--assign', default=None)
+    parser.add_argument('--pin', default=None,
+                        help='standby: JSON {gpu, slot, cpus, preinit}')
     args = parser.parse_args(argv)
     _die_with_parent()
 
@@ -66,23 +68,45 @@ def main(argv=None):
     channel = Channel(args.cmd_fd, args.ev_fd)
 
     backend = args.backend
+    pin = parse_assignment(args.pin) if args.pin else None
+    early = parse_assignment(args.assign) if args.assign else pin
     if backend == 'auto':
-        backend = 'cpu'
-        if args.assign:
-            if parse_assignment(args.assign).get('gpu') not in (None, ''):
-                backend = 'hip'
+        backend = 'hip' if early and early.get('gpu') not in (None, '') \
+            else 'cpu'
+    if early is not None:
+        # pin before anything can initialise HIP (HIP_VISIBLE_DEVICES is
+        # read once, at runtime init) and before the heavy imports
+        apply_assignment_env({'gpu': early.get('gpu'),
+                              'cpus': early.get('cpus')})
     preload_ns = _preload(backend)
+    preinit = {}
+    if pin and pin.get('preinit') == 'device' and backend == 'hip':
+        from ..ops import native
+        try:
+            mod = native.load()
+            preinit = dict(mod.preinit_device(0))
+            if os.environ.get('FENCE', 'auto') in ('auto', 'rccl'):
+                # RCCL's one-time init costs seconds: pay it while idle
+                preinit['rccl_warmup_ms'] = mod.fence_warmup(60.0)
+        except Exception as err:  # pylint: disable=broad-except
+            channel.emit('error', message='preinit failed: %s' % err)
+            return 4
 
     if args.assign:
         assignment = parse_assignment(args.assign)
     else:
-        channel.emit('standby', preload_ns=preload_ns, backend=backend)
+        channel.emit('standby', preload_ns=preload_ns, backend=backend,
+                     preinit=preinit)
         while True:
             assignment = channel.read_command()
             if assignment is None or assignment.get('cmd') == 'exit':
                 return 0
             if assignment.get('cmd') == 'assign':
                 break
+        if pin and str(assignment.get('gpu')) != str(pin.get('gpu')):
+            channel.emit('error', message='assigned GPU %s but pinned to %s'
+                         % (assignment.get('gpu'), pin.get('gpu')))
+            return 5
     apply_assignment_env(assignment)
     config = WorkerConfig(os.environ, assignment)
 
@@ -112,7 +136,13 @@ def main(argv=None):
     if events is not None:
         events.emit('worker_exit_self', worker=config.worker_id,
                     keys_done=runtime.keys_done)
-    return code
+        events.close()
+    # The engine (HBM, streams, graphs) and the fence are released by now;
+    # skip interpreter teardown (torch/HIP static destructors take ~0.5 s)
+    # so the GPU slot frees promptly.
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(code)
 
 
 if __name__ == '__main__':

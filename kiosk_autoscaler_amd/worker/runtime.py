@@ -62,6 +62,7 @@ class WorkerConfig(object):
         self.warm_start = env.get('WARM_START', '1').lower() not in (
             '0', 'false', 'no', 'off')
         self.fence = env.get('FENCE', 'auto')
+        # how long an idle worker blocks in BLMOVE: bounds drain latency
         self.poll_block = _env_float(env, 'POLL_BLOCK_S', 0.1)
         self.job_idle_exit = _env_float(env, 'JOB_IDLE_EXIT_S', 1.0)
         self.mock_work_ms = _env_float(env, 'MOCK_WORK_MS', 0.0)
@@ -86,9 +87,9 @@ class QueueConsumer(object):
         """Return up to ``limit`` ``(queue, item, processing_key)`` tuples.
 
         Sweeps every queue with non-blocking ``LMOVE`` first; when all are
-        empty, blocks on one queue (rotating) for ``poll_block`` seconds --
-        or indefinitely-short 1 s chunks with a single queue, where
-        ``BLMOVE`` wakes the instant a key lands."""
+        empty, blocks on one queue (rotating) for ``poll_block`` seconds
+        (``BLMOVE`` wakes the instant a key lands on that queue; the bound
+        keeps a drain command from waiting long)."""
         taken = []
         for queue in self.queues:
             while len(taken) < limit:
@@ -101,7 +102,7 @@ class QueueConsumer(object):
             return taken
         queue = self.queues[self._rotate % len(self.queues)]
         self._rotate += 1
-        timeout = 1.0 if len(self.queues) == 1 else self.poll_block
+        timeout = self.poll_block
         pkey = self.processing_key(queue, 0)
         item = self.redis.blmove(queue, pkey, timeout, 'RIGHT', 'LEFT')
         if item is not None:
@@ -132,8 +133,8 @@ class WorkerRuntime(object):
         self.stages = {}
         self.keys_done = 0
 
-    def _stage(self, name):
-        t = time.monotonic_ns()
+    def _stage(self, name, t=None):
+        t = time.monotonic_ns() if t is None else int(t)
         self.stages[name] = t
         self.channel.emit('stage', stage=name, t=t)
         return t
@@ -249,10 +250,12 @@ class WorkerRuntime(object):
         passes = max(p['passes'] for _, _, _, p, _ in jobs)
         service_ms = max(p['service_ms'] for _, _, _, p, _ in jobs)
         if service_ms > 0:
-            # a fixed per-key GPU service time (the benchmark's S): convert
-            # it to forward passes with this engine's measured pass time
-            passes = self.engine.passes_for(service_ms, rows)
-        result = self.engine.forward(rows, passes, jobs[0][3]['seed'])
+            # a fixed per-key GPU service time (the benchmark's S): run real
+            # forward passes until that much GPU time has been spent
+            result = self.engine.forward_for(rows, service_ms,
+                                             jobs[0][3]['seed'])
+        else:
+            result = self.engine.forward(rows, passes, jobs[0][3]['seed'])
         t_done = time.monotonic_ns()
         for queue, item, pkey, params, fields in jobs:
             if fields:

@@ -159,3 +159,10 @@ def test_fence_agent_rccl_transport(mod):
         assert r2['ok'] and r2['mode'] == 'reuse'
     finally:
         agent.close()
+
+
+def test_fence_warmup_and_preinit(mod):
+    ms = mod.fence_warmup(60.0)
+    assert ms > 0
+    stages = mod.preinit_device(0)
+    assert list(stages) == ['preinit_enter', 'preinit_context', 'preinit_done']

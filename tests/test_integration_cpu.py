@@ -74,8 +74,8 @@ def tick(scaler, s):
 
 def test_scale_up_process_scale_down(stack):
     s, client, manager, scaler, events = stack()
-    wait_for(lambda: all(p.booted for p in manager.standbys)
-             and manager.standbys)
+    wait_for(lambda: manager.standbys and all(
+        p.booted for p in manager.standbys.values()))
     enqueue(client, 3)
     assert tick(scaler, s) == 1
     wait_for(lambda: all(client.hget('predict:job%d' % i, 'status') == 'done'
