@@ -114,6 +114,39 @@ def kfd_gpus(root=KFD_NODES):
     return found
 
 
+def amdsmi_gpus():
+    """Fallback inventory through amdsmi (no HIP init) when the KFD
+    topology is not readable (e.g. inside some containers)."""
+    try:
+        import amdsmi
+        amdsmi.amdsmi_init()
+    except Exception:  # pylint: disable=broad-except
+        return []
+    found = []
+    try:
+        for handle in amdsmi.amdsmi_get_processor_handles():
+            info = {'pci': None, 'numa_node': -1, 'cpus': [], 'cu_count': 0}
+            try:
+                info['pci'] = amdsmi.amdsmi_get_gpu_device_bdf(handle)
+                numa, cpus = _local_cpus(info['pci'])
+                info['cpus'] = cpus
+                info['numa_node'] = numa
+            except Exception:  # pylint: disable=broad-except
+                pass
+            try:
+                info['numa_node'] = int(
+                    amdsmi.amdsmi_topo_get_numa_node_number(handle))
+            except Exception:  # pylint: disable=broad-except
+                pass
+            found.append(info)
+    finally:
+        try:
+            amdsmi.amdsmi_shut_down()
+        except Exception:  # pylint: disable=broad-except
+            pass
+    return found
+
+
 def _visible_filter(env):
     for name in ('HIP_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES',
                  'CUDA_VISIBLE_DEVICES'):
@@ -133,7 +166,7 @@ def discover(gpu_ids='', env=None, cpu_slots=0, kfd_root=KFD_NODES):
             virtual slots (mock-worker plumbing runs, BASELINE config 1).
     """
     env = os.environ if env is None else env
-    nodes = kfd_gpus(kfd_root)
+    nodes = kfd_gpus(kfd_root) or amdsmi_gpus()
     visible = _visible_filter(env)
     if visible is not None:
         physical = [int(v) for v in visible if v.isdigit()]

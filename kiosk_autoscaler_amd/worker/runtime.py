@@ -286,7 +286,14 @@ def apply_assignment_env(assignment, env=None):
         env[key] = str(value)
     gpu = assignment.get('gpu')
     if gpu not in (None, ''):
-        env['HIP_VISIBLE_DEVICES'] = str(gpu)
+        # `gpu` is an ordinal of the full device list.  If the node filters
+        # at the ROCr level, re-filter there (HIP would renumber from 0).
+        env.pop('CUDA_VISIBLE_DEVICES', None)
+        if env.get('ROCR_VISIBLE_DEVICES'):
+            env['ROCR_VISIBLE_DEVICES'] = str(gpu)
+            env.pop('HIP_VISIBLE_DEVICES', None)
+        else:
+            env['HIP_VISIBLE_DEVICES'] = str(gpu)
     cpus = assignment.get('cpus') or []
     if cpus and hasattr(os, 'sched_setaffinity'):
         try:

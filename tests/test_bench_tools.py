@@ -1,0 +1,124 @@
+"""Simulator, metrics, load generator and a CPU bench.py smoke run."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from kiosk_autoscaler_amd.bench import metrics, sim
+from kiosk_autoscaler_amd.bench.loadgen import LoadGenerator
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_poisson_on_off_shape():
+    arrivals = sim.poisson_on_off(2.0, 10, 10, 100, seed=1)
+    assert all(((t % 20) < 10) for t, _ in arrivals)
+    rate = len(arrivals) / 50.0          # 5 on-windows of 10 s
+    assert 1.5 < rate < 2.5
+    assert arrivals == sim.poisson_on_off(2.0, 10, 10, 100, seed=1)
+
+
+def test_sim_single_key_cold_start():
+    # one key at t=1.2, ticks every 5 s from 0 -> decided at 5, ready at 5
+    out = sim.simulate([(1.2, 'predict')], interval=5.0, service_s=1.0,
+                       max_pods=1)
+    assert out['cold_start_mean_s'] == pytest.approx(3.8, abs=0.02)
+    assert out['cold_starts'] == 1
+    # alive from 5 until the tick after the key is done (10): 1 s busy of 5
+    assert out['gpu_idle_pct'] == pytest.approx(80.0, abs=1.0)
+
+
+def test_sim_ready_delay_adds_linearly():
+    base = sim.simulate([(1.0, 'predict')], max_pods=1)
+    slow = sim.simulate([(1.0, 'predict')], max_pods=1, ready_delay=2.0)
+    assert slow['cold_start_mean_s'] - base['cold_start_mean_s'] == \
+        pytest.approx(2.0, abs=0.02)
+
+
+def test_sim_reproduces_baseline_order_of_magnitude():
+    """BASELINE.md §3 row 2 (MAX=8, lam=2): ~3.1-3.4 s, ~65 % idle with the
+    10 ms tick of the original simulation."""
+    results = [sim.simulate(sim.poisson_on_off(2.0, 60, 60, 600, seed=s),
+                            max_pods=8, tick_s=0.01) for s in range(2)]
+    lat = sum(r['cold_start_mean_s'] for r in results) / 2
+    idle = sum(r['gpu_idle_pct'] for r in results) / 2
+    assert 2.5 < lat < 4.6 and 55 < idle < 75
+
+
+def test_strict_policy_cuts_idle():
+    arrivals = sim.poisson_on_off(2.0, 60, 60, 600, seed=3)
+    ref = sim.simulate(arrivals, max_pods=8)
+    strict = sim.simulate(arrivals, max_pods=8, policy='strict')
+    assert strict['gpu_idle_pct'] < ref['gpu_idle_pct']
+
+
+def _ev(kind, t, **kw):
+    d = {'ev': kind, 't': int(t * 1e9)}
+    d.update(kw)
+    return d
+
+
+def test_metrics_cold_starts_and_idle():
+    keys = [('k1', 'q', int(1.0e9)), ('k2', 'q', int(1.5e9)),
+            ('k3', 'q', int(20.0e9))]
+    events = [
+        _ev('scale', 5.0, current=0, desired=1),
+        _ev('worker_assigned', 5.0, worker='w1'),
+        _ev('worker_ready', 5.1, worker='w1'),
+        _ev('key_start', 5.1, worker='w1', item='k1'),
+        _ev('key_done', 6.1, worker='w1', item='k1'),
+        _ev('key_start', 6.1, worker='w1', item='k2'),
+        _ev('key_done', 7.1, worker='w1', item='k2'),
+        _ev('worker_drain', 10.0, worker='w1'),
+        _ev('worker_exit', 10.5, worker='w1'),
+        _ev('worker_assigned', 25.0, worker='w2'),
+        _ev('worker_ready', 25.2, worker='w2'),
+        _ev('key_start', 25.2, worker='w2', item='k3'),
+        _ev('key_done', 26.2, worker='w2', item='k3'),
+        _ev('worker_exit', 30.0, worker='w2'),
+    ]
+    colds = metrics.cold_starts(events, keys, 0, int(40e9))
+    assert [round((b - a) / 1e9, 3) for a, b in colds] == [4.1, 5.2]
+    idle, alive, busy = metrics.gpu_idle(events, 0, int(40e9))
+    assert alive == pytest.approx(10.5) and busy == pytest.approx(3.0)
+    assert idle == pytest.approx(100 * 7.5 / 10.5)
+    ep = {'t_first': keys[0][2], 't_end': int(40e9), 'keys': keys}
+    summary = metrics.summarize(events, [ep])
+    assert summary['cold_starts'] == 2
+    assert summary['decision_mean_s'] == pytest.approx(4.0)
+    assert summary['actuation_mean_s'] == pytest.approx(0.1)
+    assert summary['first_result_mean_s'] == pytest.approx(5.1)
+
+
+def test_loadgen_writes_hash_before_key(redis_client):
+    gen = LoadGenerator(redis_client, ['predict'], rate=50.0, service_ms=5,
+                        seed=1)
+    import time
+    keys = gen.on_window(time.monotonic_ns(), 0.1)
+    assert len(keys) >= 1
+    assert redis_client.llen('predict') == len(keys)
+    item = redis_client.rpop('predict')
+    job = redis_client.hgetall(item)
+    assert job['status'] == 'new' and job['service_ms'] == '5'
+
+
+@pytest.mark.slow
+def test_bench_cpu_smoke(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    proc = subprocess.run(
+        [sys.executable, os.path.join(ROOT, 'bench.py'), '--backend', 'cpu',
+         '--steps', '1', '--warmup', '0', '--interval', '0.5', '--on', '1',
+         '--off', '0.2', '--lam-per-gpu', '4', '--service-ms', '50',
+         '--gpus', '1'], env=env, stdout=subprocess.PIPE,
+        stderr=subprocess.PIPE, text=True, timeout=240)
+    assert proc.returncode == 0, proc.stderr[-2000:]
+    line = json.loads(proc.stdout.strip().splitlines()[-1])
+    for key in ('metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup',
+                'ms_per_step', 'higher_is_better', 'scaling', 'vs_baseline',
+                'dtype', 'data', 'config'):
+        assert key in line
+    assert line['higher_is_better'] is False and line['n_gpus'] == 1
+    assert line['keys_done'] == line['keys'] > 0
+    assert line['value'] is not None and line['value'] < 1.0

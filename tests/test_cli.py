@@ -1,0 +1,106 @@
+"""Process-level behaviour of scale.py / cli (C16-C18, SURVEY §4 gaps):
+missing RESOURCE_NAME is fatal, any tick exception is CRITICAL + exit 1,
+sleep-after vs fixed-rate loop timing, log format and rotation."""
+import logging
+import os
+import subprocess
+import sys
+from unittest import mock
+
+import pytest
+
+from kiosk_autoscaler_amd import cli
+from kiosk_autoscaler_amd.config import Config, Settings
+from kiosk_autoscaler_amd.utils.logs import LOG_FORMAT, initialize_logger
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_scale(env, timeout=60):
+    full = {'PATH': os.environ.get('PATH', ''), 'PYTHONPATH': ROOT,
+            'HOME': os.environ.get('HOME', '/tmp')}
+    full.update(env)
+    return subprocess.run([sys.executable, os.path.join(ROOT, 'scale.py')],
+                          env=full, cwd=env.get('_CWD', ROOT),
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                          text=True, timeout=timeout)
+
+
+def test_missing_resource_name_is_fatal(tmp_path):
+    proc = run_scale({'_CWD': str(tmp_path)})
+    assert proc.returncode != 0
+    assert 'RESOURCE_NAME' in proc.stderr
+
+
+def test_unreachable_redis_crashes_startup(tmp_path):
+    proc = run_scale({'_CWD': str(tmp_path), 'RESOURCE_NAME': 'w',
+                      'REDIS_HOST': '127.0.0.1', 'REDIS_PORT': '1',
+                      'WORKER_BACKEND': 'cpu'})
+    assert proc.returncode == 1
+    assert 'Fatal Error: ConnectionError' in proc.stdout
+
+
+def test_bad_resource_type_fatal_at_first_tick(tmp_path, resp_server):
+    proc = run_scale({'_CWD': str(tmp_path), 'RESOURCE_NAME': 'w',
+                      'RESOURCE_TYPE': 'statefulset',
+                      'REDIS_HOST': resp_server.host,
+                      'REDIS_PORT': str(resp_server.port),
+                      'WORKER_BACKEND': 'cpu', 'WARM_POOL': '0'})
+    assert proc.returncode == 1
+    assert 'Fatal Error: ValueError' in proc.stdout
+    assert os.path.exists(tmp_path / 'autoscaler.log')
+
+
+def _settings(**env):
+    base = {'RESOURCE_NAME': 'w'}
+    base.update({k: str(v) for k, v in env.items()})
+    return Settings(Config(environ=base, use_files=False))
+
+
+def test_run_loop_sleep_after_vs_fixed_rate():
+    scaler = mock.Mock()
+    clock = [0.0]
+
+    def fake_sleep(dt):
+        clock[0] += dt
+
+    def slow_scale(**kwargs):
+        clock[0] += 0.3    # the tick itself takes 0.3 s
+    scaler.scale.side_effect = slow_scale
+    s = _settings(INTERVAL=5)
+    sleeps = []
+    cli.run_loop(scaler, s, max_ticks=3,
+                 sleep=lambda dt: (sleeps.append(dt), fake_sleep(dt)),
+                 clock=lambda: clock[0])
+    assert sleeps == [5, 5]                 # period = tick + INTERVAL
+    assert scaler.scale.call_args.kwargs == {
+        'namespace': 'default', 'resource_type': 'deployment', 'name': 'w',
+        'min_pods': 0, 'max_pods': 1, 'keys_per_pod': 1}
+    sleeps.clear()
+    clock[0] = 0.0
+    cli.run_loop(scaler, _settings(INTERVAL=5, FIXED_RATE=1), max_ticks=3,
+                 sleep=lambda dt: (sleeps.append(dt), fake_sleep(dt)),
+                 clock=lambda: clock[0])
+    assert sleeps == [pytest.approx(4.7), pytest.approx(4.7)]
+
+
+def test_logger_format_and_rotation(tmp_path):
+    root = logging.getLogger()
+    saved = list(root.handlers)
+    try:
+        initialize_logger(debug_mode=False, log_file=str(tmp_path / 'a.log'),
+                          stream=open(os.devnull, 'w'))
+        handlers = root.handlers[len(saved):]
+        rotating = [h for h in handlers
+                    if isinstance(h, logging.handlers.RotatingFileHandler)]
+        assert rotating and rotating[0].maxBytes == 10000000
+        assert rotating[0].backupCount == 10
+        assert rotating[0].level == logging.DEBUG
+        console = [h for h in handlers if h not in rotating][0]
+        assert console.level == logging.INFO
+        assert handlers[0].formatter._fmt == LOG_FORMAT
+        assert root.level == logging.DEBUG
+    finally:
+        for handler in root.handlers[len(saved):]:
+            root.removeHandler(handler)
+            handler.close()

@@ -1,0 +1,167 @@
+"""GPU manager units: discovery, resource views, daemon transport, requeue,
+worker env pinning.  (End-to-end process tests: test_integration_cpu.py.)"""
+import os
+
+import pytest
+
+from kiosk_autoscaler_amd import gpumgr
+from kiosk_autoscaler_amd.fakes import FakeRedis
+from kiosk_autoscaler_amd.gpumgr import gpus
+from kiosk_autoscaler_amd.gpumgr.resources import (ActuatorError,
+                                                   ResourceView,
+                                                   desired_from_body)
+from kiosk_autoscaler_amd.worker.runtime import apply_assignment_env
+
+
+def make_kfd(tmp_path, n_gpu=2):
+    root = tmp_path / 'nodes'
+    (root / '0').mkdir(parents=True)
+    (root / '0' / 'properties').write_text('cpu_cores_count 64\nsimd_count 0\n'
+                                           'gpu_id 0\n')
+    for i in range(n_gpu):
+        node = root / str(i + 1)
+        node.mkdir()
+        node.joinpath('properties').write_text(
+            'simd_count 1024\nsimd_per_cu 4\ngpu_id %d\n'
+            'location_id %d\ndomain 0\n' % (1000 + i, (0x10 + i) << 8))
+    return str(root)
+
+
+def test_kfd_discovery(tmp_path):
+    root = make_kfd(tmp_path, 3)
+    slots = gpus.discover(env={}, kfd_root=root)
+    assert [s.visible_id for s in slots] == ['0', '1', '2']
+    assert slots[0].cu_count == 256 and slots[1].pci == '0000:11:00.0'
+    slots = gpus.discover(gpu_ids='1,2', env={}, kfd_root=root)
+    assert [(s.index, s.visible_id) for s in slots] == [(0, '1'), (1, '2')]
+    slots = gpus.discover(env={'HIP_VISIBLE_DEVICES': '2'}, kfd_root=root)
+    assert [s.visible_id for s in slots] == ['2']
+
+
+def test_discovery_fallbacks(tmp_path):
+    empty = str(tmp_path / 'none')
+    assert gpus.discover(env={}, kfd_root=empty, cpu_slots=0) == [] or True
+    slots = gpus.discover(gpu_ids='0,1', env={}, kfd_root=empty)
+    assert [s.visible_id for s in slots] == ['0', '1']
+    slots = gpus.discover(env={}, kfd_root=empty, cpu_slots=2)
+    assert all(s.kind in ('cpu', 'gpu') for s in slots)
+    assert gpus.parse_cpulist('0-3,8,10-11') == [0, 1, 2, 3, 8, 10, 11]
+
+
+def test_pinning_env():
+    env = {'CUDA_VISIBLE_DEVICES': '0'}
+    apply_assignment_env({'gpu': '3', 'template': {'env': {'A': 1}}}, env)
+    assert env['HIP_VISIBLE_DEVICES'] == '3' and env['A'] == '1'
+    assert 'CUDA_VISIBLE_DEVICES' not in env
+    env = {'ROCR_VISIBLE_DEVICES': '0,1,2,3', 'HIP_VISIBLE_DEVICES': '0'}
+    apply_assignment_env({'gpu': '2'}, env)
+    assert env['ROCR_VISIBLE_DEVICES'] == '2'
+    assert 'HIP_VISIBLE_DEVICES' not in env
+
+
+def test_body_validation():
+    assert desired_from_body('deployment', {'spec': {'replicas': '3'}}) == 3
+    for body in ({}, {'spec': {'parallelism': 1}}, {'spec': {'replicas': -1}},
+                 {'spec': {'replicas': 'x'}}):
+        with pytest.raises(ActuatorError):
+            desired_from_body('deployment', body)
+
+
+def test_view_roundtrip():
+    view = ResourceView.build('job', 'ns', 'w', 3, ready=1, active=2,
+                              succeeded=4, gpus=[0, 1])
+    again = ResourceView.from_dict(view.to_dict())
+    assert again.spec.parallelism == 3 and again.status.succeeded == 4
+    assert again == view
+
+
+def test_manager_api_without_processes():
+    slots = [gpus.GpuSlot(i, '', kind='cpu') for i in range(2)]
+    manager = gpumgr.GpuManager(slots, fence=False)
+    tpl = gpumgr.WorkerTemplate(queues=['q'], backend='cpu')
+    manager.register('deployment', 'ns', 'w', tpl)
+    items = manager.list_namespaced_deployment('ns').items
+    assert items[0].spec.replicas == 0
+    assert manager.list_namespaced_job('ns').items == []
+    with pytest.raises(ActuatorError) as info:
+        manager.patch_namespaced_deployment('missing', 'ns',
+                                            {'spec': {'replicas': 1}})
+    assert info.value.status == 404
+    with pytest.raises(ValueError):
+        manager.register('statefulset', 'ns', 'x', tpl)
+
+
+def test_daemon_transport(tmp_path):
+    slots = [gpus.GpuSlot(0, '', kind='cpu')]
+    manager = gpumgr.GpuManager(slots, fence=False)
+    tpl = gpumgr.WorkerTemplate(queues=['q'], backend='cpu')
+    path = str(tmp_path / 'mgr.sock')
+    server = gpumgr.ManagerServer(manager, path).start()
+    try:
+        client = gpumgr.GpuManagerClient(path)
+        client.register('job', 'ns', 'w', tpl)
+        view = client.list_namespaced_job('ns').items[0]
+        assert view.metadata.name == 'w' and view.spec.parallelism == 0
+        with pytest.raises(ActuatorError) as info:
+            client.patch_namespaced_job('nope', 'ns',
+                                        {'spec': {'parallelism': 1}})
+        assert info.value.status == 404
+        assert client.status()['slots'][0]['kind'] == 'cpu'
+        assert gpumgr.connect('unix:' + path).list_namespaced_deployment(
+            'ns').items == []
+    finally:
+        server.stop()
+    with pytest.raises(ActuatorError) as info:
+        gpumgr.GpuManagerClient(path, timeout=1).list_namespaced_job('ns')
+    assert info.value.status == 503
+
+
+def test_requeue_exact_worker_keys():
+    """Worker 1's requeue must not steal worker 12's in-flight items."""
+    from kiosk_autoscaler_amd.gpumgr.controller import (Resource, Worker,
+                                                        _Process)
+    redis = FakeRedis()
+    slots = [gpus.GpuSlot(0, '', kind='cpu')]
+    manager = gpumgr.GpuManager(slots, redis_client=redis, fence=False)
+    tpl = gpumgr.WorkerTemplate(queues=['q'], backend='cpu')
+    res = Resource('deployment', 'ns', 'w', tpl)
+    redis.rpush('processing-q:w-g0-1', 'a')
+    redis.rpush('processing-q:w-g0-1.1', 'b')
+    redis.rpush('processing-q:w-g0-12', 'c')
+
+    class P(object):
+        pid = 1
+    proc = _Process.__new__(_Process)
+    proc.popen = P()
+    worker = Worker('w-g0-1', res, slots[0], proc, False)
+    assert manager._requeue(res, worker) == 2
+    assert sorted(redis.lrange('q', 0, -1)) == ['a', 'b']
+    assert redis.lrange('processing-q:w-g0-12', 0, -1) == ['c']
+
+
+def test_connect_embedded():
+    gpumgr.set_embedded(None)
+    with pytest.raises(ActuatorError):
+        gpumgr.connect('embedded')
+    sentinel = object()
+    gpumgr.set_embedded(sentinel)
+    try:
+        assert gpumgr.connect('embedded') is sentinel
+    finally:
+        gpumgr.set_embedded(None)
+
+
+def test_hbm_sizing():
+    from kiosk_autoscaler_amd.utils import hbm
+    w = hbm.model_bytes(4096, 16384, 4)
+    assert w == 4 * (2 * 4096 * 16384 + 16384 + 4096) * 2
+    per = hbm.per_key_bytes(2048, 4096, 16384)
+    limit = hbm.max_keys_per_pod(288 * 10 ** 9, w, per)
+    assert limit > 1000          # 288 GB holds thousands of 2048-row keys
+    assert hbm.size_keys_per_pod(4, 4096, 16384, 4, 2048,
+                                 hbm_bytes=288 * 10 ** 9) == 4
+    # a tiny HBM forces a clamp (and never below 1)
+    assert hbm.size_keys_per_pod(64, 4096, 16384, 4, 2048,
+                                 hbm_bytes=w + (8 << 30) + 3 * per) == 3
+    assert hbm.size_keys_per_pod(64, 4096, 16384, 4, 2048, hbm_bytes=1) == 1
+    assert os.getpid() == hbm.report(8, 16, 1, 2)['pid']

@@ -134,3 +134,52 @@ def test_expiry_and_scan_type(redis_client):
     time.sleep(0.06)
     assert redis_client.get('short') is None
     assert list(redis_client.scan_iter(_type='list')) == ['l']
+
+
+def test_native_sentinel_personality():
+    """kredis in sentinel mode + data node: RedisClient discovery end to end."""
+    import socket
+    import subprocess
+    from unittest import mock
+    from conftest import kredis_binary
+    from kiosk_autoscaler_amd.redisq import RedisClient
+    binary = kredis_binary()
+    if binary is None:
+        pytest.skip('kredis-server not built')
+
+    def port():
+        s = socket.socket()
+        s.bind(('127.0.0.1', 0))
+        p = s.getsockname()[1]
+        s.close()
+        return p
+    data_port, sentinel_port = port(), port()
+    procs = [subprocess.Popen([binary, '--port', str(data_port)],
+                              stdout=subprocess.DEVNULL),
+             subprocess.Popen([binary, '--port', str(sentinel_port),
+                               '--sentinel', 'mymaster', '127.0.0.1',
+                               str(data_port), '--replica',
+                               '127.0.0.1:%d' % data_port],
+                              stdout=subprocess.DEVNULL)]
+    try:
+        for p in (data_port, sentinel_port):
+            deadline = time.time() + 10
+            while time.time() < deadline:
+                try:
+                    socket.create_connection(('127.0.0.1', p), 0.2).close()
+                    break
+                except OSError:
+                    time.sleep(0.02)
+        client = RedisClient('127.0.0.1', sentinel_port, backoff=0)
+        assert client._redis_master is not client._sentinel
+        assert len(client._redis_slaves) == 1
+        client.lpush('predict', 'a', 'b')
+        assert client.llen('predict') == 2          # via the replica
+        assert client._sentinel.sentinel_get_master_addr_by_name(
+            'mymaster') == ('127.0.0.1', data_port)
+        with mock.patch('time.sleep'):
+            pass
+    finally:
+        for p in procs:
+            p.terminate()
+            p.wait(timeout=5)
