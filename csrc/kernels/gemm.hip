@@ -181,7 +181,30 @@ hipError_t gemm_prepare() {
   hipError_t err = configure_epi<EPI_NONE>();
   if (err == hipSuccess) err = configure_epi<EPI_BIAS_GELU>();
   if (err == hipSuccess) err = configure_epi<EPI_BIAS_RESIDUAL>();
+  if (err == hipSuccess) err = gemm256_prepare();
   return err;
+}
+
+int gemm_pick_variant(int M, int N, int K) {
+  // the 256^2 ring kernel runs one block per CU: use it only when the grid
+  // still fills the 256 CUs
+  if (gemm256_shape_ok(M, N, K) && ((M + 255) / 256) * (N / 256) >= 256)
+    return GEMM_256;
+  return GEMM_128;
+}
+
+hipError_t launch_gemm_variant(const uint16_t* A, const uint16_t* B,
+                               uint16_t* C, const float* bias,
+                               const uint16_t* R, int M, int N, int K,
+                               int epilogue, int variant, hipStream_t stream) {
+  if (variant == GEMM_AUTO) variant = gemm_pick_variant(M, N, K);
+  if (variant == GEMM_256) {
+    if ((epilogue != EPI_NONE && bias == nullptr) ||
+        (epilogue == EPI_BIAS_RESIDUAL && R == nullptr))
+      return hipErrorInvalidValue;
+    return launch_gemm256(A, B, C, bias, R, M, N, K, epilogue, stream);
+  }
+  return launch_gemm(A, B, C, bias, R, M, N, K, epilogue, stream);
 }
 
 bool gemm_shape_ok(int M, int N, int K) {

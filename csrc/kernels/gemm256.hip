@@ -1,0 +1,227 @@
+// Large-tile bf16 TN GEMM for gfx950: 256x256 block tile, 8 waves, LDS ring.
+//
+//   C[M,N] = epi(A[M,K] . B[N,K]^T)      (same contract as gemm.hip)
+//
+// Why a second kernel: the 128x128 two-barrier loop of gemm.hip tops out
+// near 0.9-1.0 PF because every k-step drains its LDS-DMA before the
+// barrier (cdna_hip_programming.md §5, "the step-3 structure's ceiling").
+// This kernel keeps the DMA in flight across barriers:
+//
+//  * K is consumed in 32-deep halves; a 4-slot LDS ring (4 x 32 KiB =
+//    128 KiB, one block per CU) holds A[256][32] + B[256][32] per slot.
+//  * at half-step h the block issues the LDS-DMA (global_load_lds_dwordx4)
+//    of half h+3, runs 32 MFMAs per wave on half h, then waits with a
+//    *counted* `s_waitcnt vmcnt(8|4|0)` -- only half h+1 must have landed,
+//    halves h+2 and h+3 stay in flight -- and a raw s_barrier (never
+//    __syncthreads, whose implicit vmcnt(0) would drain the ring).
+//  * 64-B LDS rows, 16-B chunk c of row r stored at chunk c ^ ((r>>2)&3):
+//    the 16 rows a 16-lane group reads at one k-chunk cover all 16 bank
+//    slots (conflict-free ds_read_b128); the swizzle is applied on the DMA
+//    source address because LDS-DMA writes lane-linearly (rule 21).
+//  * 8 waves as 2(M) x 4(N), 128x64 outputs per wave = 8x4 tiles of
+//    v_mfma_f32_16x16x32_bf16 with swapped operands (C^T in registers ->
+//    4 consecutive columns per lane -> 8-B stores, float4 bias).
+//  * XCD-aware bijective workgroup remap + 4-tile-row grouping.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace kiosk {
+namespace {
+
+constexpr int BM = 256, BN = 256, BKH = 32;
+constexpr int kThreads = 512;
+constexpr int kRowBytes = BKH * 2;                 // 64 B per row per half
+constexpr int kOperandBytes = BM * kRowBytes;      // 16 KiB
+constexpr int kSlotBytes = 2 * kOperandBytes;      // A + B = 32 KiB
+constexpr int kSlots = 4;
+constexpr int kLdsBytes = kSlots * kSlotBytes;     // 128 KiB
+constexpr int kGroupM = 4;
+constexpr int kLoadsPerHalf = 4;                   // glds per wave per half
+
+__device__ __forceinline__ int slot_off(int r, int c) {
+  return r * kRowBytes + ((c ^ ((r >> 2) & 3)) << 4);
+}
+
+// 16 KiB operand half = 16 x 1 KiB DMA pieces (16 rows x 64 B); wave w
+// issues pieces 2w and 2w+1.
+__device__ __forceinline__ void stage_operand(const uint16_t* __restrict__ g,
+                                              int ld, int row0, int rows,
+                                              int k0, char* lds, int wave,
+                                              int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wave * 2 + i;
+    const int r = piece * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ ((r >> 2) & 3);
+    int grow = row0 + r;
+    grow = grow < rows ? grow : rows - 1;
+    glds16(g + static_cast<size_t>(grow) * ld + k0 + c * 8,
+           lds + piece * 1024);
+  }
+}
+
+__device__ __forceinline__ void wait_ring(int halves_in_flight) {
+  // vmcnt immediates must be literals
+  if (halves_in_flight >= 2) {
+    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+  } else if (halves_in_flight == 1) {
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+    uint16_t* __restrict__ C, const float* __restrict__ bias,
+    const uint16_t* __restrict__ R, int M, int N, int K) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int wg = xcd_remap(static_cast<int>(blockIdx.x), tiles_m * tiles_n);
+  const int per_group = kGroupM * tiles_n;
+  const int group = wg / per_group;
+  const int first_m = group * kGroupM;
+  const int gsize = min(tiles_m - first_m, kGroupM);
+  const int in_group = wg - group * per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int halves = K / BKH;
+  auto stage = [&](int h) {
+    char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
+    stage_operand(A, K, m0, M, h * BKH, slot, wave, lane);
+    stage_operand(B, K, n0, N, h * BKH, slot + kOperandBytes, wave, lane);
+  };
+  stage(0);
+  if (halves > 1) stage(1);
+  if (halves > 2) stage(2);
+  wait_ring(min(halves, 3) - 1);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  const int arow = wm * 128 + (lane & 15);
+  const int brow = wn * 64 + (lane & 15);
+  const int chunk = lane >> 4;
+  for (int h = 0; h < halves; ++h) {
+    if (h + 3 < halves) stage(h + 3);
+    const char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
+    // all 12 fragment reads first (48 VGPRs), so their LDS latency
+    // overlaps instead of serialising one lgkmcnt(0) per 4 MFMAs
+    bf16x8 wb[4], xa[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      wb[j] = *reinterpret_cast<const bf16x8*>(
+          slot + kOperandBytes + slot_off(brow + j * 16, chunk));
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      xa[i] = *reinterpret_cast<const bf16x8*>(
+          slot + slot_off(arow + i * 16, chunk));
+    // keep hipcc from sinking each read next to its first MFMA; it then
+    // emits counted lgkmcnt(N) waits as the fragments arrive in order
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            wb[j], xa[i], acc[i][j], 0, 0, 0);
+    if (h + 1 < halves) {
+      __builtin_amdgcn_sched_barrier(0);
+      wait_ring(min(h + 4, halves) - (h + 2));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nb = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (EPI != EPI_NONE) {
+        const float4 b = *reinterpret_cast<const float4*>(bias + nb);
+        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+      }
+      if (EPI == EPI_BIAS_GELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+      }
+      const size_t off = static_cast<size_t>(m) * N + nb;
+      if (EPI == EPI_BIAS_RESIDUAL) {
+        const uint2 res = *reinterpret_cast<const uint2*>(R + off);
+        v[0] += bf16_to_f32(res.x & 0xffff);
+        v[1] += bf16_to_f32(res.x >> 16);
+        v[2] += bf16_to_f32(res.y & 0xffff);
+        v[3] += bf16_to_f32(res.y >> 16);
+      }
+      uint2 out;
+      out.x = f32_to_bf16(v[0]) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+      out.y = f32_to_bf16(v[2]) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+      *reinterpret_cast<uint2*>(C + off) = out;
+    }
+  }
+}
+
+template <int EPI>
+hipError_t configure256() {
+  return hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&gemm256_kernel<EPI>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+}
+
+}  // namespace
+
+hipError_t gemm256_prepare() {
+  hipError_t err = configure256<EPI_NONE>();
+  if (err == hipSuccess) err = configure256<EPI_BIAS_GELU>();
+  if (err == hipSuccess) err = configure256<EPI_BIAS_RESIDUAL>();
+  return err;
+}
+
+bool gemm256_shape_ok(int M, int N, int K) {
+  return M >= 1 && N % BN == 0 && N >= BN && K % BKH == 0 && K >= BKH;
+}
+
+hipError_t launch_gemm256(const uint16_t* A, const uint16_t* B, uint16_t* C,
+                          const float* bias, const uint16_t* R, int M, int N,
+                          int K, int epilogue, hipStream_t stream) {
+  if (!gemm256_shape_ok(M, N, K)) return hipErrorInvalidValue;
+  const int blocks = ((M + BM - 1) / BM) * (N / BN);
+  switch (epilogue) {
+    case EPI_NONE:
+      hipLaunchKernelGGL(gemm256_kernel<EPI_NONE>, dim3(blocks),
+                         dim3(kThreads), kLdsBytes, stream, A, B, C, bias, R,
+                         M, N, K);
+      break;
+    case EPI_BIAS_GELU:
+      hipLaunchKernelGGL(gemm256_kernel<EPI_BIAS_GELU>, dim3(blocks),
+                         dim3(kThreads), kLdsBytes, stream, A, B, C, bias, R,
+                         M, N, K);
+      break;
+    case EPI_BIAS_RESIDUAL:
+      hipLaunchKernelGGL(gemm256_kernel<EPI_BIAS_RESIDUAL>, dim3(blocks),
+                         dim3(kThreads), kLdsBytes, stream, A, B, C, bias, R,
+                         M, N, K);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kiosk

@@ -60,6 +60,12 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
     check_hip(launch_gemm(a, b, c, bias, r, 128, 128, 128, epi, stream),
               "preinit gemm");
   }
+  // the 256x256 ring kernel needs a 256-wide operand: reuse the buffers
+  // as [128 x 256] / [256 x 64] views (N = 256, K = 64)
+  for (int epi = 0; epi < 3; ++epi) {
+    check_hip(launch_gemm256(a, b, c, bias, r, 64, 256, 64, epi, stream),
+              "preinit gemm256");
+  }
   check_hip(launch_partial_sums(c, elems, sums, stream), "preinit sums");
   check_hip(launch_warmstart(a, elems, rec, 1, 1, 2 * kGemmLdsBytes, stream),
             "preinit warmstart");
@@ -257,11 +263,13 @@ void Engine::enqueue_forward(int rows) {
   uint16_t* cur = x_;
   uint16_t* nxt = y_;
   for (int l = 0; l < layers_; ++l) {
-    launch_or_throw(launch_gemm(cur, w1_[l], h_, b1_[l], nullptr, rows,
-                                hidden_, dim_, EPI_BIAS_GELU, stream_),
+    launch_or_throw(launch_gemm_variant(cur, w1_[l], h_, b1_[l], nullptr, rows,
+                                        hidden_, dim_, EPI_BIAS_GELU,
+                                        GEMM_AUTO, stream_),
                     "gemm1");
-    launch_or_throw(launch_gemm(h_, w2_[l], nxt, b2_[l], cur, rows, dim_,
-                                hidden_, EPI_BIAS_RESIDUAL, stream_),
+    launch_or_throw(launch_gemm_variant(h_, w2_[l], nxt, b2_[l], cur, rows,
+                                        dim_, hidden_, EPI_BIAS_RESIDUAL,
+                                        GEMM_AUTO, stream_),
                     "gemm2");
     std::swap(cur, nxt);
   }

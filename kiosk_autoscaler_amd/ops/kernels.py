@@ -24,11 +24,17 @@ def _check_bf16(t, name):
         raise ValueError('%s must be a contiguous bf16 CUDA tensor' % name)
 
 
-def gemm(a, b, bias=None, residual=None, epilogue='none', out=None):
+VARIANTS = {'auto': 0, '128': 1, '256': 2}
+
+
+def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
+         variant='auto'):
     """``epi(a @ b.T)`` with a: [M, K], b: [N, K] (bf16) -> [M, N] bf16.
 
     ``epilogue``: ``'none'``, ``'gelu'`` (``gelu_tanh(a@b.T + bias)``) or
-    ``'residual'`` (``a@b.T + bias + residual``)."""
+    ``'residual'`` (``a@b.T + bias + residual``).  ``variant``: ``'auto'``
+    (256x256 LDS-ring kernel when the grid fills the chip, else 128x128),
+    ``'128'`` or ``'256'``."""
     import torch
     mod = native.load()
     _check_bf16(a, 'a')
@@ -40,6 +46,8 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None):
     if not mod.gemm_shape_ok(M, N, K):
         raise ValueError('unsupported GEMM shape M=%d N=%d K=%d (need N %% 128'
                          ' == 0, K %% 64 == 0)' % (M, N, K))
+    if variant == '256' and N % 256:
+        raise ValueError('the 256x256 kernel needs N %% 256 == 0')
     epi = EPILOGUES[epilogue]
     if epi and (bias is None or bias.dtype != torch.float32
                 or bias.numel() != N or not bias.is_contiguous()):
@@ -53,7 +61,7 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None):
     mod.gemm(a.data_ptr(), b.data_ptr(), out.data_ptr(),
              bias.data_ptr() if bias is not None else 0,
              residual.data_ptr() if residual is not None else 0,
-             M, N, K, epi, _stream())
+             M, N, K, epi, _stream(), VARIANTS[variant])
     return out
 
 

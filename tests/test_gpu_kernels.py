@@ -166,3 +166,39 @@ def test_fence_warmup_and_preinit(mod):
     assert ms > 0
     stages = mod.preinit_device(0)
     assert list(stages) == ['preinit_enter', 'preinit_context', 'preinit_done']
+
+
+@pytest.mark.parametrize('M,N,K', [(256, 256, 32), (300, 512, 96),
+                                   (2048, 1024, 4096), (1, 256, 64)])
+@pytest.mark.parametrize('epilogue', ['none', 'gelu', 'residual'])
+def test_gemm256_ring_kernel(mod, M, N, K, epilogue):
+    """The 256x256 LDS-ring kernel against the fp32 reference (odd halves
+    counts exercise the vmcnt(4)/vmcnt(0) ring tails)."""
+    from kiosk_autoscaler_amd.ops import kernels
+    a = rand_bf16(M, K, seed=11)
+    b = rand_bf16(N, K, scale=0.1, seed=12)
+    bias = torch.randn(N, device='cuda')
+    res = rand_bf16(M, N, seed=13)
+    ref = a.float() @ b.float().t()
+    if epilogue != 'none':
+        ref = ref + bias
+    if epilogue == 'gelu':
+        ref = gelu_tanh(ref)
+    if epilogue == 'residual':
+        ref = ref + res.float()
+    c = kernels.gemm(a, b, bias=bias, residual=res, epilogue=epilogue,
+                     variant='256')
+    torch.testing.assert_close(c.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+def test_gemm256_identity(mod):
+    from kiosk_autoscaler_amd.ops import kernels
+    M = K = 512
+    N = 768
+    a = torch.eye(M, K, device='cuda', dtype=torch.bfloat16)
+    b = (torch.arange(N * K, device='cuda', dtype=torch.float32)
+         .reshape(N, K) % 241 - 120).to(torch.bfloat16)
+    c = kernels.gemm(a, b, variant='256')
+    assert torch.equal(c, b.t().contiguous()[:M])
+    assert mod.gemm_pick_variant(2048, 16384, 4096) == 2
+    assert mod.gemm_pick_variant(2048, 4096, 16384) == 1

@@ -33,7 +33,10 @@ def main():
             kernels.gemm(a, b, bias=bias, epilogue='gelu', out=out)
 
         def ours_plain():
-            kernels.gemm(a, b, out=out)
+            kernels.gemm(a, b, out=out, variant='128')
+
+        def ours_256():
+            kernels.gemm(a, b, out=out, variant='256')
 
         def theirs():
             torch.nn.functional.gelu(torch.addmm(bias.to(torch.bfloat16), a,
@@ -42,8 +45,10 @@ def main():
         def theirs_plain():
             torch.matmul(a, b.t(), out=out)
 
-        fns = {'native_gelu': ours, 'native': ours_plain,
+        fns = {'native_gelu_auto': ours, 'native128': ours_plain,
                'torch_gelu': theirs, 'torch': theirs_plain}
+        if N % 256 == 0:
+            fns['native256'] = ours_256
         results = {k: [] for k in fns}
         for fn in fns.values():
             fn()
@@ -60,10 +65,14 @@ def main():
                 ms = start.elapsed_time(end) / args.iters
                 results[name].append(2.0 * M * N * K / (ms * 1e-3) / 1e12)
         ref = (a.float() @ b.float().t())
-        ours_plain()
-        torch.cuda.synchronize()
-        err = (out.float() - ref).abs().max().item()
-        summary = {'shape': [M, N, K], 'max_abs_err': err}
+        summary = {'shape': [M, N, K]}
+        for name, fn in (('128', ours_plain), ('256', ours_256)):
+            if name == '256' and N % 256:
+                continue
+            out.zero_()
+            fn()
+            torch.cuda.synchronize()
+            summary['max_abs_err_' + name] = (out.float() - ref).abs().max().item()
         for name, vals in results.items():
             vals.sort()
             summary[name + '_tflops_median'] = round(vals[len(vals) // 2], 1)
