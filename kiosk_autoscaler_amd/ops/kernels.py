@@ -43,11 +43,13 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
     N, K2 = b.shape
     if K != K2:
         raise ValueError('inner dimensions differ: %d vs %d' % (K, K2))
-    if not mod.gemm_shape_ok(M, N, K):
+    if variant == '256':
+        if M < 1 or N % 256 or K % 32 or K < 32:
+            raise ValueError('the 256x256 kernel needs N %% 256 == 0 and '
+                             'K %% 32 == 0 (M=%d N=%d K=%d)' % (M, N, K))
+    elif not mod.gemm_shape_ok(M, N, K):
         raise ValueError('unsupported GEMM shape M=%d N=%d K=%d (need N %% 128'
                          ' == 0, K %% 64 == 0)' % (M, N, K))
-    if variant == '256' and N % 256:
-        raise ValueError('the 256x256 kernel needs N %% 256 == 0')
     epi = EPILOGUES[epilogue]
     if epi and (bias is None or bias.dtype != torch.float32
                 or bias.numel() != N or not bias.is_contiguous()):
