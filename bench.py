@@ -117,6 +117,7 @@ class Services(object):
             'KEYS_PER_POD': str(args.kpp), 'INTERVAL': str(args.interval),
             'SCALE_POLICY': args.policy,
             'SCALE_DOWN_DELAY': str(args.scale_down_delay),
+            'IDLE_INTERVAL': str(args.idle_interval),
             'GPU_IDS': ','.join(str(i) for i in range(self.n)),
             'WORKER_BACKEND': args.backend, 'WARM_POOL': str(self.n),
             'FENCE': args.fence, 'MODEL_DIM': str(args.dim),
@@ -260,6 +261,9 @@ def parse_args():
     p.add_argument('--kpp', type=int, default=1)
     p.add_argument('--policy', default='reference')
     p.add_argument('--scale-down-delay', type=float, default=0.0)
+    p.add_argument('--idle-interval', type=float, default=0.0,
+                   help='opt-in fast poll while at zero workers (changes the '
+                        "reference's INTERVAL semantics; reported separately)")
     p.add_argument('--resource-type', default='deployment')
     p.add_argument('--backend', default='hip')
     p.add_argument('--fence', default='auto')
@@ -371,6 +375,7 @@ def main():
                     'on_s': args.on, 'service_s': args.service_ms / 1e3,
                     'max_pods': args.gpus, 'keys_per_pod': args.kpp,
                     'policy': args.policy, 'resource_type': args.resource_type,
+                    'idle_interval_s': args.idle_interval,
                 },
                 'gpu_idle_pct': _r(summary['gpu_idle_pct']),
                 'baseline_gpu_idle_pct': BASELINE_IDLE_PCT,

@@ -142,6 +142,7 @@ EXTRA_DEFAULTS = (
     ('SCALE_POLICY', str, 'reference'),     # reference | strict
     ('SCALE_DOWN_DELAY', float, 0.0),       # strict: idle grace seconds
     ('FIXED_RATE', bool, False),            # tick every INTERVAL (not tick+INTERVAL)
+    ('IDLE_INTERVAL', float, 0.0),          # opt-in faster poll while at 0 pods
     ('GPU_IDS', str, ''),                   # '' = all visible GPUs
     ('GPUMGR', str, 'embedded'),            # embedded | unix:<path>
     ('WORKER_MODULE', str, 'kiosk_autoscaler_amd.worker.main'),

@@ -90,7 +90,8 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
     fence = settings.FENCE not in ('none', 'off')
     manager = GpuManager(slots, redis_client=redis_client, pool_size=pool,
                          pool_template=template, events=events, fence=fence,
-                         pool_mode=settings.WARM_POOL_MODE)
+                         pool_mode=settings.WARM_POOL_MODE,
+                         state_ttl=settings.STATE_TTL)
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

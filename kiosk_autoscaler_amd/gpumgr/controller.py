@@ -51,6 +51,7 @@ STARTING, READY, DRAINING, EXITED = 'starting', 'ready', 'draining', 'exited'
 ACTIVE_KEY = 'kiosk:active:{ns}:{name}'
 WORKER_KEY = 'kiosk:worker:{id}'
 POOL_KEY = 'kiosk:pool'
+STATE_KEY = 'kiosk:gpumgr:{ns}:{kind}:{name}'
 
 
 class WorkerTemplate(object):
@@ -221,13 +222,14 @@ class GpuManager(object):
 
     def __init__(self, slots, redis_client=None, pool_size=0,
                  pool_template=None, events=None, fence=True,
-                 pool_mode='device',
+                 pool_mode='device', state_ttl=3600,
                  fence_timeout=60.0, max_restart_backoff=10.0):
         self.slots = list(slots)
         self.redis = redis_client
         self.pool_size = max(0, int(pool_size))
         self.pool_template = pool_template
         self.pool_mode = pool_mode
+        self.state_ttl = int(state_ttl)
         self.events = events if events is not None else NULL_EVENTS
         self.fence_enabled = fence
         self.fence_timeout = fence_timeout
@@ -246,16 +248,98 @@ class GpuManager(object):
     # ------------------------------------------------------------------
     # API (the kubernetes AppsV1Api / BatchV1Api analogs)
     # ------------------------------------------------------------------
-    def register(self, kind, namespace, name, template):
+    def register(self, kind, namespace, name, template, restore=True):
+        """Create (or update the template of) a managed resource.
+
+        With ``restore`` the declared count persisted by a previous manager
+        instance is re-adopted (the Deployment-survives-a-restart analog,
+        SURVEY §5.4) and in-flight items of workers that no longer exist are
+        pushed back to their queues."""
         if kind not in ('deployment', 'job'):
             raise ValueError('kind must be deployment or job, got %r' % kind)
         with self.lock:
             key = (kind, namespace, name)
             if key not in self.resources:
-                self.resources[key] = Resource(kind, namespace, name, template)
+                resource = Resource(kind, namespace, name, template)
+                self.resources[key] = resource
+                if restore:
+                    self._restore(resource)
+                    self.recover_orphans(resource)
             else:
                 self.resources[key].template = template
             return self.resources[key].view()
+
+    # ------------------------------------------------------------------
+    # checkpoint / resume
+    # ------------------------------------------------------------------
+    def _state_key(self, resource):
+        return STATE_KEY.format(ns=resource.namespace, kind=resource.kind,
+                                name=resource.name)
+
+    def _persist(self, resource):
+        if self.redis is None:
+            return
+        try:
+            key = self._state_key(resource)
+            self.redis.hset(key, mapping={
+                'declared': resource.declared,
+                'generation': resource.generation,
+                'epoch': resource.epoch,
+                'succeeded': resource.succeeded,
+                'failed': resource.failed,
+                'updated_ns': time.monotonic_ns()})
+            if self.state_ttl > 0:
+                self.redis.expire(key, self.state_ttl)
+        except Exception as err:  # pylint: disable=broad-except
+            logger.warning('could not persist manager state: %s', err)
+
+    def _restore(self, resource):
+        if self.redis is None:
+            return
+        try:
+            state = self.redis.hgetall(self._state_key(resource))
+        except Exception as err:  # pylint: disable=broad-except
+            logger.warning('could not read manager state: %s', err)
+            return
+        if not state:
+            return
+        resource.declared = int(state.get('declared', 0))
+        resource.generation = int(state.get('generation', 0))
+        resource.epoch = int(state.get('epoch', 0))
+        resource.succeeded = int(state.get('succeeded', 0))
+        resource.failed = int(state.get('failed', 0))
+        self.events.emit('state_restored', name=resource.name,
+                         declared=resource.declared)
+        logger.info('Restored %s %s: declared=%d generation=%d.',
+                    resource.kind, resource.name, resource.declared,
+                    resource.generation)
+
+    def recover_orphans(self, resource):
+        """Requeue ``processing-<q>:<resource>-g*`` items whose worker is
+        not one of ours (a previous manager instance died with them)."""
+        if self.redis is None:
+            return 0
+        moved = 0
+        live = set(resource.workers)
+        for queue in resource.template.queues:
+            pattern = 'processing-%s:%s-g*' % (queue, resource.name)
+            try:
+                for key in list(self.redis.scan_iter(match=pattern,
+                                                     count=1000)):
+                    wid = key.split(':', 1)[1].split('.', 1)[0]
+                    if wid in live:
+                        continue
+                    while self.redis.rpoplpush(key, queue) is not None:
+                        moved += 1
+                    self.redis.delete(key)
+            except Exception as err:  # pylint: disable=broad-except
+                logger.error('orphan recovery failed: %s', err)
+        if moved:
+            self.events.emit('orphans_requeued', name=resource.name,
+                             items=moved)
+            logger.warning('Requeued %d orphaned in-flight items of %s.',
+                           moved, resource.name)
+        return moved
 
     def _list(self, kind, namespace):
         with self.lock:
@@ -282,6 +366,7 @@ class GpuManager(object):
                                name, declared, len(self.slots))
             resource.declared = declared
             resource.generation += 1
+            self._persist(resource)
             self.events.emit('patch', kind=kind, name=name, declared=declared)
             self._reconcile(resource)
             view = resource.view()
@@ -632,6 +717,7 @@ class GpuManager(object):
                            requeued, delay)
         if was_ready:
             resource.fence_wanted = True
+        self._persist(resource)
         if self.redis is not None:
             try:
                 self.redis.delete(WORKER_KEY.format(id=worker.id))

@@ -104,3 +104,16 @@ def test_logger_format_and_rotation(tmp_path):
         for handler in root.handlers[len(saved):]:
             root.removeHandler(handler)
             handler.close()
+
+
+def test_idle_interval_fast_path():
+    scaler = mock.Mock()
+    decisions = iter([0, 0, 1, 0])
+
+    def tick(**kwargs):
+        scaler.last_decision = next(decisions)
+    scaler.scale.side_effect = tick
+    sleeps = []
+    cli.run_loop(scaler, _settings(INTERVAL=5, IDLE_INTERVAL=0.25),
+                 max_ticks=4, sleep=sleeps.append, clock=lambda: 0.0)
+    assert sleeps == [0.25, 0.25, 5]

@@ -165,3 +165,32 @@ def test_hbm_sizing():
                                  hbm_bytes=w + (8 << 30) + 3 * per) == 3
     assert hbm.size_keys_per_pod(64, 4096, 16384, 4, 2048, hbm_bytes=1) == 1
     assert os.getpid() == hbm.report(8, 16, 1, 2)['pid']
+
+
+def test_state_persist_restore_and_orphans():
+    redis = FakeRedis()
+    slots = [gpus.GpuSlot(i, '', kind='cpu') for i in range(2)]
+    tpl = gpumgr.WorkerTemplate(queues=['q'], backend='cpu')
+    first = gpumgr.GpuManager(slots, redis_client=redis, fence=False)
+    first.register('deployment', 'ns', 'w', tpl)
+    with first.lock:
+        res = first.resources[('deployment', 'ns', 'w')]
+        res.declared = 2
+        res.generation = 5
+        first._persist(res)
+    state = redis.hgetall('kiosk:gpumgr:ns:deployment:w')
+    assert state['declared'] == '2' and 0 < redis.ttl(
+        'kiosk:gpumgr:ns:deployment:w') <= 3600
+    # a dead manager left in-flight items behind
+    redis.rpush('processing-q:w-g0-3', 'job-a')
+    redis.rpush('processing-q:w-g1-4.1', 'job-b')
+    redis.rpush('processing-q:other-g0-1', 'not-ours')
+    second = gpumgr.GpuManager(slots, redis_client=redis, fence=False)
+    second.register('deployment', 'ns', 'w', tpl)
+    view = second.list_namespaced_deployment('ns').items[0]
+    assert view.spec.replicas == 2 and view.metadata.generation == 5
+    assert sorted(redis.lrange('q', 0, -1)) == ['job-a', 'job-b']
+    assert redis.lrange('processing-q:other-g0-1', 0, -1) == ['not-ours']
+    third = gpumgr.GpuManager(slots, redis_client=redis, fence=False)
+    third.register('deployment', 'ns', 'w', tpl, restore=False)
+    assert third.list_namespaced_deployment('ns').items[0].spec.replicas == 0
