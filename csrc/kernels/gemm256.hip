@@ -9,11 +9,13 @@
 //
 //  * K is consumed in 32-deep halves; a 4-slot LDS ring (4 x 32 KiB =
 //    128 KiB, one block per CU) holds A[256][32] + B[256][32] per slot.
-//  * at half-step h the block issues the LDS-DMA (global_load_lds_dwordx4)
-//    of half h+3, runs 32 MFMAs per wave on half h, then waits with a
-//    *counted* `s_waitcnt vmcnt(8|4|0)` -- only half h+1 must have landed,
-//    halves h+2 and h+3 stay in flight -- and a raw s_barrier (never
-//    __syncthreads, whose implicit vmcnt(0) would drain the ring).
+//  * at half-step h (its fragments already in registers) every wave waits
+//    with a *counted* `s_waitcnt vmcnt(8)` -- only half h+1 must have
+//    landed, halves h+2 and h+3 stay in flight -- and a raw s_barrier
+//    (never __syncthreads, whose implicit vmcnt(0) would drain the ring),
+//    restages the slot half h came from with half h+4 (LDS-DMA,
+//    global_load_lds_dwordx4), issues the ds_reads of half h+1 into a second
+//    register set and runs the 32 MFMAs of half h under them.
 //  * 64-B LDS rows, 16-B chunk c of row r stored at chunk c ^ ((r>>2)&3):
 //    the 16 rows a 16-lane group reads at one k-chunk cover all 16 bank
 //    slots (conflict-free ds_read_b128); the swizzle is applied on the DMA
@@ -60,16 +62,13 @@ __device__ __forceinline__ void stage_operand(const uint16_t* __restrict__ g,
   }
 }
 
-__device__ __forceinline__ void wait_ring(int halves_in_flight) {
-  // vmcnt immediates must be literals
-  if (halves_in_flight >= 2) {
-    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-  } else if (halves_in_flight == 1) {
-    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  }
-}
+// Counted waits go through the builtin (not inline asm) so hipcc's waitcnt
+// pass sees them and adds no conservative lgkmcnt(0) of its own.  gfx9
+// encoding: vmcnt[3:0] | expcnt[6:4] (7 = no wait) | lgkmcnt[11:8] |
+// vmcnt[15:14].  kLoadsPerHalf DMA instructions per wave per half.
+constexpr int kWaitHalf1 = 0x0070 | (kLoadsPerHalf * 3);   // vmcnt(12) lgkm(0)
+constexpr int kWaitHalf2 = 0x0070 | (kLoadsPerHalf * 2);   // vmcnt(8)  lgkm(0)
+constexpr int kWaitAll = 0x0070;                           // vmcnt(0)  lgkm(0)
 
 template <int EPI>
 __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(
@@ -99,27 +98,20 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int halves = K / BKH;
+  // Stage half h into its ring slot.  Past the end the source is clamped to
+  // the last half (an L2 hit into a slot nobody reads again), so the
+  // pipeline has the same shape -- and the same counted wait -- every step.
   auto stage = [&](int h) {
     char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
-    stage_operand(A, K, m0, M, h * BKH, slot, wave, lane);
-    stage_operand(B, K, n0, N, h * BKH, slot + kOperandBytes, wave, lane);
+    const int k0 = min(h, halves - 1) * BKH;
+    stage_operand(A, K, m0, M, k0, slot, wave, lane);
+    stage_operand(B, K, n0, N, k0, slot + kOperandBytes, wave, lane);
   };
-  stage(0);
-  if (halves > 1) stage(1);
-  if (halves > 2) stage(2);
-  wait_ring(min(halves, 3) - 1);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-
   const int arow = wm * 128 + (lane & 15);
   const int brow = wn * 64 + (lane & 15);
   const int chunk = lane >> 4;
-  for (int h = 0; h < halves; ++h) {
-    if (h + 3 < halves) stage(h + 3);
+  auto read_frags = [&](int h, bf16x8 (&wb)[4], bf16x8 (&xa)[8]) {
     const char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
-    // all 12 fragment reads first (48 VGPRs), so their LDS latency
-    // overlaps instead of serialising one lgkmcnt(0) per 4 MFMAs
-    bf16x8 wb[4], xa[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       wb[j] = *reinterpret_cast<const bf16x8*>(
@@ -128,22 +120,48 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(
     for (int i = 0; i < 8; ++i)
       xa[i] = *reinterpret_cast<const bf16x8*>(
           slot + slot_off(arow + i * 16, chunk));
-    // keep hipcc from sinking each read next to its first MFMA; it then
-    // emits counted lgkmcnt(N) waits as the fragments arrive in order
-    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mma = [&](const bf16x8 (&wb)[4], const bf16x8 (&xa)[8]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
             wb[j], xa[i], acc[i][j], 0, 0, 0);
-    if (h + 1 < halves) {
-      __builtin_amdgcn_sched_barrier(0);
-      wait_ring(min(h + 4, halves) - (h + 2));
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
+  };
+  // Software pipeline, per half-step h (fragments of half h already in
+  // registers; halves h+1..h+3 staged): wait until half h+1 has landed
+  // (h+2, h+3 stay in flight) + barrier -- after it no wave still reads the
+  // slot of half h -- restage that slot with half h+4, issue the LDS reads
+  // of half h+1 into the other register set, and run the 32 MFMAs of half
+  // h while the reads and the DMA are in flight.  Branch-free on purpose: a
+  // control-flow join between the reads and the MFMAs makes the waitcnt
+  // pass drain lgkmcnt first, which serialises the two.
+  auto step = [&](int h, const bf16x8 (&wb)[4], const bf16x8 (&xa)[8],
+                  bf16x8 (&wb_next)[4], bf16x8 (&xa_next)[8]) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kWaitHalf2);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    stage(h + 4);
+    read_frags(h + 1, wb_next, xa_next);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(wb, xa);
+  };
+
+#pragma unroll
+  for (int h = 0; h < kSlots; ++h) stage(h);
+  __builtin_amdgcn_s_waitcnt(kWaitHalf1);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  bf16x8 wb0[4], xa0[8], wb1[4], xa1[8];
+  read_frags(0, wb0, xa0);
+  for (int h = 0; h < halves; h += 2) {
+    step(h, wb0, xa0, wb1, xa1);
+    if (h + 1 < halves) step(h + 1, wb1, xa1, wb0, xa0);
   }
+  // drain the tail DMAs before the workgroup's LDS can be released
+  __builtin_amdgcn_s_waitcnt(kWaitAll);
 
 #pragma unroll
   for (int i = 0; i < 8; ++i) {

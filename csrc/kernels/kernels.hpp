@@ -60,6 +60,11 @@ constexpr int kSumBlocks = 1024;
 hipError_t launch_partial_sums(const uint16_t* p, size_t n, float* partials,
                                hipStream_t stream);
 
+// Bounded GPU stall for fault injection: one wave sleeping `ms`
+// (clamped to kSpinMaxMs) of wall clock, then *done = 1 (if non-null).
+constexpr double kSpinMaxMs = 30000.0;
+hipError_t launch_spin(double ms, unsigned int* done, hipStream_t stream);
+
 // N1 warm-start: one workgroup per CU (LDS request > half the CU's LDS
 // keeps two from sharing a CU); zeroes `lds_bytes` of LDS, streams a slice
 // of `w` (n elements), runs `iters` MFMA steps and records per-WG

@@ -93,6 +93,19 @@ __global__ __launch_bounds__(256) void partial_sums_kernel(
   }
 }
 
+// Fault injection (utils/faults.py "hang_key"): one wave that sleeps until
+// `ticks` of the 100 MHz s_memrealtime clock have passed -- a stuck kernel
+// as the manager's watchdog sees it, but one that always terminates (the
+// host clamps ticks), so the grid drains even if nobody kills the process.
+__global__ __launch_bounds__(64) void spin_kernel(unsigned long long ticks,
+                                                  unsigned int* done) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+    __builtin_amdgcn_s_sleep(127);
+  }
+  if (threadIdx.x == 0 && done) *done = 1u;
+}
+
 int init_blocks(size_t n) {
   const size_t chunks = (n + 7) / 8;
   size_t blocks = (chunks + kInitThreads - 1) / kInitThreads;
@@ -130,6 +143,15 @@ hipError_t launch_partial_sums(const uint16_t* p, size_t n, float* partials,
                                hipStream_t stream) {
   hipLaunchKernelGGL(partial_sums_kernel, dim3(kSumBlocks), dim3(256),
                      4 * sizeof(float), stream, p, n, partials);
+  return hipGetLastError();
+}
+
+hipError_t launch_spin(double ms, unsigned int* done, hipStream_t stream) {
+  if (!(ms >= 0.0)) return hipErrorInvalidValue;
+  ms = ms > kSpinMaxMs ? kSpinMaxMs : ms;
+  const unsigned long long ticks =
+      static_cast<unsigned long long>(ms * 1e5);   // 100 MHz
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, stream, ticks, done);
   return hipGetLastError();
 }
 

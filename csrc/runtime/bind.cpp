@@ -10,6 +10,7 @@
 #include "../kernels/kernels.hpp"
 #include "engine.hpp"
 #include "fence.hpp"
+#include "trace.hpp"
 
 namespace py = pybind11;
 using kiosk::check_hip;
@@ -144,6 +145,14 @@ PYBIND11_MODULE(_kiosk_hip, m) {
       py::arg("device") = 0);
   m.def("synchronize", [] { check_hip(hipDeviceSynchronize(), "sync"); },
         py::call_guard<py::gil_scoped_release>());
+  m.def("roctx_available", &kiosk::roctx_available);
+  m.def("roctx_push", [](const std::string& name) {
+    kiosk::roctx_push(name.c_str());
+  });
+  m.def("roctx_pop", &kiosk::roctx_pop);
+  m.def("roctx_mark", [](const std::string& name) {
+    kiosk::roctx_mark(name.c_str());
+  });
 
   py::class_<kiosk::Engine>(m, "Engine")
       .def(py::init<int, int, int, int, int, unsigned long long>(),
@@ -176,6 +185,8 @@ PYBIND11_MODULE(_kiosk_hip, m) {
             return fwd_to_dict(r);
           },
           py::arg("rows"), py::arg("passes") = 1, py::arg("seed") = 0)
+      .def("spin", &kiosk::Engine::spin, py::arg("ms"),
+           py::call_guard<py::gil_scoped_release>())
       .def("close", &kiosk::Engine::close,
            py::call_guard<py::gil_scoped_release>())
       .def("stage_times",

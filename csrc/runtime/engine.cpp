@@ -9,6 +9,7 @@
 #include <set>
 
 #include "../kernels/kernels.hpp"
+#include "trace.hpp"
 
 namespace kiosk {
 
@@ -30,6 +31,7 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 }  // namespace
 
 std::vector<std::pair<std::string, long long>> preinit_device(int device) {
+  TraceRange range("kiosk.preinit");
   std::vector<std::pair<std::string, long long>> stages;
   stages.emplace_back("preinit_enter", monotonic_ns());
   check_hip(hipSetDevice(device), "hipSetDevice");
@@ -199,6 +201,7 @@ void Engine::close() {
 
 WarmStartResult Engine::warmstart(int iters, int lds_bytes) {
   if (closed_) throw std::runtime_error("engine closed");
+  TraceRange range("kiosk.warmstart");
   WarmStartResult r;
   r.blocks = cu_count_;
   r.iters = iters;
@@ -278,12 +281,22 @@ void Engine::enqueue_forward(int rows) {
                   "partial sums");
 }
 
+double Engine::spin(double ms) {
+  if (closed_) throw std::runtime_error("engine closed");
+  TraceRange range("kiosk.fault.spin");
+  const long long t0 = monotonic_ns();
+  check_hip(launch_spin(ms, nullptr, stream_), "launch_spin");
+  check_hip(hipStreamSynchronize(stream_), "spin sync");
+  return (monotonic_ns() - t0) / 1e6;
+}
+
 void Engine::prepare(int rows) {
   if (closed_) throw std::runtime_error("engine closed");
   if (rows < 1 || rows > max_rows_) {
     throw std::invalid_argument("rows out of range for this engine");
   }
   if (graphs_.count(rows)) return;
+  TraceRange range("kiosk.graph_capture");
   if (graphs_.size() >= 16) {
     auto victim = graphs_.begin();
     hipGraphExecDestroy(victim->second.second);
@@ -318,6 +331,7 @@ ForwardResult Engine::forward(int rows, int passes, unsigned long long seed) {
   r.passes = std::max(1, passes);
   const long long t0 = monotonic_ns();
   prepare(rows);
+  TraceRange range("kiosk.forward");
   auto exec = graphs_[rows].second;
   *seed_host_ = seed;
   check_hip(hipMemcpyAsync(seed_dev_, seed_host_, 8, hipMemcpyHostToDevice,

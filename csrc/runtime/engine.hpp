@@ -55,6 +55,8 @@ class Engine {
   WarmStartResult warmstart(int iters, int lds_bytes);
   void prepare(int rows);                      // capture + instantiate graph
   ForwardResult forward(int rows, int passes, unsigned long long seed);
+  // fault injection: stall the engine's stream for `ms` (bounded kernel)
+  double spin(double ms);
   void close();
 
   const std::vector<std::pair<std::string, long long>>& stages() const {

@@ -12,6 +12,7 @@
 #include <thread>
 
 #include "engine.hpp"
+#include "trace.hpp"
 
 namespace kiosk {
 
@@ -156,6 +157,7 @@ void Fence::wait_ready(void* comm, double timeout_s, const char* what) {
 Fence::Fence(const std::string& unique_id, int nranks, int rank,
              double timeout_s)
     : nranks_(nranks), rank_(rank), timeout_s_(timeout_s) {
+  TraceRange range("kiosk.fence.init");
   if (unique_id.size() != sizeof(ncclUniqueId)) {
     throw std::invalid_argument("unique id must be 128 bytes");
   }
@@ -194,6 +196,7 @@ std::pair<std::vector<long long>, double> Fence::allreduce(
   if (values.empty() || values.size() > 64) {
     throw std::invalid_argument("fence vector must have 1..64 entries");
   }
+  TraceRange range("kiosk.fence.allreduce");
   const size_t n = values.size();
   const double t0 = now_s();
   std::memcpy(host_, values.data(), n * sizeof(long long));
@@ -226,6 +229,7 @@ void Fence::shrink(const std::vector<int>& excluded, double timeout_s) {
   if (!rccl().CommShrink) {
     throw std::runtime_error("this RCCL has no ncclCommShrink");
   }
+  TraceRange range("kiosk.fence.shrink");
   std::vector<int> ex(excluded);
   ncclComm_t next = nullptr;
   check_nccl(rccl().CommShrink(static_cast<ncclComm_t>(comm_), ex.data(),

@@ -160,6 +160,8 @@ EXTRA_DEFAULTS = (
     ('EVENT_LOG', str, ''),                 # JSONL path | 'redis' | '' (off)
     ('TICK_KEY', str, ''),                  # publish tick times to this key
     ('STATE_TTL', int, 3600),
+    ('WORKER_TIMEOUT', float, 0.0),         # s without progress while busy -> kill (0 = off)
+    ('START_TIMEOUT', float, 0.0),          # s from assignment to READY -> kill (0 = off)
     ('DEBUG', bool, True),
     ('LOG_FILE', str, 'autoscaler.log'),
 )

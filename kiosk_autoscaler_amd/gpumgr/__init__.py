@@ -53,7 +53,8 @@ def worker_env(settings, keys_per_pod=None):
         env['EVENT_LOG'] = settings.EVENT_LOG
     for passthrough in ('PASSES_PER_KEY', 'MOCK_WORK_MS', 'WORKER_BATCH',
                         'JOB_IDLE_EXIT_S', 'POLL_BLOCK_S', 'MODEL_SEED',
-                        'KIOSK_RCCL_LIB', 'WORKER_EVENTS'):
+                        'KIOSK_RCCL_LIB', 'WORKER_EVENTS', 'KIOSK_FAULTS',
+                        'KIOSK_ROCTX'):
         if passthrough in os.environ:
             env[passthrough] = os.environ[passthrough]
     return env
@@ -91,7 +92,9 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
     manager = GpuManager(slots, redis_client=redis_client, pool_size=pool,
                          pool_template=template, events=events, fence=fence,
                          pool_mode=settings.WARM_POOL_MODE,
-                         state_ttl=settings.STATE_TTL)
+                         state_ttl=settings.STATE_TTL,
+                         worker_timeout=settings.WORKER_TIMEOUT,
+                         start_timeout=settings.START_TIMEOUT)
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

@@ -141,7 +141,7 @@ class _Process(object):
 class Worker(object):
     __slots__ = ('id', 'resource', 'slot', 'proc', 'state', 'busy',
                  't_assigned', 't_ready', 't_exit', 'exit_code', 'from_pool',
-                 'stages')
+                 'stages', 'last_beat', 'kill_reason')
 
     def __init__(self, wid, resource, slot, proc, from_pool):
         self.id = wid
@@ -156,12 +156,15 @@ class Worker(object):
         self.exit_code = None
         self.from_pool = from_pool
         self.stages = {}
+        self.last_beat = time.monotonic()   # last sign of progress
+        self.kill_reason = None
 
     def summary(self):
         return {'id': self.id, 'gpu': self.slot.index, 'pid': self.proc.pid,
                 'state': self.state, 'busy': self.busy,
                 'from_pool': self.from_pool, 't_assigned': self.t_assigned,
-                't_ready': self.t_ready, 'stages': dict(self.stages)}
+                't_ready': self.t_ready, 'stages': dict(self.stages),
+                'exit_code': self.exit_code, 'killed': self.kill_reason}
 
 
 class Resource(object):
@@ -218,12 +221,19 @@ class GpuManager(object):
         events: :class:`~kiosk_autoscaler_amd.utils.EventLog`.
         fence: run membership fences on READY-set changes.
         fence_timeout: seconds before an unacknowledged fence is abandoned.
+        worker_timeout: a *busy* worker that reports no progress (a served
+            key) for this many seconds is presumed hung -- stuck kernel,
+            deadlocked collective -- and is SIGKILLed; its in-flight items
+            are requeued like any other death (0 = off).
+        start_timeout: a worker that is not READY this long after its
+            assignment is SIGKILLed (0 = off).
     """
 
     def __init__(self, slots, redis_client=None, pool_size=0,
                  pool_template=None, events=None, fence=True,
                  pool_mode='device', state_ttl=3600,
-                 fence_timeout=60.0, max_restart_backoff=10.0):
+                 fence_timeout=60.0, max_restart_backoff=10.0,
+                 worker_timeout=0.0, start_timeout=0.0):
         self.slots = list(slots)
         self.redis = redis_client
         self.pool_size = max(0, int(pool_size))
@@ -234,6 +244,8 @@ class GpuManager(object):
         self.fence_enabled = fence
         self.fence_timeout = fence_timeout
         self.max_restart_backoff = max_restart_backoff
+        self.worker_timeout = float(worker_timeout or 0.0)
+        self.start_timeout = float(start_timeout or 0.0)
         self.resources = collections.OrderedDict()
         self.standbys = collections.OrderedDict()   # slot index -> _Process
         self.lock = threading.RLock()
@@ -480,6 +492,7 @@ class GpuManager(object):
                 else:
                     self._on_worker_messages(owner)
             self._reap_all()
+            self._watchdog()
             for resource in self.resources.values():
                 self._reconcile(resource)
                 self._maybe_fence(resource)
@@ -667,13 +680,49 @@ class GpuManager(object):
                             (worker.t_ready - worker.t_assigned) / 1e9)
             elif kind == 'busy':
                 worker.busy = True
+                worker.last_beat = time.monotonic()
+            elif kind == 'beat':
+                worker.last_beat = time.monotonic()
             elif kind == 'idle':
                 worker.busy = False
+                worker.last_beat = time.monotonic()
             elif kind == 'fenced':
                 self._on_fenced(worker.resource, message)
             elif kind == 'error':
                 logger.error('Worker %s reported: %s', worker.id,
                              message.get('message'))
+
+    def _watchdog(self):
+        """Failure detection beyond waitpid: kill workers that
+        are alive but stuck.  The kill is an ordinary death afterwards --
+        reaped, items requeued, restart backoff, fence re-run."""
+        if not (self.worker_timeout or self.start_timeout):
+            return
+        now = time.monotonic()
+        for resource in self.resources.values():
+            for worker in resource.workers.values():
+                if worker.state == EXITED or worker.kill_reason:
+                    continue
+                reason = None
+                if (self.start_timeout and worker.state == STARTING and
+                        now - worker.t_assigned / 1e9 > self.start_timeout):
+                    reason = 'not READY after %.1f s' % self.start_timeout
+                elif (self.worker_timeout and worker.busy and
+                      now - worker.last_beat > self.worker_timeout):
+                    reason = 'no progress for %.1f s' % (now -
+                                                          worker.last_beat)
+                if reason is None:
+                    continue
+                worker.kill_reason = reason
+                logger.error('Worker %s (pid %d) presumed hung: %s; '
+                             'killing it.', worker.id, worker.proc.pid,
+                             reason)
+                self.events.emit('worker_timeout', worker=worker.id,
+                                 gpu=worker.slot.index, reason=reason)
+                try:
+                    worker.proc.popen.kill()
+                except OSError:
+                    pass
 
     def _reap_all(self):
         for resource in self.resources.values():
@@ -693,7 +742,8 @@ class GpuManager(object):
 
     def _on_exit(self, resource, worker, code):
         was_ready = worker.state in (READY, DRAINING) and worker.t_ready
-        drained = worker.state == DRAINING
+        # a drained worker the watchdog had to kill still counts as failed
+        drained = worker.state == DRAINING and not worker.kill_reason
         worker.state = EXITED
         worker.exit_code = code
         worker.t_exit = time.monotonic_ns()
@@ -701,7 +751,7 @@ class GpuManager(object):
         del resource.workers[worker.id]
         self.history.append(worker.summary())
         self.events.emit('worker_exit', worker=worker.id, code=code,
-                         gpu=worker.slot.index)
+                         gpu=worker.slot.index, killed=worker.kill_reason)
         requeued = self._requeue(resource, worker)
         if resource.kind == 'job' and code == 0 and not drained:
             resource.succeeded += 1

@@ -94,6 +94,11 @@ class CpuMlpEngine(object):
         self._service_ms = float(service_ms)
         return self.forward(rows, 1, seed)
 
+    def spin(self, ms):
+        """Fault injection: a stalled device (here: the host sleeps)."""
+        time.sleep(ms / 1e3)
+        return ms
+
     def close(self):
         self.layers = []
 
@@ -156,6 +161,11 @@ class HipMlpEngine(object):
         self.pass_ms[rows] = per_pass
         total['ms'] = (time.perf_counter() - t0) * 1e3
         return total
+
+    def spin(self, ms):
+        """Fault injection: stall the serving stream with a bounded
+        spinning kernel (``csrc/kernels/misc.hip`` ``spin_kernel``)."""
+        return self.engine.spin(float(ms))
 
     def close(self):
         if self.engine is not None:

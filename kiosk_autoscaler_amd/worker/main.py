@@ -129,9 +129,14 @@ def main(argv=None):
     def engine_factory(cfg, stage):
         return create_engine(backend, cfg, stage)
 
+    faults = None
+    if os.environ.get('KIOSK_FAULTS'):
+        from ..utils.faults import FaultPlan
+        faults = FaultPlan.from_env(redis=redis_factory(),
+                                    owner=config.worker_id)
     runtime = WorkerRuntime(config, engine_factory, channel, redis_factory,
                             fence_factory=_build_fence_factory(config),
-                            event_log=events)
+                            event_log=events, faults=faults)
     code = runtime.run()
     if events is not None:
         events.emit('worker_exit_self', worker=config.worker_id,

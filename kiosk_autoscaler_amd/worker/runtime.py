@@ -20,6 +20,7 @@ import queue as queue_mod
 import time
 
 from ..redisq import exceptions as redis_errors
+from ..utils.trace import trace_range
 
 logger = logging.getLogger('Worker')
 
@@ -120,8 +121,9 @@ class WorkerRuntime(object):
     """Runs one assigned worker to completion.  Returns the exit code."""
 
     def __init__(self, config, engine_factory, channel, redis_factory,
-                 fence_factory=None, event_log=None):
+                 fence_factory=None, event_log=None, faults=None):
         self.config = config
+        self.faults = faults
         self.engine_factory = engine_factory
         self.channel = channel
         self.redis_factory = redis_factory
@@ -167,6 +169,8 @@ class WorkerRuntime(object):
             self._stage('warmstart_done')
             self._emit_event('warmstart', **{k: v for k, v in info.items()
                                              if k != 'cu_mask'})
+        if self.faults:
+            self.faults.at_start()
         t_ready = self._stage('ready')
         self.channel.emit('ready', t=t_ready, stages=self.stages)
         self._emit_event('worker_ready', gpu=cfg.slot, t_ns=t_ready,
@@ -213,7 +217,8 @@ class WorkerRuntime(object):
                 if not busy:
                     busy = True
                     self.channel.emit('busy')
-                self._process(consumer, items)
+                with trace_range('kiosk.key'):
+                    self._process(consumer, items)
                 idle_since = time.monotonic()
         finally:
             if self.fence_agent is not None:
@@ -246,6 +251,9 @@ class WorkerRuntime(object):
             jobs.append((queue, item, pkey, params, fields))
             self._emit_event('key_start', item=item, queue=queue, t_ns=t_start,
                              gpu=cfg.slot)
+        if self.faults:
+            self.faults.before_key(self.keys_done + 1, self.engine,
+                                   self.redis)
         rows = sum(p['rows'] for _, _, _, p, _ in jobs)
         passes = max(p['passes'] for _, _, _, p, _ in jobs)
         service_ms = max(p['service_ms'] for _, _, _, p, _ in jobs)
@@ -257,6 +265,13 @@ class WorkerRuntime(object):
         else:
             result = self.engine.forward(rows, passes, jobs[0][3]['seed'])
         t_done = time.monotonic_ns()
+        with trace_range('kiosk.complete'):
+            self._complete(consumer, jobs, result, t_start, t_done)
+        # liveness for the manager's watchdog (WORKER_TIMEOUT)
+        self.channel.emit('beat', keys=self.keys_done)
+
+    def _complete(self, consumer, jobs, result, t_start, t_done):
+        cfg = self.config
         for queue, item, pkey, params, fields in jobs:
             if fields:
                 self.redis.hset(item, mapping={

@@ -202,3 +202,20 @@ def test_gemm256_identity(mod):
     assert torch.equal(c, b.t().contiguous()[:M])
     assert mod.gemm_pick_variant(2048, 16384, 4096) == 2
     assert mod.gemm_pick_variant(2048, 4096, 16384) == 1
+
+
+def test_spin_kernel_and_roctx(mod):
+    engine = mod.Engine(0, 256, 512, 1, 64, 1)
+    try:
+        ms = engine.spin(50.0)
+        assert 45.0 <= ms < 2000.0, ms
+        # the engine still serves after a stall
+        out = engine.forward(64, 1, 3)
+        assert out['gpu_ms'] > 0
+    finally:
+        engine.close()
+    # roctx calls are safe whether or not a profiler is attached
+    assert isinstance(mod.roctx_available(), bool)
+    mod.roctx_push('kiosk.test')
+    mod.roctx_mark('kiosk.test.mark')
+    mod.roctx_pop()
