@@ -162,6 +162,7 @@ EXTRA_DEFAULTS = (
     ('STATE_TTL', int, 3600),
     ('WORKER_TIMEOUT', float, 0.0),         # s without progress while busy -> kill (0 = off)
     ('START_TIMEOUT', float, 0.0),          # s from assignment to READY -> kill (0 = off)
+    ('WORKER_RECYCLE', bool, True),         # drained worker -> back to the warm pool
     ('DEBUG', bool, True),
     ('LOG_FILE', str, 'autoscaler.log'),
 )

@@ -94,7 +94,8 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
                          pool_mode=settings.WARM_POOL_MODE,
                          state_ttl=settings.STATE_TTL,
                          worker_timeout=settings.WORKER_TIMEOUT,
-                         start_timeout=settings.START_TIMEOUT)
+                         start_timeout=settings.START_TIMEOUT,
+                         recycle=settings.WORKER_RECYCLE)
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

@@ -132,6 +132,7 @@ class _Process(object):
         self.t_spawn = time.monotonic_ns()
         self.booted = False
         self.eof = False
+        self.recycles = 0
 
     @property
     def pid(self):
@@ -227,13 +228,16 @@ class GpuManager(object):
             are requeued like any other death (0 = off).
         start_timeout: a worker that is not READY this long after its
             assignment is SIGKILLed (0 = off).
+        recycle: a cleanly drained worker (or a finished job worker) frees
+            its HBM and becomes its GPU's standby again, keeping the HIP
+            context -- no process re-boot before the next scale-up there.
     """
 
     def __init__(self, slots, redis_client=None, pool_size=0,
                  pool_template=None, events=None, fence=True,
                  pool_mode='device', state_ttl=3600,
                  fence_timeout=60.0, max_restart_backoff=10.0,
-                 worker_timeout=0.0, start_timeout=0.0):
+                 worker_timeout=0.0, start_timeout=0.0, recycle=True):
         self.slots = list(slots)
         self.redis = redis_client
         self.pool_size = max(0, int(pool_size))
@@ -246,6 +250,8 @@ class GpuManager(object):
         self.max_restart_backoff = max_restart_backoff
         self.worker_timeout = float(worker_timeout or 0.0)
         self.start_timeout = float(start_timeout or 0.0)
+        self.recycle = bool(recycle)
+        self.retiring = []   # recycled processes told to exit
         self.resources = collections.OrderedDict()
         self.standbys = collections.OrderedDict()   # slot index -> _Process
         self.lock = threading.RLock()
@@ -441,6 +447,8 @@ class GpuManager(object):
                          for w in r.workers.values() if w.state != EXITED]
                 alive += [p for p in self.standbys.values()
                           if p.popen.poll() is None]
+                alive += [p for p in self.retiring
+                          if p.popen.poll() is None]
             if not alive:
                 break
             if self._thread is None:
@@ -452,7 +460,7 @@ class GpuManager(object):
                 for worker in resource.workers.values():
                     if worker.proc.popen.poll() is None:
                         worker.proc.popen.kill()
-            for proc in self.standbys.values():
+            for proc in list(self.standbys.values()) + self.retiring:
                 if proc.popen.poll() is None:
                     proc.popen.kill()
         self._stop.set()
@@ -544,6 +552,10 @@ class GpuManager(object):
             if proc.popen.poll() is not None:
                 proc.pipe.close()
                 del self.standbys[index]
+        for proc in list(self.retiring):
+            if proc.popen.poll() is not None:
+                proc.pipe.close()
+                self.retiring.remove(proc)
                 changed = True
         for slot in self._free_slots()[:self.pool_size]:
             if slot.index not in self.standbys:
@@ -582,13 +594,48 @@ class GpuManager(object):
             if message is None:
                 proc.eof = True
                 continue
-            if message.get('ev') == 'standby':
-                proc.booted = True
-                self._publish_pool()
-                self.events.emit('standby_ready', pid=proc.pid,
-                                 slot=proc.slot,
-                                 boot_s=(time.monotonic_ns() - proc.t_spawn)
-                                 / 1e9, preinit=message.get('preinit'))
+            self._on_standby_message(proc, message)
+
+    def _on_standby_message(self, proc, message):
+        if message.get('ev') == 'standby':
+            proc.booted = True
+            self._publish_pool()
+            self.events.emit('standby_ready', pid=proc.pid, slot=proc.slot,
+                             boot_s=(time.monotonic_ns() - proc.t_spawn)
+                             / 1e9, preinit=message.get('preinit'),
+                             recycled=proc.role == 'standby' and
+                             proc.recycles > 0)
+
+    def _recycle_ok(self, resource):
+        tpl = self.pool_template
+        return bool(self.recycle and self.pool_size and tpl is not None and
+                    not self._stopping and
+                    resource.template.module == tpl.module and
+                    resource.template.backend == tpl.backend)
+
+    def _on_recycled(self, worker, message):
+        """A worker finished cleanly and kept its process: account for it
+        like an exit, then adopt the process as its GPU's standby."""
+        if worker.state == EXITED:
+            return
+        resource = worker.resource
+        proc = worker.proc
+        self._on_exit(resource, worker, int(message.get('code', 0)),
+                      recycled=True)
+        slot = worker.slot
+        proc.recycles += 1
+        if (self._recycle_ok(resource) and slot.index not in self.standbys
+                and len(self.standbys) < self.pool_size):
+            proc.role = 'standby'
+            proc.slot = slot.index
+            proc.booted = False     # until its 'standby' message
+            self.standbys[slot.index] = proc
+            self._publish_pool()
+            self.events.emit('worker_recycled', worker=worker.id,
+                             gpu=slot.index, pid=proc.pid)
+        else:
+            proc.pipe.send({'cmd': 'exit'})
+            self.retiring.append(proc)
 
     def _free_slots(self):
         used = set()
@@ -607,6 +654,7 @@ class GpuManager(object):
             'namespace': resource.namespace, 'resource': resource.name,
             'template': resource.template.to_dict(),
             't_assign': time.monotonic_ns(),
+            'recycle': self._recycle_ok(resource),
         }
         proc = self._take_standby(resource.template, slot)
         from_pool = proc is not None
@@ -633,7 +681,8 @@ class GpuManager(object):
         if worker.state in (DRAINING, EXITED):
             return
         worker.state = DRAINING
-        worker.proc.pipe.send({'cmd': 'drain', 'reason': reason})
+        worker.proc.pipe.send({'cmd': 'drain', 'reason': reason,
+                               'recycle': self._recycle_ok(worker.resource)})
         self.events.emit('worker_drain', worker=worker.id, reason=reason)
         logger.info('Draining worker %s (%s).', worker.id, reason)
 
@@ -688,6 +737,11 @@ class GpuManager(object):
                 worker.last_beat = time.monotonic()
             elif kind == 'fenced':
                 self._on_fenced(worker.resource, message)
+            elif kind == 'recycled':
+                self._on_recycled(worker, message)
+            elif kind == 'standby':
+                # the rest of a batch that also held 'recycled'
+                self._on_standby_message(worker.proc, message)
             elif kind == 'error':
                 logger.error('Worker %s reported: %s', worker.id,
                              message.get('message'))
@@ -739,19 +793,25 @@ class GpuManager(object):
             if proc.popen.poll() is not None:
                 proc.pipe.close()
                 del self.standbys[index]
+        for proc in list(self.retiring):
+            if proc.popen.poll() is not None:
+                proc.pipe.close()
+                self.retiring.remove(proc)
 
-    def _on_exit(self, resource, worker, code):
+    def _on_exit(self, resource, worker, code, recycled=False):
         was_ready = worker.state in (READY, DRAINING) and worker.t_ready
         # a drained worker the watchdog had to kill still counts as failed
         drained = worker.state == DRAINING and not worker.kill_reason
         worker.state = EXITED
         worker.exit_code = code
         worker.t_exit = time.monotonic_ns()
-        worker.proc.pipe.close()
+        if not recycled:
+            worker.proc.pipe.close()
         del resource.workers[worker.id]
         self.history.append(worker.summary())
         self.events.emit('worker_exit', worker=worker.id, code=code,
-                         gpu=worker.slot.index, killed=worker.kill_reason)
+                         gpu=worker.slot.index, killed=worker.kill_reason,
+                         recycled=recycled)
         requeued = self._requeue(resource, worker)
         if resource.kind == 'job' and code == 0 and not drained:
             resource.succeeded += 1

@@ -3,7 +3,8 @@
 Manager -> worker (``--cmd-fd``), one JSON object per line:
 ``assign`` (GPU, template, ids), ``drain``, ``fence`` / ``fence_abort``,
 ``exit``.  Worker -> manager (``--ev-fd``): ``standby``, ``stage``,
-``ready``, ``busy`` / ``idle``, ``fenced``, ``error``.
+``ready``, ``busy`` / ``beat`` / ``idle``, ``fenced``, ``recycled``,
+``error``.
 """
 import json
 import os
@@ -46,9 +47,14 @@ class Channel(object):
         return json.loads(line)
 
     def read_command(self):
-        """Blocking read of the next command (``None`` on EOF)."""
+        """Blocking read of the next command (``None`` on EOF).  Once the
+        reader thread runs (after the first assignment), commands come from
+        its queue."""
         if self.cmd_fd is None:
             return None
+        if self._reader is not None:
+            message = self.commands.get()
+            return None if message.get('cmd') == 'eof' else message
         return self._read_line()
 
     def start_reader(self):

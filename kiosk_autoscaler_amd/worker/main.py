@@ -8,9 +8,13 @@ Two start modes (both spawned by :mod:`kiosk_autoscaler_amd.gpumgr`):
 * **cold** (``--assign JSON``): the same, but start immediately.
 
 After assignment the process pins itself (``HIP_VISIBLE_DEVICES`` + CPU
-affinity), builds the engine and runs :class:`WorkerRuntime`.
+affinity), builds the engine and runs :class:`WorkerRuntime`.  When the
+manager drains it with ``recycle`` (or a job worker finishes), it releases
+the engine and reports ``recycled`` + ``standby``: the process, with its HIP
+context, becomes its GPU's standby again.
 """
 import argparse
+import gc
 import logging
 import os
 import sys
@@ -63,8 +67,7 @@ def main(argv=None):
         format='[%(asctime)s]:[%(levelname)s]:[%(name)s]: %(message)s')
 
     from .channel import Channel
-    from .runtime import (WorkerConfig, WorkerRuntime, apply_assignment_env,
-                          parse_assignment)
+    from .runtime import apply_assignment_env, parse_assignment
     channel = Channel(args.cmd_fd, args.ev_fd)
 
     backend = args.backend
@@ -92,21 +95,62 @@ def main(argv=None):
             channel.emit('error', message='preinit failed: %s' % err)
             return 4
 
-    if args.assign:
-        assignment = parse_assignment(args.assign)
-    else:
-        channel.emit('standby', preload_ns=preload_ns, backend=backend,
-                     preinit=preinit)
-        while True:
-            assignment = channel.read_command()
-            if assignment is None or assignment.get('cmd') == 'exit':
-                return 0
-            if assignment.get('cmd') == 'assign':
+    assignment = parse_assignment(args.assign) if args.assign else None
+    recycles = 0
+    max_recycles = int(os.environ.get('WORKER_MAX_RECYCLES', 64))
+    while True:
+        if assignment is None:
+            assignment = _wait_for_assignment(channel, pin, preload_ns,
+                                              backend, preinit)
+            if assignment is None:
+                code = 0
                 break
-        if pin and str(assignment.get('gpu')) != str(pin.get('gpu')):
-            channel.emit('error', message='assigned GPU %s but pinned to %s'
-                         % (assignment.get('gpu'), pin.get('gpu')))
-            return 5
+            if isinstance(assignment, int):     # pinned to another GPU
+                code = assignment
+                break
+        code, runtime = _serve(assignment, backend, channel)
+        # Recycle: a cleanly drained (or finished job) worker has released
+        # its HBM, streams and communicator but keeps its HIP context and
+        # loaded code objects -- it goes back to being this GPU's standby,
+        # so the next scale-up on it skips the ~2 s process boot.
+        if not (code == 0 and runtime.recycle and
+                recycles < max_recycles):
+            break
+        recycles += 1
+        gc.collect()
+        channel.emit('recycled', code=code, keys_done=runtime.keys_done,
+                     recycles=recycles)
+        pin = {'gpu': assignment.get('gpu'), 'slot': assignment.get('slot'),
+               'cpus': assignment.get('cpus')}
+        assignment = None
+    # The engine (HBM, streams, graphs) and the fence are released by now;
+    # skip interpreter teardown (torch/HIP static destructors take ~0.5 s)
+    # so the GPU slot frees promptly.
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(code)
+
+
+def _wait_for_assignment(channel, pin, preload_ns, backend, preinit):
+    """Standby: report, then block until ``assign`` (or ``exit``/EOF)."""
+    channel.emit('standby', preload_ns=preload_ns, backend=backend,
+                 preinit=preinit)
+    while True:
+        message = channel.read_command()
+        if message is None or message.get('cmd') in ('exit', 'eof'):
+            return None
+        if message.get('cmd') == 'assign':
+            break
+    if pin and str(message.get('gpu')) != str(pin.get('gpu')):
+        channel.emit('error', message='assigned GPU %s but pinned to %s'
+                     % (message.get('gpu'), pin.get('gpu')))
+        return 5
+    return message
+
+
+def _serve(assignment, backend, channel):
+    """Run one assignment to completion: ``(exit code, runtime)``."""
+    from .runtime import WorkerConfig, WorkerRuntime, apply_assignment_env
     apply_assignment_env(assignment)
     config = WorkerConfig(os.environ, assignment)
 
@@ -142,12 +186,7 @@ def main(argv=None):
         events.emit('worker_exit_self', worker=config.worker_id,
                     keys_done=runtime.keys_done)
         events.close()
-    # The engine (HBM, streams, graphs) and the fence are released by now;
-    # skip interpreter teardown (torch/HIP static destructors take ~0.5 s)
-    # so the GPU slot frees promptly.
-    sys.stdout.flush()
-    sys.stderr.flush()
-    os._exit(code)
+    return code, runtime
 
 
 if __name__ == '__main__':

@@ -68,6 +68,7 @@ class WorkerConfig(object):
         self.job_idle_exit = _env_float(env, 'JOB_IDLE_EXIT_S', 1.0)
         self.mock_work_ms = _env_float(env, 'MOCK_WORK_MS', 0.0)
         self.record_events = env.get('WORKER_EVENTS', '1') not in ('0', '')
+        self.recycle = bool(assignment.get('recycle', False))
 
 
 class QueueConsumer(object):
@@ -132,6 +133,9 @@ class WorkerRuntime(object):
         self.engine = None
         self.fence_agent = None
         self.draining = False
+        # back to the standby pool after a clean finish (manager's call:
+        # set by the assignment, overridden by the drain command)
+        self.recycle = bool(config.recycle)
         self.stages = {}
         self.keys_done = 0
 
@@ -153,8 +157,12 @@ class WorkerRuntime(object):
             except queue_mod.Empty:
                 return
             cmd = message.get('cmd')
-            if cmd in ('drain', 'exit', 'eof'):
+            if cmd == 'drain':
                 self.draining = True
+                self.recycle = bool(message.get('recycle', False))
+            elif cmd in ('exit', 'eof'):
+                self.draining = True
+                self.recycle = False
             elif cmd in ('fence', 'fence_abort') and self.fence_agent:
                 self.fence_agent.submit(message)
 
@@ -187,6 +195,8 @@ class WorkerRuntime(object):
             logger.exception('worker %s failed to start', cfg.worker_id)
             self.channel.emit('error', message='%s: %s' % (
                 type(err).__name__, err))
+            if self.engine is not None:
+                self.engine.close()
             return 3
         consumer = QueueConsumer(self.redis, cfg.worker_id, cfg.queues,
                                  cfg.poll_block)

@@ -138,3 +138,52 @@ def test_worker_crash_requeues(stack):
     assert view.status.restarts == 1
     wait_for(lambda: client.hget('predict:job0', 'status') == 'done',
              timeout=30)
+
+
+def test_drained_worker_recycled_into_pool(stack):
+    """Scale-down returns the worker process (HIP context and all) to the
+    pool; the next scale-up on that GPU reuses the very same process."""
+    s, client, manager, scaler, events = stack()
+    wait_for(lambda: manager.standbys and all(
+        p.booted for p in manager.standbys.values()))
+    first_pid = manager.standbys[0].pid
+    enqueue(client, 1)
+    assert tick(scaler, s) == 1
+    wait_for(lambda: client.hget('predict:job0', 'status') == 'done')
+    assert tick(scaler, s) == 0
+    wait_for(lambda: 0 in manager.standbys and manager.standbys[0].booted)
+    assert manager.standbys[0].pid == first_pid
+    assert any(e['ev'] == 'worker_recycled' for e in events.records)
+    exit_ev = [e for e in events.records if e['ev'] == 'worker_exit'][0]
+    assert exit_ev['recycled'] is True and exit_ev['code'] == 0
+    client.delete('predict:job0')
+    enqueue(client, 1)
+    assert tick(scaler, s) == 1
+    wait_for(lambda: client.hget('predict:job0', 'status') == 'done')
+    worker = manager.status()['resources'][0]['workers'][0]
+    assert worker['pid'] == first_pid and worker['from_pool'] is True
+
+
+def test_recycle_disabled_exits(stack):
+    s, client, manager, scaler, events = stack(WARM_POOL='0')
+    enqueue(client, 1)
+    assert tick(scaler, s) == 1
+    wait_for(lambda: client.hget('predict:job0', 'status') == 'done')
+    pid = manager.status()['resources'][0]['workers'][0]['pid']
+    assert tick(scaler, s) == 0
+    wait_for(lambda: not manager.status()['resources'][0]['workers'])
+    wait_for(lambda: _dead(pid))
+    assert not manager.standbys
+
+
+def _dead(pid):
+    try:
+        os.kill(pid, 0)
+    except OSError:
+        return True
+    # a zombie until reaped by the manager's poll
+    try:
+        with open('/proc/%d/stat' % pid) as f:
+            return f.read().split()[2] == 'Z'
+    except OSError:
+        return True
