@@ -107,7 +107,10 @@ class Services(object):
         self.redis = StrictRedis(host='127.0.0.1', port=self.port,
                                  decode_responses=True)
         wait_for(lambda: self._ping(), 20, what='redis')
-        env = dict(os.environ)
+        # the autoscaler and its workers are not torchrun ranks: keep the
+        # launcher's rendezvous variables out of their environment
+        env = {k: v for k, v in os.environ.items()
+               if k not in TORCHRUN_VARS and not k.startswith('TORCHELASTIC')}
         env.update({
             'REDIS_HOST': '127.0.0.1', 'REDIS_PORT': str(self.port),
             'REDIS_INTERVAL': '1', 'QUEUES': args.queues,
@@ -276,6 +279,12 @@ def parse_args():
     p.add_argument('--idle-timeout', type=float, default=120.0)
     p.add_argument('--drain-timeout', type=float, default=300.0)
     return p.parse_args()
+
+
+TORCHRUN_VARS = ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'LOCAL_WORLD_SIZE',
+                 'GROUP_RANK', 'GROUP_WORLD_SIZE', 'ROLE_RANK', 'ROLE_NAME',
+                 'ROLE_WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT',
+                 'OMP_NUM_THREADS_SET')
 
 
 def main():

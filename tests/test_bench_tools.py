@@ -122,3 +122,26 @@ def test_bench_cpu_smoke(tmp_path):
     assert line['higher_is_better'] is False and line['n_gpus'] == 1
     assert line['keys_done'] == line['keys'] > 0
     assert line['value'] is not None and line['value'] < 1.0
+
+
+@pytest.mark.slow
+def test_bench_torchrun_two_ranks_cpu(tmp_path):
+    """The driver's N>1 launch shape (torchrun, one rank per GPU) on CPU:
+    ranks rendezvous over gloo, rank 0 alone drives the node-wide stack
+    with MAX_PODS=2 and prints exactly one JSON line."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    proc = subprocess.run(
+        [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+         '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
+         '--master-port', '29631', os.path.join(ROOT, 'bench.py'),
+         '--backend', 'cpu', '--steps', '1', '--warmup', '0', '--interval',
+         '0.5', '--on', '1', '--off', '0.2', '--lam-per-gpu', '4',
+         '--service-ms', '50', '--gpus', '2'], env=env, cwd=str(tmp_path),
+        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+        timeout=300)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    lines = [l for l in proc.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line['n_gpus'] == 2 and line['config']['max_pods'] == 2
+    assert line['keys_done'] == line['keys'] > 0

@@ -171,7 +171,7 @@ def test_fence_warmup_and_preinit(mod):
 @pytest.mark.parametrize('M,N,K', [(256, 256, 32), (300, 512, 96),
                                    (2048, 1024, 4096), (1, 256, 64)])
 @pytest.mark.parametrize('epilogue', ['none', 'gelu', 'residual'])
-def test_gemm256_ring_kernel(mod, M, N, K, epilogue):
+def test_gemm256_ring_kernel(mod, M, N, K, epilogue, variant='256'):
     """The 256x256 LDS-ring kernel against the fp32 reference (odd halves
     counts exercise the vmcnt(4)/vmcnt(0) ring tails)."""
     from kiosk_autoscaler_amd.ops import kernels
@@ -187,7 +187,7 @@ def test_gemm256_ring_kernel(mod, M, N, K, epilogue):
     if epilogue == 'residual':
         ref = ref + res.float()
     c = kernels.gemm(a, b, bias=bias, residual=res, epilogue=epilogue,
-                     variant='256')
+                     variant=variant)
     torch.testing.assert_close(c.float(), ref, atol=3e-2, rtol=2e-2)
 
 

@@ -49,6 +49,7 @@ def main():
                'torch_gelu': theirs, 'torch': theirs_plain}
         if N % 256 == 0:
             fns['native256'] = ours_256
+
         results = {k: [] for k in fns}
         for fn in fns.values():
             fn()
@@ -67,7 +68,7 @@ def main():
         ref = (a.float() @ b.float().t())
         summary = {'shape': [M, N, K]}
         for name, fn in (('128', ours_plain), ('256', ours_256)):
-            if name == '256' and N % 256:
+            if name.startswith('256') and N % 256:
                 continue
             out.zero_()
             fn()
