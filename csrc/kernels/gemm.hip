@@ -188,8 +188,11 @@ hipError_t gemm_prepare() {
 int gemm_pick_variant(int M, int N, int K) {
   // the 256^2 ring kernel runs one block per CU: use it only when the grid
   // still fills the 256 CUs
-  if (gemm256_shape_ok(M, N, K) && ((M + 255) / 256) * (N / 256) >= 256)
+  const int rows = (M + 255) / 256;
+  if (gemm256_shape_ok(M, N, K, 256) && rows * (N / 256) >= 256)
     return GEMM_256;
+  if (gemm256_shape_ok(M, N, K, 128) && rows * (N / 128) >= 256)
+    return GEMM_256x128;
   return GEMM_128;
 }
 
@@ -198,11 +201,12 @@ hipError_t launch_gemm_variant(const uint16_t* A, const uint16_t* B,
                                const uint16_t* R, int M, int N, int K,
                                int epilogue, int variant, hipStream_t stream) {
   if (variant == GEMM_AUTO) variant = gemm_pick_variant(M, N, K);
-  if (variant == GEMM_256) {
+  if (variant == GEMM_256 || variant == GEMM_256x128) {
     if ((epilogue != EPI_NONE && bias == nullptr) ||
         (epilogue == EPI_BIAS_RESIDUAL && R == nullptr))
       return hipErrorInvalidValue;
-    return launch_gemm256(A, B, C, bias, R, M, N, K, epilogue, stream);
+    return launch_gemm256(A, B, C, bias, R, M, N, K, epilogue, stream,
+                          variant == GEMM_256 ? 256 : 128);
   }
   return launch_gemm(A, B, C, bias, R, M, N, K, epilogue, stream);
 }

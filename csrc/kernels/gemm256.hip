@@ -1,4 +1,5 @@
-// Large-tile bf16 TN GEMM for gfx950: 256x256 block tile, 8 waves, LDS ring.
+// Large-tile bf16 TN GEMM for gfx950: 256xBN block tile (BN = 256 or 128),
+// 8 waves, LDS ring.
 //
 //   C[M,N] = epi(A[M,K] . B[N,K]^T)      (same contract as gemm.hip)
 //
@@ -8,7 +9,8 @@
 // This kernel keeps the DMA in flight across barriers:
 //
 //  * K is consumed in 32-deep halves; a 4-slot LDS ring (4 x 32 KiB =
-//    128 KiB, one block per CU) holds A[256][32] + B[256][32] per slot.
+//    128 KiB for BN = 256, one block per CU) holds A[256][32] + B[BN][32]
+//    per slot.
 //  * at half-step h (its fragments already in registers) every wave waits
 //    with a *counted* `s_waitcnt vmcnt(8)` -- only half h+1 must have
 //    landed, halves h+2 and h+3 stay in flight -- and a raw s_barrier
@@ -20,9 +22,11 @@
 //    each ds_read_b128 lane group covers all 16 bank slots (conflict-free,
 //    see swz()); the swizzle is applied on the DMA source address because
 //    LDS-DMA writes lane-linearly (rule 21).
-//  * 8 waves as 2(M) x 4(N), 128x64 outputs per wave = 8x4 tiles of
-//    v_mfma_f32_16x16x32_bf16 with swapped operands (C^T in registers ->
-//    4 consecutive columns per lane -> 8-B stores, float4 bias).
+//  * BN = 256: 8 waves as 2(M) x 4(N), 128x64 outputs per wave = 8x4
+//    tiles of v_mfma_f32_16x16x32_bf16; BN = 128 (for N where 256-wide
+//    tiles leave CUs idle, e.g. 2048x4096): 4(M) x 2(N) waves of 64x64.
+//    Swapped MFMA operands (C^T in registers -> 4 consecutive columns per
+//    lane -> 8-B stores, float4 bias).
 //  * XCD-aware bijective workgroup remap + 4-tile-row grouping.
 #include "common.hpp"
 #include "kernels.hpp"
@@ -30,13 +34,28 @@
 namespace kiosk {
 namespace {
 
-constexpr int BM = 256, BN = 256, BKH = 32;
+constexpr int BM = 256, BKH = 32;
+constexpr int kWaves = 8;
 constexpr int kRowBytes = BKH * 2;                 // 64 B per row per half
-constexpr int kOperandBytes = BM * kRowBytes;      // 16 KiB
-constexpr int kSlotBytes = 2 * kOperandBytes;      // A + B = 32 KiB
 constexpr int kSlots = 4;
-constexpr int kLdsBytes = kSlots * kSlotBytes;     // 128 KiB
 constexpr int kGroupM = 4;
+
+// Per-BN geometry.  LDS slot = A[256][32] + B[BN][32]; an operand half is
+// rows/16 DMA pieces of 16 rows x 64 B spread over the 8 waves.
+template <int BN>
+struct Geo {
+  static constexpr int kWavesM = BN == 256 ? 2 : 4;
+  static constexpr int kWavesN = kWaves / kWavesM;
+  static constexpr int TM = BM / kWavesM / 16;     // 16-row tiles per wave
+  static constexpr int TN = BN / kWavesN / 16;     // 16-col tiles per wave
+  static constexpr int kABytes = BM * kRowBytes;   // 16 KiB
+  static constexpr int kSlotBytes = (BM + BN) * kRowBytes;
+  static constexpr int kLdsBytes = kSlots * kSlotBytes;
+  static constexpr int kPiecesA = BM / 16 / kWaves;
+  static constexpr int kPiecesB = BN / 16 / kWaves;
+  static constexpr int kLoadsPerHalf = kPiecesA + kPiecesB;  // glds/wave
+  static constexpr int kReads = TM + TN;           // ds_read_b128 per half
+};
 
 // ds_read_b128 is serviced in 16-lane groups {0-3,12-15,20-27},
 // {4-11,16-19,28-31}, ... (MI355X_MICROARCH.md §LDS), not 16 consecutive
@@ -50,14 +69,13 @@ __device__ __forceinline__ int slot_off(int r, int c) {
   return r * kRowBytes + ((c ^ swz(r)) << 4);
 }
 
-// 16 KiB operand half = 16 x 1 KiB DMA pieces (16 rows x 64 B); each of
-// the WAVES waves issues 16 / WAVES consecutive pieces.
-template <int WAVES>
+// An operand half = DMA pieces of 16 rows x 64 B (1 KiB); wave w issues
+// pieces [w * kPieces, (w + 1) * kPieces).
+template <int kPieces>
 __device__ __forceinline__ void stage_operand(const uint16_t* __restrict__ g,
                                               int ld, int row0, int rows,
                                               int k0, char* lds, int wave,
                                               int lane) {
-  constexpr int kPieces = 16 / WAVES;
 #pragma unroll
   for (int i = 0; i < kPieces; ++i) {
     const int piece = wave * kPieces + i;
@@ -78,11 +96,10 @@ constexpr int waitcnt_vm(int vm) {
   return (vm & 0xF) | (((vm >> 4) & 3) << 14) | 0x0070;
 }
 
-// WAVES = 8: 2(M) x 4(N) waves of 128x64 outputs (2 waves per SIMD).
-// (WAVES = 4, 128x128 per wave with the accumulators in AGPRs, compiles
-// but hipcc spills ~270 registers inside the loop: not instantiated.)
-template <int EPI, int WAVES>
-__global__ __launch_bounds__(64 * WAVES, 1) void gemm256_kernel(
+// (A 4-wave 128x128-per-wave layout with the accumulators in AGPRs was
+// tried: hipcc spills ~270 registers inside the loop.)
+template <int EPI, int BN>
+__global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
     uint16_t* __restrict__ C, const float* __restrict__ bias,
     const uint16_t* __restrict__ R, int M, int N, int K) {
@@ -98,19 +115,19 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm256_kernel(
   const int m0 = (first_m + in_group % gsize) * BM;
   const int n0 = (in_group / gsize) * BN;
 
-  constexpr int kWavesN = WAVES / 2;
-  constexpr int TN = BN / kWavesN / 16;      // 16-wide N tiles per wave
-  constexpr int kLoadsPerHalf = 2 * (16 / WAVES);   // glds per wave per half
+  using G = Geo<BN>;
+  constexpr int TM = G::TM, TN = G::TN, kSlotBytes = G::kSlotBytes;
+  constexpr int kLoadsPerHalf = G::kLoadsPerHalf;
   constexpr int kWaitHalf1 = waitcnt_vm(3 * kLoadsPerHalf);
   constexpr int kWaitHalf2 = waitcnt_vm(2 * kLoadsPerHalf);
   constexpr int kWaitAll = waitcnt_vm(0);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave / kWavesN, wn = wave % kWavesN;
+  const int wm = wave / G::kWavesN, wn = wave % G::kWavesN;
 
-  f32x4 acc[8][TN];
+  f32x4 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -121,26 +138,27 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm256_kernel(
   auto stage = [&](int h) {
     char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
     const int k0 = min(h, halves - 1) * BKH;
-    stage_operand<WAVES>(A, K, m0, M, k0, slot, wave, lane);
-    stage_operand<WAVES>(B, K, n0, N, k0, slot + kOperandBytes, wave, lane);
+    stage_operand<G::kPiecesA>(A, K, m0, M, k0, slot, wave, lane);
+    stage_operand<G::kPiecesB>(B, K, n0, N, k0, slot + G::kABytes, wave,
+                               lane);
   };
-  const int arow = wm * 128 + (lane & 15);
+  const int arow = wm * (TM * 16) + (lane & 15);
   const int brow = wn * (TN * 16) + (lane & 15);
   const int chunk = lane >> 4;
-  auto read_frags = [&](int h, bf16x8 (&wb)[TN], bf16x8 (&xa)[8]) {
+  auto read_frags = [&](int h, bf16x8 (&wb)[TN], bf16x8 (&xa)[TM]) {
     const char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
 #pragma unroll
     for (int j = 0; j < TN; ++j)
       wb[j] = *reinterpret_cast<const bf16x8*>(
-          slot + kOperandBytes + slot_off(brow + j * 16, chunk));
+          slot + G::kABytes + slot_off(brow + j * 16, chunk));
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < TM; ++i)
       xa[i] = *reinterpret_cast<const bf16x8*>(
           slot + slot_off(arow + i * 16, chunk));
   };
-  auto mma = [&](const bf16x8 (&wb)[TN], const bf16x8 (&xa)[8]) {
+  auto mma = [&](const bf16x8 (&wb)[TN], const bf16x8 (&xa)[TM]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
@@ -154,8 +172,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm256_kernel(
   // h while the reads and the DMA are in flight.  Branch-free on purpose: a
   // control-flow join between the reads and the MFMAs makes the waitcnt
   // pass drain lgkmcnt first, which serialises the two.
-  auto step = [&](int h, const bf16x8 (&wb)[TN], const bf16x8 (&xa)[8],
-                  bf16x8 (&wb_next)[TN], bf16x8 (&xa_next)[8]) {
+  auto step = [&](int h, const bf16x8 (&wb)[TN], const bf16x8 (&xa)[TM],
+                  bf16x8 (&wb_next)[TN], bf16x8 (&xa_next)[TM]) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(kWaitHalf2);
     __builtin_amdgcn_s_barrier();
@@ -164,13 +182,14 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm256_kernel(
     read_frags(h + 1, wb_next, xa_next);
     mma(wb, xa);
     // spread the next half's LDS reads through the MFMA cluster: per
-    // quarter 3 ds_read_b128 then 8 MFMAs (the glds stay up front).
+    // quarter a quarter of the ds_read_b128s, then a quarter of the MFMAs
+    // (the glds stay up front).
     // Measured +1..4 % over issuing all 12 reads ahead of the cluster
     // (profiles/r1_gemm/gemm_ab_swizzle_interleave.jsonl).
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x100, (8 + TN) / 4, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 8 * TN / 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, G::kReads / 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TM * TN / 4, 0);
     }
   };
 
@@ -179,7 +198,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm256_kernel(
   __builtin_amdgcn_s_waitcnt(kWaitHalf1);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
-  bf16x8 wb0[TN], xa0[8], wb1[TN], xa1[8];
+  bf16x8 wb0[TN], xa0[TM], wb1[TN], xa1[TM];
   read_frags(0, wb0, xa0);
   for (int h = 0; h < halves; h += 2) {
     step(h, wb0, xa0, wb1, xa1);
@@ -189,8 +208,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm256_kernel(
   __builtin_amdgcn_s_waitcnt(kWaitAll);
 
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (TM * 16) + i * 16 + (lane & 15);
     if (m >= M) continue;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -220,39 +239,40 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gemm256_kernel(
   }
 }
 
-template <int EPI, int WAVES>
+template <int EPI, int BN>
 hipError_t configure256() {
   return hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&gemm256_kernel<EPI, WAVES>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+      reinterpret_cast<const void*>(&gemm256_kernel<EPI, BN>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, Geo<BN>::kLdsBytes);
 }
 
-template <int WAVES>
+template <int BN>
 hipError_t configure256_all() {
-  hipError_t err = configure256<EPI_NONE, WAVES>();
-  if (err == hipSuccess) err = configure256<EPI_BIAS_GELU, WAVES>();
-  if (err == hipSuccess) err = configure256<EPI_BIAS_RESIDUAL, WAVES>();
+  hipError_t err = configure256<EPI_NONE, BN>();
+  if (err == hipSuccess) err = configure256<EPI_BIAS_GELU, BN>();
+  if (err == hipSuccess) err = configure256<EPI_BIAS_RESIDUAL, BN>();
   return err;
 }
 
-template <int WAVES>
+template <int BN>
 hipError_t launch256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                      const float* bias, const uint16_t* R, int M, int N,
                      int K, int epilogue, hipStream_t stream) {
   const int blocks = ((M + BM - 1) / BM) * (N / BN);
-  const dim3 grid(blocks), block(64 * WAVES);
+  const dim3 grid(blocks), block(64 * kWaves);
+  const int lds = Geo<BN>::kLdsBytes;
   switch (epilogue) {
     case EPI_NONE:
-      hipLaunchKernelGGL((gemm256_kernel<EPI_NONE, WAVES>), grid, block,
-                         kLdsBytes, stream, A, B, C, bias, R, M, N, K);
+      hipLaunchKernelGGL((gemm256_kernel<EPI_NONE, BN>), grid, block, lds,
+                         stream, A, B, C, bias, R, M, N, K);
       break;
     case EPI_BIAS_GELU:
-      hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_GELU, WAVES>), grid, block,
-                         kLdsBytes, stream, A, B, C, bias, R, M, N, K);
+      hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_GELU, BN>), grid, block,
+                         lds, stream, A, B, C, bias, R, M, N, K);
       break;
     case EPI_BIAS_RESIDUAL:
-      hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_RESIDUAL, WAVES>), grid,
-                         block, kLdsBytes, stream, A, B, C, bias, R, M, N, K);
+      hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_RESIDUAL, BN>), grid,
+                         block, lds, stream, A, B, C, bias, R, M, N, K);
       break;
     default:
       return hipErrorInvalidValue;
@@ -263,18 +283,23 @@ hipError_t launch256(const uint16_t* A, const uint16_t* B, uint16_t* C,
 }  // namespace
 
 hipError_t gemm256_prepare() {
-  return configure256_all<8>();
+  hipError_t err = configure256_all<256>();
+  if (err == hipSuccess) err = configure256_all<128>();
+  return err;
 }
 
-bool gemm256_shape_ok(int M, int N, int K) {
-  return M >= 1 && N % BN == 0 && N >= BN && K % BKH == 0 && K >= BKH;
+bool gemm256_shape_ok(int M, int N, int K, int bn) {
+  return (bn == 256 || bn == 128) && M >= 1 && N % bn == 0 && N >= bn &&
+         K % BKH == 0 && K >= BKH;
 }
 
 hipError_t launch_gemm256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                           const float* bias, const uint16_t* R, int M, int N,
-                          int K, int epilogue, hipStream_t stream) {
-  if (!gemm256_shape_ok(M, N, K)) return hipErrorInvalidValue;
-  return launch256<8>(A, B, C, bias, R, M, N, K, epilogue, stream);
+                          int K, int epilogue, hipStream_t stream, int bn) {
+  if (!gemm256_shape_ok(M, N, K, bn)) return hipErrorInvalidValue;
+  if (bn == 128)
+    return launch256<128>(A, B, C, bias, R, M, N, K, epilogue, stream);
+  return launch256<256>(A, B, C, bias, R, M, N, K, epilogue, stream);
 }
 
 }  // namespace kiosk

@@ -31,19 +31,23 @@ bool gemm_shape_ok(int M, int N, int K);
 hipError_t gemm_prepare();  // call once before launching / capturing
 
 // Kernel variants: 0 = auto (256x256 ring kernel when it yields >= 256
-// tiles, else 128x128), 1 = 128x128 two-barrier, 2 = 256x256 LDS ring.
-enum GemmVariant { GEMM_AUTO = 0, GEMM_128 = 1, GEMM_256 = 2 };
+// tiles, else the 256x128 ring when that does, else 128x128), 1 = 128x128
+// two-barrier, 2 = 256x256 LDS ring, 3 = 256x128 LDS ring.
+enum GemmVariant {
+  GEMM_AUTO = 0, GEMM_128 = 1, GEMM_256 = 2, GEMM_256x128 = 3
+};
 hipError_t launch_gemm_variant(const uint16_t* A, const uint16_t* B,
                                uint16_t* C, const float* bias,
                                const uint16_t* R, int M, int N, int K,
                                int epilogue, int variant, hipStream_t stream);
 int gemm_pick_variant(int M, int N, int K);
-// 256x256 ring kernel (gemm256.hip)
-bool gemm256_shape_ok(int M, int N, int K);
+// 256 x bn ring kernel (gemm256.hip), bn = 256 or 128
+bool gemm256_shape_ok(int M, int N, int K, int bn = 256);
 hipError_t gemm256_prepare();
 hipError_t launch_gemm256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                           const float* bias, const uint16_t* R, int M, int N,
-                          int K, int epilogue, hipStream_t stream);
+                          int K, int epilogue, hipStream_t stream,
+                          int bn = 256);
 
 // Uniform [lo, hi) init, counter-based (reproducible for a seed).
 hipError_t launch_init_uniform_bf16(uint16_t* p, size_t n, uint64_t seed,

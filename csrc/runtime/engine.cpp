@@ -65,8 +65,11 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   // the 256x256 ring kernel needs a 256-wide operand: reuse the buffers
   // as [128 x 256] / [256 x 64] views (N = 256, K = 64)
   for (int epi = 0; epi < 3; ++epi) {
-    check_hip(launch_gemm256(a, b, c, bias, r, 64, 256, 64, epi, stream),
-              "preinit gemm256");
+    for (int bn : {256, 128}) {
+      check_hip(launch_gemm256(a, b, c, bias, r, 64, 256, 64, epi, stream,
+                               bn),
+                "preinit gemm256");
+    }
   }
   check_hip(launch_partial_sums(c, elems, sums, stream), "preinit sums");
   check_hip(launch_warmstart(a, elems, rec, 1, 1, 2 * kGemmLdsBytes, stream),

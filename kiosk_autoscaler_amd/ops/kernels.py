@@ -24,7 +24,7 @@ def _check_bf16(t, name):
         raise ValueError('%s must be a contiguous bf16 CUDA tensor' % name)
 
 
-VARIANTS = {'auto': 0, '128': 1, '256': 2}
+VARIANTS = {'auto': 0, '128': 1, '256': 2, '256x128': 3}
 
 
 def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
@@ -33,8 +33,9 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
 
     ``epilogue``: ``'none'``, ``'gelu'`` (``gelu_tanh(a@b.T + bias)``) or
     ``'residual'`` (``a@b.T + bias + residual``).  ``variant``: ``'auto'``
-    (256x256 LDS-ring kernel when the grid fills the chip, else 128x128),
-    ``'128'`` or ``'256'``."""
+    (256x256 LDS-ring kernel when the grid fills the chip, else the 256x128
+    ring when that does, else 128x128), ``'128'``, ``'256'`` or
+    ``'256x128'``."""
     import torch
     mod = native.load()
     _check_bf16(a, 'a')
@@ -43,10 +44,12 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
     N, K2 = b.shape
     if K != K2:
         raise ValueError('inner dimensions differ: %d vs %d' % (K, K2))
-    if variant == '256':
-        if M < 1 or N % 256 or K % 32 or K < 32:
-            raise ValueError('the 256x256 kernel needs N %% 256 == 0 and '
-                             'K %% 32 == 0 (M=%d N=%d K=%d)' % (M, N, K))
+    if variant in ('256', '256x128'):
+        bn = 256 if variant == '256' else 128
+        if M < 1 or N % bn or K % 32 or K < 32:
+            raise ValueError('the 256x%d kernel needs N %% %d == 0 and '
+                             'K %% 32 == 0 (M=%d N=%d K=%d)'
+                             % (bn, bn, M, N, K))
     elif not mod.gemm_shape_ok(M, N, K):
         raise ValueError('unsupported GEMM shape M=%d N=%d K=%d (need N %% 128'
                          ' == 0, K %% 64 == 0)' % (M, N, K))

@@ -169,11 +169,15 @@ def test_fence_warmup_and_preinit(mod):
 
 
 @pytest.mark.parametrize('M,N,K', [(256, 256, 32), (300, 512, 96),
-                                   (2048, 1024, 4096), (1, 256, 64)])
+                                   (2048, 1024, 4096), (1, 256, 64),
+                                   (520, 384, 160)])
 @pytest.mark.parametrize('epilogue', ['none', 'gelu', 'residual'])
-def test_gemm256_ring_kernel(mod, M, N, K, epilogue, variant='256'):
-    """The 256x256 LDS-ring kernel against the fp32 reference (odd halves
-    counts exercise the vmcnt(4)/vmcnt(0) ring tails)."""
+@pytest.mark.parametrize('variant', ['256', '256x128'])
+def test_gemm256_ring_kernel(mod, M, N, K, epilogue, variant):
+    """The 256x256 / 256x128 LDS-ring kernels against the fp32 reference
+    (odd half counts exercise the clamped tail staging)."""
+    if variant == '256' and N % 256:
+        pytest.skip('N not a multiple of 256')
     from kiosk_autoscaler_amd.ops import kernels
     a = rand_bf16(M, K, seed=11)
     b = rand_bf16(N, K, scale=0.1, seed=12)
@@ -198,10 +202,12 @@ def test_gemm256_identity(mod):
     a = torch.eye(M, K, device='cuda', dtype=torch.bfloat16)
     b = (torch.arange(N * K, device='cuda', dtype=torch.float32)
          .reshape(N, K) % 241 - 120).to(torch.bfloat16)
-    c = kernels.gemm(a, b, variant='256')
-    assert torch.equal(c, b.t().contiguous()[:M])
+    for variant in ('256', '256x128'):
+        c = kernels.gemm(a, b, variant=variant)
+        assert torch.equal(c, b.t().contiguous()[:M]), variant
     assert mod.gemm_pick_variant(2048, 16384, 4096) == 2
-    assert mod.gemm_pick_variant(2048, 4096, 16384) == 1
+    assert mod.gemm_pick_variant(2048, 4096, 16384) == 3
+    assert mod.gemm_pick_variant(256, 1024, 1024) == 1
 
 
 def test_spin_kernel_and_roctx(mod):

@@ -38,6 +38,9 @@ def main():
         def ours_256():
             kernels.gemm(a, b, out=out, variant='256')
 
+        def ours_256x128():
+            kernels.gemm(a, b, out=out, variant='256x128')
+
         def theirs():
             torch.nn.functional.gelu(torch.addmm(bias.to(torch.bfloat16), a,
                                                  b.t()), approximate='tanh')
@@ -49,6 +52,7 @@ def main():
                'torch_gelu': theirs, 'torch': theirs_plain}
         if N % 256 == 0:
             fns['native256'] = ours_256
+        fns['native256x128'] = ours_256x128
 
         results = {k: [] for k in fns}
         for fn in fns.values():
@@ -67,8 +71,9 @@ def main():
                 results[name].append(2.0 * M * N * K / (ms * 1e-3) / 1e12)
         ref = (a.float() @ b.float().t())
         summary = {'shape': [M, N, K]}
-        for name, fn in (('128', ours_plain), ('256', ours_256)):
-            if name.startswith('256') and N % 256:
+        for name, fn in (('128', ours_plain), ('256', ours_256),
+                         ('256x128', ours_256x128)):
+            if name == '256' and N % 256:
                 continue
             out.zero_()
             fn()
