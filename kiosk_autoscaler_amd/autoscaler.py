@@ -41,11 +41,17 @@ class Autoscaler(object):
         scale_down_delay: seconds a lower target must persist before a
             scale-down is applied (``strict`` hysteresis; 0 = immediate).
         events: optional :class:`~kiosk_autoscaler_amd.utils.EventLog`.
+        tally: ``'reference'`` (``LLEN`` on a replica, then a ``SCAN`` of
+            the master: two non-atomic reads, SURVEY §5.2, so an item a
+            worker moves in between can be counted twice or missed) or
+            ``'atomic'`` (``LLEN`` + ``KEYS processing-q:*`` in one
+            ``MULTI``/``EXEC`` on the master: one consistent snapshot).
     """
 
     def __init__(self, redis_client, queues='predict', queue_delim=',',
                  actuator=None, policy='reference', scale_down_delay=0.0,
-                 events=None, clock=timeit.default_timer):
+                 events=None, clock=timeit.default_timer,
+                 tally='reference'):
         self.redis_keys = {q: 0 for q in queues.split(queue_delim)}
         self.in_progress = {q: 0 for q in self.redis_keys}
         self.redis_client = redis_client
@@ -60,6 +66,9 @@ class Autoscaler(object):
         self._clock = clock
         self._lower_since = None
         self.last_decision = None
+        if tally not in ('reference', 'atomic'):
+            raise ValueError('unknown tally mode %r' % tally)
+        self.tally = tally
 
     # -- C6 ------------------------------------------------------------------
     def tally_queues(self):
@@ -67,16 +76,38 @@ class Autoscaler(object):
         start = self._clock()
         for queue in self.redis_keys:
             self.logger.debug('Tallying items in queue `%s`.', queue)
-            waiting = self.redis_client.llen(queue)
             pattern = 'processing-{}:*'.format(queue)
-            running = sum(1 for _ in self.redis_client.scan_iter(
-                match=pattern, count=1000))
+            counted = None
+            if self.tally == 'atomic':
+                counted = self._tally_atomic(queue, pattern)
+            if counted is None:
+                waiting = self.redis_client.llen(queue)
+                running = sum(1 for _ in self.redis_client.scan_iter(
+                    match=pattern, count=1000))
+            else:
+                waiting, running = counted
             self.in_progress[queue] = running
             self.redis_keys[queue] = waiting + running
         self.logger.debug('Finished tallying redis keys in %s seconds.',
                           self._clock() - start)
         self.logger.info('In-progress or new redis keys: %s', self.redis_keys)
         return dict(self.redis_keys)
+
+    def _tally_atomic(self, queue, pattern):
+        """``(LLEN, #processing keys)`` from one MULTI/EXEC on the master, or
+        ``None`` on a connection error (the caller falls back to the
+        retrying reference path, so a failover still heals itself)."""
+        from .redisq.exceptions import ConnectionError as RedisConnError
+        try:
+            pipe = self.redis_client.pipeline(transaction=True)
+            pipe.llen(queue)
+            pipe.keys(pattern)
+            waiting, keys = pipe.execute()
+        except RedisConnError as err:
+            self.logger.warning('atomic tally of `%s` failed (%s); using '
+                                'LLEN + SCAN', queue, err)
+            return None
+        return int(waiting), len(keys)
 
     # -- C7-C9: actuator access ------------------------------------------------
     def get_actuator(self):

@@ -64,7 +64,7 @@ def build(settings=None, redis_client=None, actuator=None, events=None):
                         queue_delim=settings.QUEUE_DELIMITER,
                         actuator=actuator, policy=settings.SCALE_POLICY,
                         scale_down_delay=settings.SCALE_DOWN_DELAY,
-                        events=events)
+                        events=events, tally=settings.TALLY_MODE)
     return redis_client, scaler, manager
 
 

@@ -141,6 +141,7 @@ REFERENCE_DEFAULTS = (
 EXTRA_DEFAULTS = (
     ('SCALE_POLICY', str, 'reference'),     # reference | strict
     ('SCALE_DOWN_DELAY', float, 0.0),       # strict: idle grace seconds
+    ('TALLY_MODE', str, 'reference'),       # reference (LLEN+SCAN) | atomic (MULTI)
     ('FIXED_RATE', bool, False),            # tick every INTERVAL (not tick+INTERVAL)
     ('IDLE_INTERVAL', float, 0.0),          # opt-in faster poll while at 0 pods
     ('GPU_IDS', str, ''),                   # '' = all visible GPUs

@@ -186,3 +186,54 @@ def test_strict_policy_with_hysteresis(redis_client):
     assert scaler.scale('ns', 'deployment', 'w', 0, 8, 1) == 4  # held
     clock[0] = 11.0
     assert scaler.scale('ns', 'deployment', 'w', 0, 8, 1) == 1  # applied
+
+
+def test_atomic_tally_matches_and_is_consistent(redis_client):
+    """TALLY_MODE=atomic: LLEN + KEYS in one MULTI/EXEC.  A consumer that
+    keeps moving items between the queue and processing keys never makes
+    the atomic tally over- or under-count (SURVEY §5.2 race)."""
+    import threading
+    for i in range(20):
+        redis_client.lpush('q', 'item%d' % i)
+    from kiosk_autoscaler_amd import Autoscaler
+    scaler = Autoscaler(redis_client, 'q', tally='atomic')
+    assert scaler.tally_queues() == {'q': 20}
+    stop = threading.Event()
+
+    def churn():
+        n = 0
+        while not stop.is_set():
+            key = 'processing-q:w%d' % (n % 7)
+            if redis_client.lmove('q', key, 'RIGHT', 'LEFT') is None:
+                continue
+            # every move is atomic: the item is always in exactly one list
+            redis_client.lmove(key, 'q', 'RIGHT', 'LEFT')
+            n += 1
+    thread = threading.Thread(target=churn, daemon=True)
+    thread.start()
+    try:
+        for _ in range(200):
+            assert scaler.tally_queues()['q'] == 20
+    finally:
+        stop.set()
+        thread.join(5)
+    with pytest.raises(ValueError):
+        Autoscaler(redis_client, 'q', tally='nope')
+
+
+def test_atomic_tally_through_sentinel_proxy_and_kredis(resp_server,
+                                                         kredis_server):
+    """The MULTI/EXEC tally over real sockets: the retrying proxy routes the
+    pipeline to the master; both RESP servers implement MULTI + KEYS."""
+    from kiosk_autoscaler_amd import Autoscaler
+    from kiosk_autoscaler_amd.redisq import RedisClient
+    for server in (resp_server, kredis_server):
+        proxy = RedisClient(host=server.host, port=server.port, backoff=0)
+        proxy.delete('q')
+        proxy.lpush('q', 'a', 'b', 'c')
+        proxy.lpush('processing-q:w1', 'x')
+        proxy.lpush('processing-q:w2', 'y')
+        proxy.lpush('processing-qq:w3', 'z')          # another queue
+        scaler = Autoscaler(proxy, 'q', tally='atomic')
+        assert scaler.tally_queues() == {'q': 5}
+        assert scaler.in_progress == {'q': 2}
