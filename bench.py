@@ -38,6 +38,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from kiosk_autoscaler_amd.bench import gpu_util  # noqa: E402  (no torch)
+
 METRIC = ('scale-up latency (s) first-key->GPU-ready + GPU-idle-% at fixed '
           'QPS, 1/2/4/8 GPU')
 # BASELINE.md §3, QUEUES=predict, MAX_PODS=8, KEYS_PER_POD=1, lam=2/s,
@@ -329,6 +331,9 @@ def main():
             for w in range(args.warmup):
                 run_episode(svc, gen, args, 0.5 * args.interval,
                             'warmup %d' % w)
+        sampler = None
+        if rank == 0:
+            sampler = start_util_sampler(args.gpus)
         barrier()
         sync()
         t0 = time.perf_counter()
@@ -340,6 +345,7 @@ def main():
         sync()
         barrier()
         elapsed = time.perf_counter() - t0
+        util = sampler.stop() if sampler is not None else None
         if dist is not None:
             tensor = torch.tensor([elapsed], dtype=torch.float64)
             dist.all_reduce(tensor, op=dist.ReduceOp.MAX)
@@ -352,7 +358,8 @@ def main():
             ref = reference_sim(episodes, args)
             value = summary['latency_mean_s']
             detail = {'summary': summary, 'reference_sim': ref,
-                      'args': vars(args)}
+                      'args': vars(args), 'amdsmi': util,
+                      'amdsmi_error': getattr(sampler, 'error', None)}
             with open(os.path.join(OUT_DIR, 'bench_detail_n%d.json' %
                                    args.gpus), 'w') as handle:
                 json.dump(detail, handle, indent=1, default=str)
@@ -398,6 +405,10 @@ def main():
                 'first_result_mean_s': _r(summary['first_result_mean_s']),
                 'queue_wait_mean_s': _r(summary['queue_wait_mean_s']),
                 'keys_done': summary['keys_done'], 'keys': summary['keys'],
+                # hardware cross-check of the event-derived busy fraction
+                'event_busy_wall_pct': _r(100.0 * summary['gpu_busy_s'] /
+                                          max(1e-9, elapsed * args.gpus)),
+                'amdsmi_gfx_busy_pct': _r(gpu_util.mean_busy(util)),
                 'reference_sim_latency_s': _r(ref['latency_mean_s']),
                 'reference_sim_gpu_idle_pct': _r(ref['gpu_idle_pct']),
             }
@@ -407,6 +418,25 @@ def main():
             svc.stop()
         if dist is not None:
             dist.destroy_process_group()
+
+
+def start_util_sampler(n_gpus):
+    """amdsmi gfx-activity sampling over the managed GPUs (None on CPU)."""
+    if os.environ.get('KIOSK_AMDSMI', '1') == '0':
+        return None
+    bdfs = None
+    try:
+        from kiosk_autoscaler_amd.gpumgr import gpus
+        slots = gpus.discover(','.join(str(i) for i in range(n_gpus)),
+                              env={}, cpu_slots=0)
+        found = [s.pci for s in slots if getattr(s, 'pci', None)]
+        if len(found) == n_gpus:
+            bdfs = found
+    except Exception:  # pylint: disable=broad-except
+        pass
+    sampler = gpu_util.UtilSampler(0.1, bdfs)
+    sampler.start()
+    return sampler
 
 
 def _r(value, nd=4):

@@ -145,3 +145,16 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
     line = json.loads(lines[0])
     assert line['n_gpus'] == 2 and line['config']['max_pods'] == 2
     assert line['keys_done'] == line['keys'] > 0
+
+
+def test_util_sampler_degrades_without_driver():
+    from kiosk_autoscaler_amd.bench import gpu_util
+    sampler = gpu_util.UtilSampler(0.01)
+    started = sampler.start()
+    result = sampler.stop()
+    if not started:                      # CPU container: no amdgpu driver
+        assert result is None and sampler.error
+    assert gpu_util.mean_busy(None) is None
+    assert gpu_util.mean_busy({'a': {'gfx_busy_pct': 10.0, 'samples': 1},
+                               'b': {'gfx_busy_pct': 30.0, 'samples': 2}}) \
+        == 20.0
