@@ -46,9 +46,15 @@ __global__ __launch_bounds__(256) void warmstart_kernel(
 
   // 3. MFMA loop on operands drawn from LDS (zeros) xor the weight mix
   const int lane = threadIdx.x & 63;
+  // sign + mantissa from the weight mix, exponent pinned to 2^-1: an xor
+  // of many weights cancels the exponent bits (tiny values the MFMA flushes
+  // to zero), so the loop would otherwise multiply zeros
+  constexpr uint32_t kSignMant = 0x807f807fu, kHalf = 0x3f003f00u;
   uint4 raw = *reinterpret_cast<const uint4*>(smem + lane * 16);
-  raw.x ^= mix.x & 0x3f7f3f7fu; raw.y ^= mix.y & 0x3f7f3f7fu;
-  raw.z ^= mix.z & 0x3f7f3f7fu; raw.w ^= mix.w & 0x3f7f3f7fu;
+  raw.x = ((raw.x ^ mix.x) & kSignMant) | kHalf;
+  raw.y = ((raw.y ^ mix.y) & kSignMant) | kHalf;
+  raw.z = ((raw.z ^ mix.z) & kSignMant) | kHalf;
+  raw.w = ((raw.w ^ mix.w) & kSignMant) | kHalf;
   const bf16x8 a = __builtin_bit_cast(bf16x8, raw);
   uint4 rb = uint4{raw.y, raw.z, raw.w, raw.x};
   const bf16x8 b = __builtin_bit_cast(bf16x8, rb);

@@ -128,6 +128,9 @@ def test_warmstart_touches_every_cu(mod):
         assert info['blocks'] == cus
         assert info['cus_touched'] == cus, info['cus_touched']
         assert info['xccs_touched'] == 8
+        # the MFMA loop multiplies real (weight-derived) operands
+        assert info['checksum'] != 0.0 and info['checksum'] == \
+            info['checksum']
         assert info['kernel_us'] > 0 and info['span_us'] > 0
     finally:
         engine.close()
