@@ -188,6 +188,8 @@ class Resource(object):
         self.fence_inflight = None   # (epoch, members, t_start)
         self.fence_wanted = False
         self.fence_fresh = False     # force re-init after a failed epoch
+        self.fence_failures = 0      # consecutive failed/abandoned epochs
+        self.fence_retry_at = 0.0    # monotonic s; backoff after failures
 
     @property
     def key(self):
@@ -260,6 +262,10 @@ class GpuManager(object):
         self._wake_r, self._wake_w = os.pipe()
         os.set_blocking(self._wake_r, False)
         self._worker_seq = itertools.count()
+        # worker ids must not repeat across manager restarts (persisted
+        # state, orphan recovery, events): <name>-g<slot>-<instance>-<seq>
+        self.instance = '%x' % ((os.getpid() << 20 ^ time.time_ns() >> 10)
+                                & 0xfffff)
         self._stopping = False
         self.history = []   # exited workers, for accounting
 
@@ -646,8 +652,8 @@ class GpuManager(object):
         return [s for s in self.slots if s.index not in used]
 
     def _start_worker(self, resource, slot):
-        wid = '%s-g%d-%d' % (resource.name, slot.index,
-                             next(self._worker_seq))
+        wid = '%s-g%d-%s-%d' % (resource.name, slot.index, self.instance,
+                                next(self._worker_seq))
         assign = {
             'cmd': 'assign', 'worker_id': wid, 'gpu': slot.visible_id,
             'slot': slot.index, 'cpus': slot.cpus, 'kind': resource.kind,
@@ -889,11 +895,11 @@ class GpuManager(object):
                         w.proc.pipe.send({'cmd': 'fence_abort',
                                           'epoch': epoch})
                 resource.fence_inflight = None
-                resource.fence_wanted = True
-                resource.fence_fresh = True
+                self._fence_failed(resource)
             else:
                 return
-        if not resource.fence_wanted:
+        if not resource.fence_wanted or \
+                time.monotonic() < resource.fence_retry_at:
             return
         members = sorted((w.id for w in resource.ready()),
                          key=lambda wid: resource.workers[wid].slot.index)
@@ -918,6 +924,17 @@ class GpuManager(object):
         resource.fence_inflight = (epoch, members, time.monotonic())
         self.events.emit('fence_start', epoch=epoch, members=members)
 
+    def _fence_failed(self, resource):
+        """Retry with a fresh communicator after an exponential backoff, so
+        a persistently failing bootstrap cannot spin on RCCL inits."""
+        resource.fence_wanted = True
+        resource.fence_fresh = True
+        resource.fence_failures += 1
+        delay = min(30.0, 0.25 * 2 ** min(resource.fence_failures - 1, 8))
+        resource.fence_retry_at = time.monotonic() + delay
+        self.events.emit('fence_retry', name=resource.name, delay_s=delay,
+                         failures=resource.fence_failures)
+
     def _on_fenced(self, resource, message):
         inflight = resource.fence_inflight
         if inflight is None or message.get('epoch') != inflight[0]:
@@ -927,10 +944,10 @@ class GpuManager(object):
         if not message.get('ok', False):
             logger.warning('Fence epoch %d failed: %s', epoch,
                            message.get('detail'))
-            resource.fence_wanted = True
-            resource.fence_fresh = True
+            self._fence_failed(resource)
             return
         resource.fence_fresh = False
+        resource.fence_failures = 0
         resource.fenced_epoch = epoch
         resource.fenced_members = members
         self.events.emit('fence_done', epoch=epoch, members=members,

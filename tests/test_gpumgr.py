@@ -194,3 +194,18 @@ def test_state_persist_restore_and_orphans():
     third = gpumgr.GpuManager(slots, redis_client=redis, fence=False)
     third.register('deployment', 'ns', 'w', tpl, restore=False)
     assert third.list_namespaced_deployment('ns').items[0].spec.replicas == 0
+
+
+def test_worker_ids_unique_across_instances_and_fence_backoff():
+    slots = [gpus.GpuSlot(0, '', kind='cpu')]
+    a = gpumgr.GpuManager(slots, fence=False)
+    b = gpumgr.GpuManager(slots, fence=False)
+    assert a.instance != b.instance or a is b
+    from kiosk_autoscaler_amd.gpumgr.controller import Resource
+    tpl = gpumgr.WorkerTemplate(queues=['q'], backend='cpu')
+    res = Resource('deployment', 'ns', 'w', tpl)
+    a._fence_failed(res)
+    first = res.fence_retry_at
+    a._fence_failed(res)
+    assert res.fence_failures == 2 and res.fence_retry_at > first
+    assert res.fence_wanted and res.fence_fresh
