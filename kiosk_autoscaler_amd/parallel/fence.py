@@ -297,10 +297,20 @@ class FenceAgent(object):
                 if self.channel is not None:
                     self.channel.emit('fenced', **report)
 
-    def close(self):
+    def close(self, timeout=5.0):
+        """Stop the fence thread and release the communicator.  Returns
+        ``False`` if the thread is still inside a collective: the
+        communicator is then left alone (destroying it under a running
+        all-reduce would be a use-after-free in the native layer) and the
+        caller must not reuse this process for another worker."""
         self._queue.put(None)
-        self._thread.join(timeout=5)
+        self._thread.join(timeout=timeout)
+        if self._thread.is_alive():
+            logger.warning('fence thread still in a collective at close; '
+                           'leaving its communicator to process exit')
+            return False
         self.transport.close()
+        return True
 
 
 def choose_transport(kind, backend, redis, group, timeout=60.0):

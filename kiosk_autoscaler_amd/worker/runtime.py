@@ -231,8 +231,8 @@ class WorkerRuntime(object):
                     self._process(consumer, items)
                 idle_since = time.monotonic()
         finally:
-            if self.fence_agent is not None:
-                self.fence_agent.close()
+            if self.fence_agent is not None and not self.fence_agent.close():
+                self.recycle = False    # a collective may still be running
             if self.engine is not None:
                 self.engine.close()
         return 0

@@ -159,3 +159,32 @@ def test_choose_transport(redis_client):
     with pytest.raises(ValueError):
         fence_mod.choose_transport('mpi', 'cpu', redis_client, 'g')
     assert os.environ is not None
+
+
+def test_agent_close_never_destroys_a_busy_communicator():
+    """close() while the fence thread is stuck in a collective must leave
+    the transport alone and report it (the worker then is not recycled)."""
+    import threading
+    from kiosk_autoscaler_amd.parallel.fence import FenceAgent
+    release = threading.Event()
+    closed = []
+
+    class Stuck(object):
+        name = 'stuck'
+
+        def allreduce(self, epoch, members, rank, vec, previous=None,
+                      fresh=False):
+            release.wait(10)
+            return vec, {}
+
+        def close(self):
+            closed.append(True)
+
+    agent = FenceAgent('w-0', 0, Stuck())
+    agent.submit({'cmd': 'fence', 'epoch': 1, 'members': ['w-0'],
+                  'slots': [0]})
+    import time
+    time.sleep(0.1)
+    assert agent.close(timeout=0.2) is False and closed == []
+    release.set()
+    agent._thread.join(5)
