@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSVs (one or more passes) per kernel.
+
+Usage: python tools/pmc_summary.py gpurun_out/pmc/a gpurun_out/pmc/b
+Prints one JSON line per kernel with the mean of each counter per dispatch
+and derived ratios: MFMA utilisation (SQ_VALU_MFMA_BUSY_CYCLES over
+GRBM_GUI_ACTIVE/8 x 1024 SIMDs), LDS bank-conflict share, and the
+wave-cycle split (parked / issue-stalled / issuing).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def load(dirs):
+    sums = collections.defaultdict(lambda: collections.defaultdict(float))
+    counts = collections.defaultdict(lambda: collections.defaultdict(set))
+    for d in dirs:
+        for path in glob.glob(os.path.join(d, '**', '*counter_collection*.csv'),
+                              recursive=True):
+            with open(path) as handle:
+                for row in csv.DictReader(handle):
+                    name = row.get('Kernel_Name', '')
+                    counter = row.get('Counter_Name', '')
+                    value = float(row.get('Counter_Value', 0) or 0)
+                    dispatch = row.get('Dispatch_Id', '')
+                    sums[name][counter] += value
+                    counts[name][counter].add(dispatch)
+    out = {}
+    for name, by_counter in sums.items():
+        out[name] = {c: v / max(1, len(counts[name][c]))
+                     for c, v in by_counter.items()}
+    return out
+
+
+def derive(c):
+    d = {}
+    if c.get('GRBM_GUI_ACTIVE') and 'SQ_VALU_MFMA_BUSY_CYCLES' in c:
+        d['mfma_util'] = c['SQ_VALU_MFMA_BUSY_CYCLES'] / (
+            c['GRBM_GUI_ACTIVE'] / 8.0 * 1024)
+    if c.get('SQ_LDS_IDX_ACTIVE'):
+        d['lds_conflict_share'] = c.get('SQ_LDS_BANK_CONFLICT', 0) / \
+            c['SQ_LDS_IDX_ACTIVE']
+    total = sum(c.get(k, 0) for k in ('SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY',
+                                      'SQ_ACTIVE_INST_ANY'))
+    if total:
+        for k in ('SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_ANY'):
+            d[k.lower() + '_share'] = c.get(k, 0) / total
+    return d
+
+
+def main():
+    data = load(sys.argv[1:])
+    for name, counters in sorted(data.items()):
+        short = name.split('(')[0].replace('kiosk::(anonymous namespace)::',
+                                           '')
+        row = {'kernel': short}
+        row.update({k: round(v, 1) for k, v in sorted(counters.items())})
+        row.update({k: round(v, 4) for k, v in derive(counters).items()})
+        print(json.dumps(row))
+
+
+if __name__ == '__main__':
+    main()
