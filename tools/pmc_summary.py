@@ -55,8 +55,8 @@ def derive(c):
 def main():
     data = load(sys.argv[1:])
     for name, counters in sorted(data.items()):
-        short = name.split('(')[0].replace('kiosk::(anonymous namespace)::',
-                                           '')
+        short = name.replace('kiosk::(anonymous namespace)::', '')
+        short = short.replace('void ', '').split('(')[0]
         row = {'kernel': short}
         row.update({k: round(v, 1) for k, v in sorted(counters.items())})
         row.update({k: round(v, 4) for k, v in derive(counters).items()})
