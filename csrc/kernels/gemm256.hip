@@ -88,6 +88,27 @@ __device__ __forceinline__ void stage_operand(const uint16_t* __restrict__ g,
   }
 }
 
+// One DMA piece (16 rows x 64 B) of an operand half: `piece` indexes the
+// operand's 1 KiB pieces.
+__device__ __forceinline__ void stage_piece(const uint16_t* __restrict__ g,
+                                            int ld, int row0, int rows,
+                                            int k0, char* lds, int piece,
+                                            int lane) {
+  const int r = piece * 16 + (lane >> 2);
+  const int c = (lane & 3) ^ swz(r);
+  int grow = row0 + r;
+  grow = grow < rows ? grow : rows - 1;
+  glds16(g + static_cast<size_t>(grow) * ld + k0 + c * 8,
+         lds + piece * 1024);
+}
+
+// Items p in [0, n) are issued in quarter p * 4 / n: how many land in q.
+constexpr int per_quarter(int n, int q) {
+  int c = 0;
+  for (int p = 0; p < n; ++p) c += (p * 4 / n == q);
+  return c;
+}
+
 // Counted waits go through the builtin (not inline asm) so hipcc's waitcnt
 // pass sees them and adds no conservative lgkmcnt(0) of its own.  gfx9
 // encoding: vmcnt[3:0] | expcnt[6:4] (7 = no wait) | lgkmcnt[11:8] |
@@ -172,22 +193,73 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   // h while the reads and the DMA are in flight.  Branch-free on purpose: a
   // control-flow join between the reads and the MFMAs makes the waitcnt
   // pass drain lgkmcnt first, which serialises the two.
+  // SPREAD (BN = 256): the step's DMA pieces and LDS reads are issued in
+  // program order as four quarters (pieces, then reads, of quarter q), so
+  // hipcc (which keeps LDS-writing DMAs and LDS reads in order) slots a
+  // quarter of the MFMAs behind each: no block of 4 DMA issues (~60+ cycles
+  // each) ahead of the cluster.  +3..5 % at 256x256, -3..+1 % at 256x128
+  // (profiles/r1_gemm/gemm_spread_dma.jsonl), so only the former uses it.
+  constexpr bool SPREAD = BN == 256;
+  auto stage_q = [&](int h, int q) {
+    char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
+    const int k0 = min(h, halves - 1) * BKH;
+#pragma unroll
+    for (int p = 0; p < kLoadsPerHalf; ++p) {
+      if (p * 4 / kLoadsPerHalf != q) continue;
+      if (p < G::kPiecesA)
+        stage_piece(A, K, m0, M, k0, slot, wave * G::kPiecesA + p, lane);
+      else
+        stage_piece(B, K, n0, N, k0, slot + G::kABytes,
+                    wave * G::kPiecesB + (p - G::kPiecesA), lane);
+    }
+  };
+  auto read_q = [&](int h, int q, bf16x8 (&wb)[TN], bf16x8 (&xa)[TM]) {
+    const char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
+#pragma unroll
+    for (int r = 0; r < G::kReads; ++r) {
+      if (r * 4 / G::kReads != q) continue;
+      if (r < TN)
+        wb[r] = *reinterpret_cast<const bf16x8*>(
+            slot + G::kABytes + slot_off(brow + r * 16, chunk));
+      else
+        xa[r - TN] = *reinterpret_cast<const bf16x8*>(
+            slot + slot_off(arow + (r - TN) * 16, chunk));
+    }
+  };
   auto step = [&](int h, const bf16x8 (&wb)[TN], const bf16x8 (&xa)[TM],
                   bf16x8 (&wb_next)[TN], bf16x8 (&xa_next)[TM]) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(kWaitHalf2);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    stage(h + 4);
-    read_frags(h + 1, wb_next, xa_next);
+    if constexpr (SPREAD) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        stage_q(h + 4, q);
+        read_q(h + 1, q, wb_next, xa_next);
+      }
+    } else {
+      stage(h + 4);
+      read_frags(h + 1, wb_next, xa_next);
+    }
     mma(wb, xa);
     // spread the next half's LDS reads through the MFMA cluster: per
-    // quarter a quarter of the ds_read_b128s, then a quarter of the MFMAs
-    // (the glds stay up front).
+    // quarter a quarter of the ds_read_b128s, then a quarter of the MFMAs.
     // Measured +1..4 % over issuing all 12 reads ahead of the cluster
     // (profiles/r1_gemm/gemm_ab_swizzle_interleave.jsonl).
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      if constexpr (SPREAD) {
+        // builtin arguments must be literal constants: one call per quarter
+        constexpr int c0 = per_quarter(kLoadsPerHalf, 0);
+        constexpr int c1 = per_quarter(kLoadsPerHalf, 1);
+        constexpr int c2 = per_quarter(kLoadsPerHalf, 2);
+        constexpr int c3 = per_quarter(kLoadsPerHalf, 3);
+        if (q == 0 && c0) __builtin_amdgcn_sched_group_barrier(0x010, c0, 0);
+        if (q == 1 && c1) __builtin_amdgcn_sched_group_barrier(0x010, c1, 0);
+        if (q == 2 && c2) __builtin_amdgcn_sched_group_barrier(0x010, c2, 0);
+        if (q == 3 && c3) __builtin_amdgcn_sched_group_barrier(0x010, c3, 0);
+      }
       __builtin_amdgcn_sched_group_barrier(0x100, G::kReads / 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, TM * TN / 4, 0);
     }

@@ -80,8 +80,6 @@ def compile_units(verbose=False, jobs=4):
             if src.endswith('.cpp'):
                 cmd = [HIPCC] + flags + ['-x', 'hip', '-c', src, '-o', obj]
             jobs_list.append(cmd)
-        units_obj = obj
-        del units_obj
     with concurrent.futures.ThreadPoolExecutor(max_workers=jobs) as pool:
         list(pool.map(lambda c: _run(c, verbose), jobs_list))
     return [os.path.join(OBJ, os.path.basename(s) + '.o') for s in units]
@@ -93,7 +91,24 @@ def link_extension(objects, verbose=False):
     cmd = [HIPCC, '-shared', '-fPIC', '--offload-arch=' + ARCH] + objects + \
         ['-o', EXT_PATH, '-ldl']
     _run(cmd, verbose)
+    check_no_undefined_own_symbols(EXT_PATH)
     return EXT_PATH
+
+
+def check_no_undefined_own_symbols(path):
+    """The link cannot use --no-undefined (Python symbols resolve at import
+    time), so a declaration/definition mismatch in our own code would only
+    surface as an import error on the GPU box.  Fail the build instead."""
+    nm = shutil.which('nm') or '/opt/rocm/lib/llvm/bin/llvm-nm'
+    out = subprocess.run([nm, '-D', '-C', '--undefined-only', path],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True).stdout
+    missing = [line.split()[-1] if '(' not in line else line.strip()
+               for line in out.splitlines() if 'kiosk::' in line]
+    if missing:
+        os.remove(path)
+        raise RuntimeError('undefined kiosk:: symbols in %s:\n  %s' % (
+            path, '\n  '.join(missing)))
 
 
 def build_kredis(verbose=False):
