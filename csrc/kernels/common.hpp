@@ -43,11 +43,13 @@ __device__ __forceinline__ void wait_vmcnt0() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// tanh-approximated GELU with tanh(u) = 1 - 2 / (exp(2u) + 1).
+// tanh-approximated GELU: 0.5 x (1 + tanh u) = x * sigmoid(2u)
+// = x / (1 + exp(-2u)), u = sqrt(2/pi) (x + 0.044715 x^3).  One v_exp_f32
+// and one v_rcp_f32 (~1 ulp) instead of an IEEE division sequence; the
+// limits are exact (exp -> inf gives x * 0, exp -> 0 gives x).
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-  const float t = 1.0f - 2.0f / (__expf(2.0f * u) + 1.0f);
-  return 0.5f * x * (1.0f + t);
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * u));
 }
 
 // Bijective XCD-aware remap of a linear workgroup id: consecutive remapped
