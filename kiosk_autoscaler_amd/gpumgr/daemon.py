@@ -21,7 +21,7 @@ import socket
 import socketserver
 import threading
 
-from .controller import GpuManager, WorkerTemplate
+from .controller import WorkerTemplate
 from .resources import ActuatorError, ResourceList, ResourceView
 
 logger = logging.getLogger('GpuManagerTransport')
