@@ -51,8 +51,10 @@ def build(settings=None, redis_client=None, actuator=None, events=None):
                               source='autoscaler')
     manager = None
     if actuator is None:
-        if settings.GPUMGR.startswith('unix:'):
-            # the daemon registers the resource from its own environment
+        if settings.GPUMGR.startswith('unix:') or \
+                settings.GPUMGR.startswith('k8s'):
+            # the daemon registers the resource from its own environment;
+            # with k8s the Deployment/Job already exists in the cluster
             actuator = gpumgr.connect(settings.GPUMGR)
         else:
             manager = gpumgr.build_manager(settings, redis_client=redis_client,

@@ -145,7 +145,7 @@ EXTRA_DEFAULTS = (
     ('FIXED_RATE', bool, False),            # tick every INTERVAL (not tick+INTERVAL)
     ('IDLE_INTERVAL', float, 0.0),          # opt-in faster poll while at 0 pods
     ('GPU_IDS', str, ''),                   # '' = all visible GPUs
-    ('GPUMGR', str, 'embedded'),            # embedded | unix:<path>
+    ('GPUMGR', str, 'embedded'),            # embedded | unix:<path> | k8s
     ('WORKER_MODULE', str, 'kiosk_autoscaler_amd.worker.main'),
     ('WORKER_BACKEND', str, 'auto'),        # auto | hip | cpu
     ('WARM_POOL', int, -1),                 # standby processes (-1 = MAX_PODS)

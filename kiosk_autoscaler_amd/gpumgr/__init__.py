@@ -21,9 +21,15 @@ def set_embedded(manager):
 
 
 def connect(address=None):
+    """The actuator for ``GPUMGR``: ``embedded`` (this process's manager),
+    ``unix:<path>`` (the manager daemon) or ``k8s`` / ``k8s-kubeconfig``
+    (the Kubernetes API, like the reference)."""
     address = address or os.environ.get('GPUMGR', 'embedded')
     if address.startswith('unix:'):
         return GpuManagerClient(address[len('unix:'):])
+    if address in ('k8s', 'k8s-kubeconfig'):
+        from .k8s import KubernetesActuator
+        return KubernetesActuator(in_cluster=address == 'k8s')
     if _EMBEDDED is None:
         raise ActuatorError(503, 'no embedded GPU manager is running')
     return _EMBEDDED
