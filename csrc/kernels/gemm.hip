@@ -185,26 +185,44 @@ hipError_t gemm_prepare() {
   return err;
 }
 
-int gemm_pick_variant(int M, int N, int K) {
-  // the 256^2 ring kernel runs one block per CU: use it only when the grid
-  // still fills the 256 CUs
+int gemm_pick_variant(int M, int N, int K, bool have_workspace) {
+  // the 256-row ring kernels run one block per CU: use the 256x256 one
+  // when its grid fills the 256 CUs, else split K across the idle CUs
+  // (needs a workspace), else the 256x128 ring, else the 128x128 kernel
   const int rows = (M + 255) / 256;
   if (gemm256_shape_ok(M, N, K, 256) && rows * (N / 256) >= 256)
     return GEMM_256;
+  if (have_workspace && gemm256_shape_ok(M, N, K, 256) &&
+      gemm256_splits(M, N, K) > 1)
+    return GEMM_256_SPLITK;
   if (gemm256_shape_ok(M, N, K, 128) && rows * (N / 128) >= 256)
     return GEMM_256x128;
   return GEMM_128;
 }
 
+size_t gemm_workspace_bytes(int M, int N, int K) {
+  return gemm256_splitk_workspace(M, N, K);
+}
+
 hipError_t launch_gemm_variant(const uint16_t* A, const uint16_t* B,
                                uint16_t* C, const float* bias,
                                const uint16_t* R, int M, int N, int K,
-                               int epilogue, int variant, hipStream_t stream) {
-  if (variant == GEMM_AUTO) variant = gemm_pick_variant(M, N, K);
+                               int epilogue, int variant, hipStream_t stream,
+                               float* workspace, size_t workspace_bytes) {
+  if ((epilogue != EPI_NONE && bias == nullptr) ||
+      (epilogue == EPI_BIAS_RESIDUAL && R == nullptr) ||
+      epilogue < EPI_NONE || epilogue > EPI_BIAS_RESIDUAL)
+    return hipErrorInvalidValue;
+  if (variant == GEMM_AUTO)
+    variant = gemm_pick_variant(
+        M, N, K, workspace != nullptr &&
+                     workspace_bytes >= gemm_workspace_bytes(M, N, K));
+  if (variant == GEMM_256_SPLITK) {
+    return launch_gemm256_splitk(A, B, C, bias, R, M, N, K, epilogue,
+                                 gemm256_splits(M, N, K), workspace,
+                                 workspace_bytes, stream);
+  }
   if (variant == GEMM_256 || variant == GEMM_256x128) {
-    if ((epilogue != EPI_NONE && bias == nullptr) ||
-        (epilogue == EPI_BIAS_RESIDUAL && R == nullptr))
-      return hipErrorInvalidValue;
     return launch_gemm256(A, B, C, bias, R, M, N, K, epilogue, stream,
                           variant == GEMM_256 ? 256 : 128);
   }

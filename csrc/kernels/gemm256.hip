@@ -28,6 +28,8 @@
 //    Swapped MFMA operands (C^T in registers -> 4 consecutive columns per
 //    lane -> 8-B stores, float4 bias).
 //  * XCD-aware bijective workgroup remap + 4-tile-row grouping.
+#include <algorithm>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -123,8 +125,13 @@ template <int EPI, int BN>
 __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
     uint16_t* __restrict__ C, const float* __restrict__ bias,
-    const uint16_t* __restrict__ R, int M, int N, int K) {
+    const uint16_t* __restrict__ R, int M, int N, int K, int lda) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // split-K: blockIdx.y picks a K/gridDim.y slice (K is the slice length,
+  // lda the full row stride); EPI_PARTIAL writes fp32 partials per slice
+  const int split = static_cast<int>(blockIdx.y);
+  A += static_cast<size_t>(split) * K;
+  B += static_cast<size_t>(split) * K;
   const int tiles_n = N / BN;
   const int tiles_m = (M + BM - 1) / BM;
   const int wg = xcd_remap(static_cast<int>(blockIdx.x), tiles_m * tiles_n);
@@ -159,8 +166,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   auto stage = [&](int h) {
     char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
     const int k0 = min(h, halves - 1) * BKH;
-    stage_operand<G::kPiecesA>(A, K, m0, M, k0, slot, wave, lane);
-    stage_operand<G::kPiecesB>(B, K, n0, N, k0, slot + G::kABytes, wave,
+    stage_operand<G::kPiecesA>(A, lda, m0, M, k0, slot, wave, lane);
+    stage_operand<G::kPiecesB>(B, lda, n0, N, k0, slot + G::kABytes, wave,
                                lane);
   };
   const int arow = wm * (TM * 16) + (lane & 15);
@@ -207,9 +214,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     for (int p = 0; p < kLoadsPerHalf; ++p) {
       if (p * 4 / kLoadsPerHalf != q) continue;
       if (p < G::kPiecesA)
-        stage_piece(A, K, m0, M, k0, slot, wave * G::kPiecesA + p, lane);
+        stage_piece(A, lda, m0, M, k0, slot, wave * G::kPiecesA + p, lane);
       else
-        stage_piece(B, K, n0, N, k0, slot + G::kABytes,
+        stage_piece(B, lda, n0, N, k0, slot + G::kABytes,
                     wave * G::kPiecesB + (p - G::kPiecesA), lane);
     }
   };
@@ -287,6 +294,13 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     for (int j = 0; j < TN; ++j) {
       const int nb = n0 + wn * (TN * 16) + j * 16 + (lane >> 4) * 4;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (EPI == EPI_PARTIAL) {
+        float* P = reinterpret_cast<float*>(C) +
+                   static_cast<size_t>(split) * M * N;
+        *reinterpret_cast<float4*>(P + static_cast<size_t>(m) * N + nb) =
+            float4{v[0], v[1], v[2], v[3]};
+        continue;
+      }
       if (EPI != EPI_NONE) {
         const float4 b = *reinterpret_cast<const float4*>(bias + nb);
         v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
@@ -323,28 +337,116 @@ hipError_t configure256_all() {
   hipError_t err = configure256<EPI_NONE, BN>();
   if (err == hipSuccess) err = configure256<EPI_BIAS_GELU, BN>();
   if (err == hipSuccess) err = configure256<EPI_BIAS_RESIDUAL, BN>();
+  if (err == hipSuccess) err = configure256<EPI_PARTIAL, BN>();
   return err;
 }
 
 template <int BN>
 hipError_t launch256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                      const float* bias, const uint16_t* R, int M, int N,
-                     int K, int epilogue, hipStream_t stream) {
+                     int K, int lda, int splits, int epilogue,
+                     hipStream_t stream) {
   const int blocks = ((M + BM - 1) / BM) * (N / BN);
-  const dim3 grid(blocks), block(64 * kWaves);
+  const dim3 grid(blocks, splits), block(64 * kWaves);
   const int lds = Geo<BN>::kLdsBytes;
   switch (epilogue) {
     case EPI_NONE:
       hipLaunchKernelGGL((gemm256_kernel<EPI_NONE, BN>), grid, block, lds,
-                         stream, A, B, C, bias, R, M, N, K);
+                         stream, A, B, C, bias, R, M, N, K, lda);
       break;
     case EPI_BIAS_GELU:
       hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_GELU, BN>), grid, block,
-                         lds, stream, A, B, C, bias, R, M, N, K);
+                         lds, stream, A, B, C, bias, R, M, N, K, lda);
       break;
     case EPI_BIAS_RESIDUAL:
       hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_RESIDUAL, BN>), grid,
-                         block, lds, stream, A, B, C, bias, R, M, N, K);
+                         block, lds, stream, A, B, C, bias, R, M, N, K, lda);
+      break;
+    case EPI_PARTIAL:
+      hipLaunchKernelGGL((gemm256_kernel<EPI_PARTIAL, BN>), grid, block,
+                         lds, stream, A, B, C, bias, R, M, N, K, lda);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// out = epi(sum_s P[s]) over `splits` fp32 partial planes of M x N; each
+// thread owns 8 consecutive columns (two float4 per plane, one 16-B bf16
+// store).  N % 8 == 0 (N is a multiple of 128 here).
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(
+    const float* __restrict__ P, int splits, int M, int N,
+    const float* __restrict__ bias, const uint16_t* __restrict__ R,
+    uint16_t* __restrict__ out) {
+  const size_t total = static_cast<size_t>(M) * N / 8;
+  const size_t plane = static_cast<size_t>(M) * N;
+  for (size_t c = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+       c < total; c += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    const size_t off = c * 8;
+    float v[8];
+    {
+      const float4 a = *reinterpret_cast<const float4*>(P + off);
+      const float4 b = *reinterpret_cast<const float4*>(P + off + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+      v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+    for (int s = 1; s < splits; ++s) {
+      const float4 a = *reinterpret_cast<const float4*>(P + s * plane + off);
+      const float4 b =
+          *reinterpret_cast<const float4*>(P + s * plane + off + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+    if (EPI != EPI_NONE) {
+      const int n = static_cast<int>(off % N);
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + n);
+      const float4 b1 = *reinterpret_cast<const float4*>(bias + n + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+      v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    }
+    if (EPI == EPI_BIAS_GELU) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = gelu_tanh(v[r]);
+    }
+    if (EPI == EPI_BIAS_RESIDUAL) {
+      const uint4 res = *reinterpret_cast<const uint4*>(R + off);
+      const uint32_t w[4] = {res.x, res.y, res.z, res.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[2 * r] += bf16_to_f32(w[r] & 0xffff);
+        v[2 * r + 1] += bf16_to_f32(w[r] >> 16);
+      }
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      o[r] = f32_to_bf16(v[2 * r]) |
+             (static_cast<uint32_t>(f32_to_bf16(v[2 * r + 1])) << 16);
+    *reinterpret_cast<uint4*>(out + off) = uint4{o[0], o[1], o[2], o[3]};
+  }
+}
+
+hipError_t launch_reduce(const float* P, int splits, int M, int N,
+                         const float* bias, const uint16_t* R, uint16_t* out,
+                         int epilogue, hipStream_t stream) {
+  const size_t chunks = static_cast<size_t>(M) * N / 8;
+  const int blocks = static_cast<int>(
+      std::min<size_t>((chunks + 255) / 256, 256 * 16));
+  switch (epilogue) {
+    case EPI_NONE:
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_NONE>, dim3(blocks),
+                         dim3(256), 0, stream, P, splits, M, N, bias, R, out);
+      break;
+    case EPI_BIAS_GELU:
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_BIAS_GELU>, dim3(blocks),
+                         dim3(256), 0, stream, P, splits, M, N, bias, R, out);
+      break;
+    case EPI_BIAS_RESIDUAL:
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_BIAS_RESIDUAL>,
+                         dim3(blocks), dim3(256), 0, stream, P, splits, M, N,
+                         bias, R, out);
       break;
     default:
       return hipErrorInvalidValue;
@@ -368,10 +470,44 @@ bool gemm256_shape_ok(int M, int N, int K, int bn) {
 hipError_t launch_gemm256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                           const float* bias, const uint16_t* R, int M, int N,
                           int K, int epilogue, hipStream_t stream, int bn) {
-  if (!gemm256_shape_ok(M, N, K, bn)) return hipErrorInvalidValue;
+  if (!gemm256_shape_ok(M, N, K, bn) || epilogue == EPI_PARTIAL)
+    return hipErrorInvalidValue;
   if (bn == 128)
-    return launch256<128>(A, B, C, bias, R, M, N, K, epilogue, stream);
-  return launch256<256>(A, B, C, bias, R, M, N, K, epilogue, stream);
+    return launch256<128>(A, B, C, bias, R, M, N, K, K, 1, epilogue, stream);
+  return launch256<256>(A, B, C, bias, R, M, N, K, K, 1, epilogue, stream);
+}
+
+int gemm256_splits(int M, int N, int K) {
+  // split K for the 256x256 kernel only while its grid leaves CUs idle,
+  // each slice keeps >= 2048 of K, and the slices stay 32-aligned
+  const int tiles = ((M + BM - 1) / BM) * (N / 256);
+  if (tiles >= 256 || N % 256 || K % BKH) return 1;
+  int s = 1;
+  while (s < 4 && tiles * s < 256 && K % (2 * s * BKH) == 0 &&
+         K / (2 * s) >= 2048)
+    s *= 2;
+  return s;
+}
+
+size_t gemm256_splitk_workspace(int M, int N, int K) {
+  const int s = gemm256_splits(M, N, K);
+  return s > 1 ? static_cast<size_t>(s) * M * N * sizeof(float) : 0;
+}
+
+hipError_t launch_gemm256_splitk(const uint16_t* A, const uint16_t* B,
+                                 uint16_t* C, const float* bias,
+                                 const uint16_t* R, int M, int N, int K,
+                                 int epilogue, int splits, float* workspace,
+                                 size_t workspace_bytes, hipStream_t stream) {
+  if (splits < 2 || K % (splits * BKH) || M < 1 || N % 256 ||
+      workspace == nullptr ||
+      workspace_bytes < static_cast<size_t>(splits) * M * N * sizeof(float))
+    return hipErrorInvalidValue;
+  hipError_t err = launch256<256>(A, B, reinterpret_cast<uint16_t*>(workspace),
+                                  nullptr, nullptr, M, N, K / splits, K,
+                                  splits, EPI_PARTIAL, stream);
+  if (err != hipSuccess) return err;
+  return launch_reduce(workspace, splits, M, N, bias, R, C, epilogue, stream);
 }
 
 }  // namespace kiosk

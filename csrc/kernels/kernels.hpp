@@ -11,6 +11,7 @@ enum Epilogue {
   EPI_NONE = 0,           // C = A.B^T
   EPI_BIAS_GELU = 1,      // C = gelu_tanh(A.B^T + bias)
   EPI_BIAS_RESIDUAL = 2,  // C = A.B^T + bias + R
+  EPI_PARTIAL = 3,        // internal: fp32 split-K partial planes
 };
 
 // GEMM tile geometry (shared with the warm-start kernel, which
@@ -31,16 +32,23 @@ bool gemm_shape_ok(int M, int N, int K);
 hipError_t gemm_prepare();  // call once before launching / capturing
 
 // Kernel variants: 0 = auto (256x256 ring kernel when it yields >= 256
-// tiles, else the 256x128 ring when that does, else 128x128), 1 = 128x128
-// two-barrier, 2 = 256x256 LDS ring, 3 = 256x128 LDS ring.
+// tiles, else split-K 256x256 when a workspace is given, else the 256x128
+// ring when that fills the chip, else 128x128), 1 = 128x128 two-barrier,
+// 2 = 256x256 LDS ring, 3 = 256x128 LDS ring, 4 = split-K 256x256 (fp32
+// partials in `workspace` + one fused reduce/epilogue kernel).
 enum GemmVariant {
-  GEMM_AUTO = 0, GEMM_128 = 1, GEMM_256 = 2, GEMM_256x128 = 3
+  GEMM_AUTO = 0, GEMM_128 = 1, GEMM_256 = 2, GEMM_256x128 = 3,
+  GEMM_256_SPLITK = 4
 };
 hipError_t launch_gemm_variant(const uint16_t* A, const uint16_t* B,
                                uint16_t* C, const float* bias,
                                const uint16_t* R, int M, int N, int K,
-                               int epilogue, int variant, hipStream_t stream);
-int gemm_pick_variant(int M, int N, int K);
+                               int epilogue, int variant, hipStream_t stream,
+                               float* workspace = nullptr,
+                               size_t workspace_bytes = 0);
+int gemm_pick_variant(int M, int N, int K, bool have_workspace = false);
+// bytes of fp32 workspace the split-K path needs for this shape (0: none)
+size_t gemm_workspace_bytes(int M, int N, int K);
 // 256 x bn ring kernel (gemm256.hip), bn = 256 or 128
 bool gemm256_shape_ok(int M, int N, int K, int bn = 256);
 hipError_t gemm256_prepare();
@@ -48,6 +56,13 @@ hipError_t launch_gemm256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                           const float* bias, const uint16_t* R, int M, int N,
                           int K, int epilogue, hipStream_t stream,
                           int bn = 256);
+int gemm256_splits(int M, int N, int K);
+size_t gemm256_splitk_workspace(int M, int N, int K);
+hipError_t launch_gemm256_splitk(const uint16_t* A, const uint16_t* B,
+                                 uint16_t* C, const float* bias,
+                                 const uint16_t* R, int M, int N, int K,
+                                 int epilogue, int splits, float* workspace,
+                                 size_t workspace_bytes, hipStream_t stream);
 
 // Uniform [lo, hi) init, counter-based (reproducible for a seed).
 hipError_t launch_init_uniform_bf16(uint16_t* p, size_t n, uint64_t seed,

@@ -63,12 +63,15 @@ PYBIND11_MODULE(_kiosk_hip, m) {
   m.attr("sum_blocks") = kiosk::kSumBlocks;
 
   m.def("gemm_shape_ok", &kiosk::gemm_shape_ok);
-  m.def("gemm_pick_variant", &kiosk::gemm_pick_variant);
+  m.def("gemm_pick_variant", &kiosk::gemm_pick_variant, py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("have_workspace") = false);
+  m.def("gemm_workspace_bytes", &kiosk::gemm_workspace_bytes);
   m.def(
       "gemm",
       [](unsigned long long a, unsigned long long b, unsigned long long c,
          unsigned long long bias, unsigned long long res, int M, int N, int K,
-         int epilogue, unsigned long long stream, int variant) {
+         int epilogue, unsigned long long stream, int variant,
+         unsigned long long workspace, unsigned long long workspace_bytes) {
         static bool prepared = false;
         if (!prepared) {
           check_hip(kiosk::gemm_prepare(), "gemm_prepare");
@@ -78,12 +81,14 @@ PYBIND11_MODULE(_kiosk_hip, m) {
                       ptr<const uint16_t>(a), ptr<const uint16_t>(b),
                       ptr<uint16_t>(c), ptr<const float>(bias),
                       ptr<const uint16_t>(res), M, N, K, epilogue, variant,
-                      stream_of(stream)),
+                      stream_of(stream), ptr<float>(workspace),
+                      static_cast<size_t>(workspace_bytes)),
                   "launch_gemm");
       },
       py::arg("a"), py::arg("b"), py::arg("c"), py::arg("bias") = 0,
       py::arg("res") = 0, py::arg("M"), py::arg("N"), py::arg("K"),
       py::arg("epilogue") = 0, py::arg("stream") = 0, py::arg("variant") = 0,
+      py::arg("workspace") = 0, py::arg("workspace_bytes") = 0,
       py::call_guard<py::gil_scoped_release>());
   m.def(
       "init_uniform_bf16",

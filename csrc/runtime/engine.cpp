@@ -44,7 +44,9 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   // 128x128 operands + bias + output + sums + warm-start record
   const size_t elems = 128 * 128;
   char* scratch = nullptr;
-  const size_t bytes = 4 * elems * 2 + 128 * 4 + kSumBlocks * 4 + 4096;
+  const size_t ws_bytes = 2 * 64 * 256 * sizeof(float);   // split-K probe
+  const size_t bytes =
+      4 * elems * 2 + 128 * 4 + kSumBlocks * 4 + 4096 + ws_bytes;
   check_hip(hipMalloc(reinterpret_cast<void**>(&scratch), bytes),
             "hipMalloc(preinit)");
   uint16_t* a = reinterpret_cast<uint16_t*>(scratch);
@@ -54,6 +56,7 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   float* bias = reinterpret_cast<float*>(r + elems);
   float* sums = bias + 128;
   uint32_t* rec = reinterpret_cast<uint32_t*>(sums + kSumBlocks);
+  float* ws = reinterpret_cast<float*>(scratch + bytes - ws_bytes);
   check_hip(launch_init_uniform_bf16(a, 4 * elems, 1, -1.f, 1.f, stream),
             "preinit init");
   check_hip(launch_init_uniform_f32(bias, 128, 2, -1.f, 1.f, stream),
@@ -70,6 +73,10 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
                                bn),
                 "preinit gemm256");
     }
+    // split-K partial kernel + this epilogue's reduce kernel
+    check_hip(launch_gemm256_splitk(a, b, c, bias, r, 64, 256, 64, epi, 2, ws,
+                                    ws_bytes, stream),
+              "preinit gemm256 split-K");
   }
   check_hip(launch_partial_sums(c, elems, sums, stream), "preinit sums");
   check_hip(launch_warmstart(a, elems, rec, 1, 1, 2 * kGemmLdsBytes, stream),
@@ -130,6 +137,17 @@ Engine::Engine(int device, int dim, int hidden, int layers, int max_rows,
   const size_t h_off = off; off = align_up(off + size_t(max_rows) * hidden * 2, A);
   const size_t p_off = off; off = align_up(off + kSumBlocks * 4, A);
   const size_t s_off = off; off = align_up(off + 8, A);
+  // split-K workspace: the largest fp32 partial set either GEMM can want
+  // for any row count up to max_rows (the split count changes only at
+  // 256-row boundaries, so probing those and max_rows covers every M)
+  size_t ws = 0;
+  for (int m = 256; m < max_rows + 256; m += 256) {
+    const int rows = std::min(m, max_rows);
+    ws = std::max(ws, gemm_workspace_bytes(rows, hidden, dim));
+    ws = std::max(ws, gemm_workspace_bytes(rows, dim, hidden));
+  }
+  const size_t w_off = off; off = align_up(off + ws, A);
+  workspace_bytes_ = ws;
   arena_bytes_ = off;
   check_hip(hipMalloc(reinterpret_cast<void**>(&arena_), arena_bytes_),
             "hipMalloc(arena)");
@@ -144,6 +162,7 @@ Engine::Engine(int device, int dim, int hidden, int layers, int max_rows,
   h_ = reinterpret_cast<uint16_t*>(arena_ + h_off);
   partials_ = reinterpret_cast<float*>(arena_ + p_off);
   seed_dev_ = reinterpret_cast<unsigned long long*>(arena_ + s_off);
+  workspace_ = ws ? reinterpret_cast<float*>(arena_ + w_off) : nullptr;
   check_hip(hipHostMalloc(reinterpret_cast<void**>(&seed_host_), 8),
             "hipHostMalloc(seed)");
   check_hip(hipHostMalloc(reinterpret_cast<void**>(&partials_host_),
@@ -271,11 +290,13 @@ void Engine::enqueue_forward(int rows) {
   for (int l = 0; l < layers_; ++l) {
     launch_or_throw(launch_gemm_variant(cur, w1_[l], h_, b1_[l], nullptr, rows,
                                         hidden_, dim_, EPI_BIAS_GELU,
-                                        GEMM_AUTO, stream_),
+                                        GEMM_AUTO, stream_, workspace_,
+                                        workspace_bytes_),
                     "gemm1");
     launch_or_throw(launch_gemm_variant(h_, w2_[l], nxt, b2_[l], cur, rows,
                                         dim_, hidden_, EPI_BIAS_RESIDUAL,
-                                        GEMM_AUTO, stream_),
+                                        GEMM_AUTO, stream_, workspace_,
+                                        workspace_bytes_),
                     "gemm2");
     std::swap(cur, nxt);
   }
@@ -368,6 +389,7 @@ std::map<std::string, double> Engine::info() const {
   out["hbm_free_bytes"] = static_cast<double>(free_b);
   out["hbm_total_bytes"] = static_cast<double>(total_b);
   out["arena_bytes"] = static_cast<double>(arena_bytes_);
+  out["workspace_bytes"] = static_cast<double>(workspace_bytes_);
   out["graphs"] = static_cast<double>(graphs_.size());
   int clock_khz = 0;
   hipDeviceGetAttribute(&clock_khz, hipDeviceAttributeClockRate, device_);

@@ -94,6 +94,8 @@ class Engine {
   uint16_t* y_ = nullptr;      // layer output / pong
   uint16_t* h_ = nullptr;      // hidden activation
   float* partials_ = nullptr;
+  float* workspace_ = nullptr;     // split-K fp32 partials (may be null)
+  size_t workspace_bytes_ = 0;
   unsigned long long* seed_dev_ = nullptr;
   unsigned long long* seed_host_ = nullptr;   // pinned staging
   float* partials_host_ = nullptr;            // pinned

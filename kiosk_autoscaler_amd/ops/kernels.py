@@ -24,7 +24,7 @@ def _check_bf16(t, name):
         raise ValueError('%s must be a contiguous bf16 CUDA tensor' % name)
 
 
-VARIANTS = {'auto': 0, '128': 1, '256': 2, '256x128': 3}
+VARIANTS = {'auto': 0, '128': 1, '256': 2, '256x128': 3, '256splitk': 4}
 
 
 def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
@@ -34,8 +34,10 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
     ``epilogue``: ``'none'``, ``'gelu'`` (``gelu_tanh(a@b.T + bias)``) or
     ``'residual'`` (``a@b.T + bias + residual``).  ``variant``: ``'auto'``
     (256x256 LDS-ring kernel when the grid fills the chip, else the 256x128
-    ring when that does, else 128x128), ``'128'``, ``'256'`` or
-    ``'256x128'``."""
+    ring when that does, else 128x128; split-K 256x256 where the grid alone
+    would leave CUs idle), ``'128'``, ``'256'``, ``'256x128'`` or
+    ``'256splitk'`` (fp32 partials in a temporary workspace + one fused
+    reduce/epilogue kernel)."""
     import torch
     mod = native.load()
     _check_bf16(a, 'a')
@@ -44,7 +46,12 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
     N, K2 = b.shape
     if K != K2:
         raise ValueError('inner dimensions differ: %d vs %d' % (K, K2))
-    if variant in ('256', '256x128'):
+    if variant == '256splitk':
+        if mod.gemm_workspace_bytes(M, N, K) == 0:
+            raise ValueError('split-K does not apply to M=%d N=%d K=%d '
+                             '(the 256x256 grid already fills the chip, or '
+                             'K is too short)' % (M, N, K))
+    elif variant in ('256', '256x128'):
         bn = 256 if variant == '256' else 128
         if M < 1 or N % bn or K % 32 or K < 32:
             raise ValueError('the 256x%d kernel needs N %% %d == 0 and '
@@ -63,10 +70,15 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
             raise ValueError('residual must be [M, N]')
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    ws_bytes = mod.gemm_workspace_bytes(M, N, K) \
+        if variant in ('auto', '256splitk') else 0
+    workspace = torch.empty(max(1, ws_bytes // 4), dtype=torch.float32,
+                            device=a.device) if ws_bytes else None
     mod.gemm(a.data_ptr(), b.data_ptr(), out.data_ptr(),
              bias.data_ptr() if bias is not None else 0,
              residual.data_ptr() if residual is not None else 0,
-             M, N, K, epi, _stream(), VARIANTS[variant])
+             M, N, K, epi, _stream(), VARIANTS[variant],
+             workspace.data_ptr() if workspace is not None else 0, ws_bytes)
     return out
 
 

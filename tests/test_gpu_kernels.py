@@ -228,3 +228,37 @@ def test_spin_kernel_and_roctx(mod):
     mod.roctx_push('kiosk.test')
     mod.roctx_mark('kiosk.test.mark')
     mod.roctx_pop()
+
+
+@pytest.mark.parametrize('M,N,K', [(2048, 1024, 4096), (512, 512, 16384),
+                                   (300, 512, 8192)])
+@pytest.mark.parametrize('epilogue', ['none', 'gelu', 'residual'])
+def test_gemm_splitk(mod, M, N, K, epilogue):
+    """Split-K 256x256: fp32 partial planes + fused reduce/epilogue."""
+    from kiosk_autoscaler_amd.ops import kernels
+    assert mod.gemm_workspace_bytes(M, N, K) > 0
+    a = rand_bf16(M, K, seed=21)
+    b = rand_bf16(N, K, scale=0.05, seed=22)
+    bias = torch.randn(N, device='cuda')
+    res = rand_bf16(M, N, seed=23)
+    ref = a.float() @ b.float().t()
+    if epilogue != 'none':
+        ref = ref + bias
+    if epilogue == 'gelu':
+        ref = gelu_tanh(ref)
+    if epilogue == 'residual':
+        ref = ref + res.float()
+    c = kernels.gemm(a, b, bias=bias, residual=res, epilogue=epilogue,
+                     variant='256splitk')
+    torch.testing.assert_close(c.float(), ref, atol=3e-2, rtol=2e-2)
+    auto = kernels.gemm(a, b, bias=bias, residual=res, epilogue=epilogue)
+    assert torch.equal(auto, c)          # auto picks split-K here
+
+
+def test_splitk_dispatch(mod):
+    assert mod.gemm_pick_variant(2048, 4096, 16384, True) == 4
+    assert mod.gemm_pick_variant(2048, 4096, 16384, False) == 3
+    assert mod.gemm_pick_variant(2048, 16384, 4096, True) == 2
+    assert mod.gemm_workspace_bytes(2048, 16384, 4096) == 0
+    assert mod.gemm_workspace_bytes(2048, 4096, 16384) == \
+        2 * 2048 * 4096 * 4

@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     import torch
-    from kiosk_autoscaler_amd.ops import kernels
+    from kiosk_autoscaler_amd.ops import kernels, native
+    mod = native.load()
     parser = argparse.ArgumentParser()
     parser.add_argument('--iters', type=int, default=20)
     parser.add_argument('--rounds', type=int, default=5)
@@ -41,6 +42,9 @@ def main():
         def ours_256x128():
             kernels.gemm(a, b, out=out, variant='256x128')
 
+        def ours_splitk():
+            kernels.gemm(a, b, out=out, variant='256splitk')
+
         def theirs():
             torch.nn.functional.gelu(torch.addmm(bias.to(torch.bfloat16), a,
                                                  b.t()), approximate='tanh')
@@ -53,6 +57,8 @@ def main():
         if N % 256 == 0:
             fns['native256'] = ours_256
         fns['native256x128'] = ours_256x128
+        if mod.gemm_workspace_bytes(M, N, K):
+            fns['native256splitk'] = ours_splitk
 
         results = {k: [] for k in fns}
         for fn in fns.values():
