@@ -286,41 +286,70 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   // drain the tail DMAs before the workgroup's LDS can be released
   __builtin_amdgcn_s_waitcnt(kWaitAll);
 
+  // Epilogue.  Lane l holds row (l & 15), columns 4g..4g+3 (g = l >> 4) of
+  // every 16x16 tile.  Lanes l and l ^ 16 (same row, column groups g and
+  // g ^ 1) swap one tile's half of a tile pair (v_permlane16_swap, a VALU
+  // op), so every lane then owns 8 consecutive columns and issues one 16-B
+  // store where it issued two 8-B ones: the epilogue is store-issue-bound
+  // (guide T21).
+  auto finish = [&](int m, int nb, const f32x4& a, float (&v)[4]) {
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    if (EPI != EPI_NONE) {
+      const float4 b = *reinterpret_cast<const float4*>(bias + nb);
+      v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+    }
+    if (EPI == EPI_BIAS_GELU) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+    }
+    if (EPI == EPI_BIAS_RESIDUAL) {
+      const uint2 res = *reinterpret_cast<const uint2*>(
+          R + static_cast<size_t>(m) * N + nb);
+      v[0] += bf16_to_f32(res.x & 0xffff);
+      v[1] += bf16_to_f32(res.x >> 16);
+      v[2] += bf16_to_f32(res.y & 0xffff);
+      v[3] += bf16_to_f32(res.y >> 16);
+    }
+  };
+  auto pack2 = [](float lo, float hi) {
+    return f32_to_bf16(lo) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
+  };
+  const int g = lane >> 4;
+  const bool odd = (g & 1) != 0;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    // m is the same for lanes l and l ^ 16, so a skipped row skips both
+    // partners of every exchange below
     const int m = m0 + wm * (TM * 16) + i * 16 + (lane & 15);
     if (m >= M) continue;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int nb = n0 + wn * (TN * 16) + j * 16 + (lane >> 4) * 4;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      const int nb = n0 + wn * (TN * 16) + j * 16 + g * 4;
       if (EPI == EPI_PARTIAL) {
         float* P = reinterpret_cast<float*>(C) +
                    static_cast<size_t>(split) * M * N;
         *reinterpret_cast<float4*>(P + static_cast<size_t>(m) * N + nb) =
-            float4{v[0], v[1], v[2], v[3]};
-        continue;
+            float4{acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       }
-      if (EPI != EPI_NONE) {
-        const float4 b = *reinterpret_cast<const float4*>(bias + nb);
-        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-      }
-      if (EPI == EPI_BIAS_GELU) {
+    }
+    if (EPI == EPI_PARTIAL) continue;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
-      }
-      const size_t off = static_cast<size_t>(m) * N + nb;
-      if (EPI == EPI_BIAS_RESIDUAL) {
-        const uint2 res = *reinterpret_cast<const uint2*>(R + off);
-        v[0] += bf16_to_f32(res.x & 0xffff);
-        v[1] += bf16_to_f32(res.x >> 16);
-        v[2] += bf16_to_f32(res.y & 0xffff);
-        v[3] += bf16_to_f32(res.y >> 16);
-      }
-      uint2 out;
-      out.x = f32_to_bf16(v[0]) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
-      out.y = f32_to_bf16(v[2]) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
-      *reinterpret_cast<uint2*>(C + off) = out;
+    for (int jp = 0; jp < TN; jp += 2) {
+      const int base = n0 + wn * (TN * 16) + jp * 16;
+      float v0[4], v1[4];
+      finish(m, base + g * 4, acc[i][jp], v0);
+      finish(m, base + 16 + g * 4, acc[i][jp + 1], v1);
+      // v_permlane16_swap(X, Y) swaps the odd 16-lane rows of X with the
+      // even rows of Y.  With X = this lane's tile-jp half and Y = its
+      // tile-(jp+1) half, even rows end with {own jp, partner's jp} and odd
+      // rows with {partner's jp+1, own jp+1}: both are {X', Y'}.
+      const auto x0 = __builtin_amdgcn_permlane16_swap(
+          pack2(v0[0], v0[1]), pack2(v1[0], v1[1]), false, false);
+      const auto x1 = __builtin_amdgcn_permlane16_swap(
+          pack2(v0[2], v0[3]), pack2(v1[2], v1[3]), false, false);
+      const uint4 out = uint4{x0[0], x1[0], x0[1], x1[1]};
+      const int col = odd ? base + 16 + (g - 1) * 4 : base + g * 4;
+      *reinterpret_cast<uint4*>(C + static_cast<size_t>(m) * N + col) = out;
     }
   }
 }
