@@ -46,7 +46,8 @@ METRIC = ('scale-up latency (s) first-key->GPU-ready + GPU-idle-% at fixed '
 # INTERVAL=5 (BASELINE config 4 at N=8): 3.13 s cold start, 65.6 % idle.
 BASELINE_LATENCY_S = 3.13
 BASELINE_IDLE_PCT = 65.6
-OUT_DIR = os.path.join(ROOT, 'gpurun_out')
+# KIOSK_BENCH_OUT redirects the detail/event files (tests use a tmp dir)
+OUT_DIR = os.environ.get('KIOSK_BENCH_OUT') or os.path.join(ROOT, 'gpurun_out')
 
 
 def log(msg):
@@ -409,6 +410,7 @@ def main():
                 'event_busy_wall_pct': _r(100.0 * summary['gpu_busy_s'] /
                                           max(1e-9, elapsed * args.gpus)),
                 'amdsmi_gfx_busy_pct': _r(gpu_util.mean_busy(util)),
+                'fence': {k: _r(v) for k, v in summary['fence'].items()},
                 'reference_sim_latency_s': _r(ref['latency_mean_s']),
                 'reference_sim_gpu_idle_pct': _r(ref['gpu_idle_pct']),
             }

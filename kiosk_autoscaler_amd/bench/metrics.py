@@ -156,6 +156,22 @@ def gpu_idle(events, t_lo, t_hi):
             alive_total / 1e9, busy_total / 1e9)
 
 
+def fence_stats(events):
+    """N4 membership fences seen in the run: transport(s), count, mean wall
+    time (manager: epoch start -> rank 0 ack), communicator set-up and
+    all-reduce times reported by rank 0."""
+    done = [e for e in events if e.get('ev') == 'fence_done']
+    return {
+        'fences': len(done),
+        'fence_transport': sorted({str(e.get('transport')) for e in done}),
+        'fence_wall_ms_mean': _mean([1e3 * e['wall_s'] for e in done
+                                     if e.get('wall_s') is not None]),
+        'fence_init_ms_mean': _mean([e.get('init_ms') for e in done]),
+        'fence_allreduce_us_mean': _mean([e.get('allreduce_us')
+                                          for e in done]),
+    }
+
+
 def summarize(events, episodes):
     per = [episode_metrics(events, ep) for ep in episodes]
     lat = [v for p in per for v in p['cold_starts_s']]
@@ -178,5 +194,6 @@ def summarize(events, episodes):
         'gpu_busy_s': busy_s,
         'keys': sum(p['keys'] for p in per),
         'keys_done': sum(p['keys_done'] for p in per),
+        'fence': fence_stats(events),
         'episodes': per,
     }

@@ -106,7 +106,7 @@ def test_loadgen_writes_hash_before_key(redis_client):
 
 @pytest.mark.slow
 def test_bench_cpu_smoke(tmp_path):
-    env = dict(os.environ, PYTHONPATH=ROOT)
+    env = dict(os.environ, PYTHONPATH=ROOT, KIOSK_BENCH_OUT=str(tmp_path))
     proc = subprocess.run(
         [sys.executable, os.path.join(ROOT, 'bench.py'), '--backend', 'cpu',
          '--steps', '1', '--warmup', '0', '--interval', '0.5', '--on', '1',
@@ -122,6 +122,7 @@ def test_bench_cpu_smoke(tmp_path):
     assert line['higher_is_better'] is False and line['n_gpus'] == 1
     assert line['keys_done'] == line['keys'] > 0
     assert line['value'] is not None and line['value'] < 1.0
+    assert (tmp_path / 'bench_detail_n1.json').exists()
 
 
 @pytest.mark.slow
@@ -129,7 +130,7 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
     """The driver's N>1 launch shape (torchrun, one rank per GPU) on CPU:
     ranks rendezvous over gloo, rank 0 alone drives the node-wide stack
     with MAX_PODS=2 and prints exactly one JSON line."""
-    env = dict(os.environ, PYTHONPATH=ROOT)
+    env = dict(os.environ, PYTHONPATH=ROOT, KIOSK_BENCH_OUT=str(tmp_path))
     proc = subprocess.run(
         [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
          '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
