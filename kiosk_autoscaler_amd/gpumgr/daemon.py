@@ -190,7 +190,19 @@ def main(argv=None):
     args = parser.parse_args(argv)
     settings = Settings(require_resource_name=False)
     initialize_logger(settings.DEBUG, log_file='')
-    manager = build_manager(settings).start()
+    # the manager needs Redis for requeue, persisted state, orphan recovery
+    # and the fence ids; unreachable Redis at start is fatal (crash-only,
+    # like the autoscaler: the supervisor restarts the daemon)
+    from ..redisq import RedisClient
+    from ..utils.events import EventLog
+    redis = RedisClient(host=settings.REDIS_HOST, port=settings.REDIS_PORT,
+                        backoff=settings.REDIS_INTERVAL)
+    if settings.EVENT_LOG == 'redis':
+        events = EventLog(redis_client=redis, source='gpumgr')
+    else:
+        events = EventLog(path=settings.EVENT_LOG or None, source='gpumgr')
+    manager = build_manager(settings, redis_client=redis,
+                            events=events).start()
     server = ManagerServer(manager, args.socket).start()
     logger.info('GPU manager listening on %s', args.socket)
     try:

@@ -187,3 +187,45 @@ def _dead(pid):
             return f.read().split()[2] == 'Z'
     except OSError:
         return True
+
+
+def test_daemon_mode_end_to_end(resp_server, tmp_path):
+    """GPUMGR=unix:<sock>: the manager runs as its own process (workers
+    outlive an autoscaler crash); the reconcile core talks to it over the
+    socket and the daemon's workers consume from Redis."""
+    import subprocess
+    import sys
+    sock = str(tmp_path / 'mgr.sock')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, REDIS_HOST=resp_server.host,
+               REDIS_PORT=str(resp_server.port), RESOURCE_NAME='worker',
+               QUEUES='predict', MAX_PODS='1', WORKER_BACKEND='cpu',
+               WARM_POOL='0', FENCE='store', REDIS_INTERVAL='0')
+    daemon = subprocess.Popen(
+        [sys.executable, '-m', 'kiosk_autoscaler_amd.gpumgr.daemon',
+         '--socket', sock], env=env, cwd=str(tmp_path),
+        stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        wait_for(lambda: os.path.exists(sock), timeout=30)
+        client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                             decode_responses=True)
+        enqueue(client, 2)
+        actuator = gpumgr.connect('unix:' + sock)
+        proxy = RedisClient(host=resp_server.host, port=resp_server.port,
+                            backoff=0)
+        scaler = Autoscaler(proxy, 'predict', actuator=actuator)
+        assert scaler.scale('default', 'deployment', 'worker', 0, 1, 1) == 1
+        wait_for(lambda: all(client.hget('predict:job%d' % i, 'status') ==
+                             'done' for i in range(2)), timeout=60)
+        # the daemon persisted its declared count in Redis
+        state = client.hgetall('kiosk:gpumgr:default:deployment:worker')
+        assert state['declared'] == '1'
+        assert scaler.scale('default', 'deployment', 'worker', 0, 1, 1) == 0
+        wait_for(lambda: actuator.list_namespaced_deployment('default')
+                 .items[0].status.available_replicas == 0, timeout=30)
+    finally:
+        daemon.terminate()
+        try:
+            daemon.wait(20)
+        except subprocess.TimeoutExpired:
+            daemon.kill()
