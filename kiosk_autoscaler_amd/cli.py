@@ -59,6 +59,14 @@ def build(settings=None, redis_client=None, actuator=None, events=None):
         else:
             manager = gpumgr.build_manager(settings, redis_client=redis_client,
                                            events=events)
+            if 0 < len(manager.slots) < settings.MAX_PODS:
+                # one worker per GPU, so MAX_PODS beyond the
+                # node's GPUs could only ever be pending
+                logging.getLogger('autoscaler').warning(
+                    'MAX_PODS=%d exceeds the %d GPU slots of this node; '
+                    'clamping to %d.', settings.MAX_PODS, len(manager.slots),
+                    len(manager.slots))
+                settings.MAX_PODS = len(manager.slots)
             manager.start()
             gpumgr.set_embedded(manager)
             actuator = manager

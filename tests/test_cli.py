@@ -117,3 +117,19 @@ def test_idle_interval_fast_path():
     cli.run_loop(scaler, _settings(INTERVAL=5, IDLE_INTERVAL=0.25),
                  max_ticks=4, sleep=sleeps.append, clock=lambda: 0.0)
     assert sleeps == [0.25, 0.25, 5]
+
+
+def test_max_pods_clamped_to_gpu_slots(resp_server):
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    s = _settings(MAX_PODS=5, GPU_IDS='0,1', WORKER_BACKEND='cpu',
+                  WARM_POOL=0, REDIS_HOST=resp_server.host,
+                  REDIS_PORT=resp_server.port, FENCE='none')
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    _, scaler, manager = cli.build(s, redis_client=client)
+    try:
+        assert s.MAX_PODS == 2 and len(manager.slots) == 2
+    finally:
+        manager.stop(timeout=5)
+        from kiosk_autoscaler_amd import gpumgr
+        gpumgr.set_embedded(None)
