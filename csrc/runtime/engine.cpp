@@ -107,6 +107,19 @@ Engine::Engine(int device, int dim, int hidden, int layers, int max_rows,
   if (layers < 1 || max_rows < 1) {
     throw std::invalid_argument("layers and max_rows must be >= 1");
   }
+  // a constructor that throws never runs the destructor: release whatever
+  // was created before the failure, then rethrow
+  try {
+    init(device, seed);
+  } catch (...) {
+    close();
+    throw;
+  }
+}
+
+void Engine::init(int device, unsigned long long seed) {
+  const int dim = dim_, hidden = hidden_, layers = layers_;
+  const int max_rows = max_rows_;
   stage("engine_enter");
   check_hip(hipSetDevice(device), "hipSetDevice");
   check_hip(hipFree(nullptr), "hip context init");

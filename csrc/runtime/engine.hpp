@@ -77,6 +77,7 @@ class Engine {
 
  private:
   void stage(const char* name);
+  void init(int device, unsigned long long seed);   // constructor body
   void enqueue_forward(int rows);              // one pass on stream_
   void launch_or_throw(hipError_t err, const char* what);
 

@@ -157,13 +157,25 @@ void Fence::wait_ready(void* comm, double timeout_s, const char* what) {
 Fence::Fence(const std::string& unique_id, int nranks, int rank,
              double timeout_s)
     : nranks_(nranks), rank_(rank), timeout_s_(timeout_s) {
-  TraceRange range("kiosk.fence.init");
   if (unique_id.size() != sizeof(ncclUniqueId)) {
     throw std::invalid_argument("unique id must be 128 bytes");
   }
   if (nranks < 1 || rank < 0 || rank >= nranks) {
     throw std::invalid_argument("bad rank / nranks");
   }
+  try {
+    init(unique_id);
+  } catch (...) {
+    abort();     // a half-built communicator is never finalized
+    destroy();   // frees the stream and buffers created so far
+    throw;
+  }
+}
+
+void Fence::init(const std::string& unique_id) {
+  TraceRange range("kiosk.fence.init");
+  const int nranks = nranks_, rank = rank_;
+  const double timeout_s = timeout_s_;
   const RcclApi& api = rccl();
   check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking),
             "fence stream");

@@ -45,6 +45,7 @@ class Fence {
 
  private:
   void wait_ready(void* comm, double timeout_s, const char* what);
+  void init(const std::string& unique_id);   // constructor body
 
   void* comm_ = nullptr;        // ncclComm_t
   hipStream_t stream_ = nullptr;
