@@ -53,9 +53,17 @@ def build(settings=None, redis_client=None, actuator=None, events=None):
     if actuator is None:
         if settings.GPUMGR.startswith('unix:') or \
                 settings.GPUMGR.startswith('k8s'):
-            # the daemon registers the resource from its own environment;
-            # with k8s the Deployment/Job already exists in the cluster
+            # with k8s the Deployment/Job already exists in the cluster; a
+            # shared manager daemon learns this autoscaler's resource here
+            # (an invalid RESOURCE_TYPE stays fatal at the first tick, as in
+            # the reference)
             actuator = gpumgr.connect(settings.GPUMGR)
+            if settings.GPUMGR.startswith('unix:') and \
+                    settings.RESOURCE_TYPE in ('deployment', 'job'):
+                actuator.register(settings.RESOURCE_TYPE,
+                                  settings.RESOURCE_NAMESPACE,
+                                  settings.RESOURCE_NAME,
+                                  gpumgr.template_for(settings))
         else:
             manager = gpumgr.build_manager(settings, redis_client=redis_client,
                                            events=events)

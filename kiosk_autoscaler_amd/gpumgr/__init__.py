@@ -66,6 +66,17 @@ def worker_env(settings, keys_per_pod=None):
     return env
 
 
+def template_for(settings, backend=None, keys_per_pod=None):
+    """The worker template (pod-template analog) of an autoscaler's
+    resource, from its settings."""
+    kpp = keys_per_pod or settings.KEYS_PER_POD
+    return WorkerTemplate(queues=settings.queues,
+                          module=settings.WORKER_MODULE,
+                          env=worker_env(settings, kpp),
+                          backend=backend or settings.WORKER_BACKEND,
+                          keys_per_pod=kpp)
+
+
 def build_manager(settings, redis_client=None, events=None, slots=None,
                   extra_env=None):
     """Build (not start) the manager + register the configured resource."""
@@ -85,12 +96,8 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
             settings.MODEL_LAYERS, settings.ROWS_PER_KEY,
             reserve=settings.HBM_RESERVE_BYTES,
             per_key=settings.HBM_PER_KEY_BYTES)
-    env = worker_env(settings, kpp)
-    env.update(extra_env or {})
-    template = WorkerTemplate(queues=settings.queues,
-                              module=settings.WORKER_MODULE,
-                              env=env, backend=backend,
-                              keys_per_pod=kpp)
+    template = template_for(settings, backend, kpp)
+    template.env.update(extra_env or {})
     pool = settings.WARM_POOL
     if pool < 0:
         pool = min(max(settings.MAX_PODS, 0), len(slots))
@@ -112,4 +119,4 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
 __all__ = ['GpuManager', 'WorkerTemplate', 'GpuManagerClient',
            'ManagerServer', 'GpuSlot', 'discover', 'ActuatorError',
            'ResourceList', 'ResourceView', 'connect', 'set_embedded',
-           'build_manager', 'resolve_backend']
+           'build_manager', 'resolve_backend', 'template_for']

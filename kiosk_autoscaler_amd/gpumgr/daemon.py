@@ -45,7 +45,14 @@ def handle_request(manager, request):
                          request['body'])
             return {'ok': True, 'item': view.to_dict()}
         if op == 'register':
+            # several autoscalers (one per consumer, as kiosk deploys them)
+            # can share this node's GPUs: each registers its own resource
             template = WorkerTemplate(**request['template'])
+            if template.backend == 'auto':
+                from . import resolve_backend
+                template.backend = resolve_backend('auto', manager.slots)
+            if template.backend == 'hip':
+                _size_for_hbm(template)
             view = manager.register(request['kind'], request['namespace'],
                                     request['name'], template)
             return {'ok': True, 'item': view.to_dict()}
@@ -56,6 +63,27 @@ def handle_request(manager, request):
         return {'ok': False, 'status': err.status, 'reason': err.reason}
     except (KeyError, TypeError, ValueError) as err:
         return {'ok': False, 'status': 400, 'reason': str(err)}
+
+
+def _size_for_hbm(template):
+    """Clamp a remotely registered template's KEYS_PER_POD to HBM, as
+    ``build_manager`` does for the daemon's own resource."""
+    from ..utils import hbm
+    env = template.env
+
+    def num(name, default):
+        try:
+            return int(env.get(name, default))
+        except (TypeError, ValueError):
+            return default
+    kpp = hbm.size_keys_per_pod(
+        template.keys_per_pod, num('MODEL_DIM', 4096),
+        num('MODEL_HIDDEN', 16384), num('MODEL_LAYERS', 4),
+        num('ROWS_PER_KEY', 2048),
+        reserve=num('HBM_RESERVE_BYTES', 8 << 30),
+        per_key=num('HBM_PER_KEY_BYTES', 0))
+    template.keys_per_pod = kpp
+    env['KEYS_PER_POD'] = kpp
 
 
 class _Handler(socketserver.StreamRequestHandler):

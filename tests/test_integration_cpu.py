@@ -229,3 +229,56 @@ def test_daemon_mode_end_to_end(resp_server, tmp_path):
             daemon.wait(20)
         except subprocess.TimeoutExpired:
             daemon.kill()
+
+
+def test_shared_daemon_serves_two_autoscalers(resp_server, tmp_path):
+    """Two autoscalers (one per consumer, as kiosk deploys them) share one
+    node's GPU slots through one manager daemon: each registers its own
+    resource and queue, and both get workers."""
+    import subprocess
+    import sys
+    sock = str(tmp_path / 'mgr.sock')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    base = dict(os.environ, PYTHONPATH=root, REDIS_HOST=resp_server.host,
+                REDIS_PORT=str(resp_server.port), WORKER_BACKEND='cpu',
+                FENCE='store', REDIS_INTERVAL='0')
+    daemon_env = dict(base, MAX_PODS='2', WARM_POOL='0')
+    daemon_env.pop('RESOURCE_NAME', None)
+    daemon = subprocess.Popen(
+        [sys.executable, '-m', 'kiosk_autoscaler_amd.gpumgr.daemon',
+         '--socket', sock], env=daemon_env, cwd=str(tmp_path),
+        stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        wait_for(lambda: os.path.exists(sock), timeout=30)
+        client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                             decode_responses=True)
+        scalers = []
+        for name, queue in (('seg', 'segmentation'), ('trk', 'tracking')):
+            s = settings_for(resp_server, RESOURCE_NAME=name, QUEUES=queue,
+                             GPUMGR='unix:' + sock, WARM_POOL='0')
+            proxy = RedisClient(host=resp_server.host, port=resp_server.port,
+                                backoff=0)
+            _, scaler, manager = __import__(
+                'kiosk_autoscaler_amd.cli', fromlist=['build']).build(
+                    s, redis_client=proxy)
+            assert manager is None
+            scalers.append((s, scaler))
+            enqueue(client, 2, queue=queue)
+        for s, scaler in scalers:
+            assert tick(scaler, s) == 1
+        wait_for(lambda: all(
+            client.hget('%s:job%d' % (q, i), 'status') == 'done'
+            for q in ('segmentation', 'tracking') for i in range(2)),
+            timeout=60)
+        status = gpumgr.connect('unix:' + sock).status()
+        names = sorted(r['metadata']['name'] for r in status['resources'])
+        assert names == ['seg', 'trk']
+        gpus_used = {w['gpu'] for r in status['resources']
+                     for w in r['workers']}
+        assert gpus_used == {0, 1}            # one slot each
+    finally:
+        daemon.terminate()
+        try:
+            daemon.wait(20)
+        except subprocess.TimeoutExpired:
+            daemon.kill()
