@@ -115,3 +115,31 @@ def test_gpu_hung_kernel_killed_by_watchdog(stack):
     dead = manager.history[0]
     assert dead['killed'].startswith('no progress')
     assert float(client.hget('predict:job0', 'compute_ms')) > 0
+
+
+@pytest.mark.gpu
+def test_gpu_worker_recycled_and_reused(stack):
+    """A drained HIP worker frees its engine and becomes the GPU's standby;
+    the next scale-up on that GPU reuses the same process (HIP context kept)
+    and serves with a freshly built engine."""
+    s, client, manager, scaler, events = stack(
+        WARM_POOL='1', WORKER_BACKEND='hip', FENCE='none',
+        MODEL_DIM='1024', MODEL_HIDDEN='4096', MODEL_LAYERS='2',
+        ROWS_PER_KEY='256')
+    wait_for(lambda: manager.standbys and all(
+        p.booted for p in manager.standbys.values()), timeout=120)
+    pid = manager.standbys[0].pid
+    for round_ in range(2):
+        client.delete('predict:job0')
+        enqueue(client, 1)
+        assert tick(scaler, s) == 1
+        wait_for(lambda: client.hget('predict:job0', 'status') == 'done',
+                 timeout=120)
+        worker = manager.status()['resources'][0]['workers'][0]
+        assert worker['pid'] == pid and worker['from_pool']
+        assert tick(scaler, s) == 0
+        wait_for(lambda: 0 in manager.standbys and
+                 manager.standbys[0].booted, timeout=60)
+        assert manager.standbys[0].pid == pid
+    ready = [e for e in events.records if e['ev'] == 'worker_recycled']
+    assert len(ready) == 2
