@@ -24,7 +24,10 @@ Contract: ``python bench.py --gpus N --steps K --warmup W`` (torchrun with
 N ranks for N > 1; rank 0 drives, every rank brackets the K timed steps with
 barrier + torch.cuda.synchronize(), elapsed = max over ranks).  Scaling is
 weak: arrival rate = ``--lam-per-gpu`` x N (0.25/s per GPU -> 2/s at N = 8,
-exactly BASELINE config 4).  Rank 0 prints one JSON line.
+exactly BASELINE config 4) in 60 s bursts (``--on``, config 4's "60 s on");
+config 4's 60 s off period is shortened to "until the stack has scaled to
+zero, then ``--off`` s", because nothing is measured while no worker is
+alive.  Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -260,7 +263,7 @@ def parse_args():
     p.add_argument('--warmup', type=int, default=1)
     p.add_argument('--interval', type=float, default=5.0)
     p.add_argument('--lam-per-gpu', type=float, default=0.25)
-    p.add_argument('--on', type=float, default=20.0)
+    p.add_argument('--on', type=float, default=60.0)
     p.add_argument('--off', type=float, default=2.0)
     p.add_argument('--service-ms', type=int, default=1000)
     p.add_argument('--queues', default='predict')
@@ -389,7 +392,9 @@ def main():
                     'parallelism': 'replica-dp%d' % args.gpus,
                     'queues': args.queues, 'interval_s': args.interval,
                     'lambda_per_s': args.lam_per_gpu * args.gpus,
-                    'on_s': args.on, 'service_s': args.service_ms / 1e3,
+                    'on_s': args.on,
+                    'off': 'until scaled to zero, then %g s' % args.off,
+                    'service_s': args.service_ms / 1e3,
                     'max_pods': args.gpus, 'keys_per_pod': args.kpp,
                     'policy': args.policy, 'resource_type': args.resource_type,
                     'idle_interval_s': args.idle_interval,
