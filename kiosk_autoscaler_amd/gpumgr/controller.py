@@ -695,6 +695,25 @@ class GpuManager(object):
     def _reconcile(self, resource):
         live = resource.live()
         if len(live) < resource.declared and not self._stopping:
+            # a deployment scaling back up while one of its workers is still
+            # draining: cancel the drain instead of waiting for the process
+            # to leave and starting over (if the worker has already left its
+            # serving loop, it reports `recycled` and is replaced as usual)
+            if resource.kind == 'deployment':
+                for worker in resource.workers.values():
+                    if len(live) >= resource.declared:
+                        break
+                    if worker.state == DRAINING and not worker.kill_reason \
+                            and worker.t_ready:
+                        if worker.proc.pipe.send({'cmd': 'undrain'}):
+                            worker.state = READY
+                            live.append(worker)
+                            self.events.emit('worker_undrain',
+                                             worker=worker.id)
+                            logger.info('Cancelled the drain of worker %s.',
+                                        worker.id)
+                if len(live) >= resource.declared:
+                    return
             if time.monotonic() < resource.restart_backoff_until:
                 return
             free = self._free_slots()

@@ -1,8 +1,8 @@
 """Worker side of the manager <-> worker pipe protocol.
 
 Manager -> worker (``--cmd-fd``), one JSON object per line:
-``assign`` (GPU, template, ids), ``drain``, ``fence`` / ``fence_abort``,
-``exit``.  Worker -> manager (``--ev-fd``): ``standby``, ``stage``,
+``assign`` (GPU, template, ids), ``drain`` / ``undrain``, ``fence`` /
+``fence_abort``, ``exit``.  Worker -> manager (``--ev-fd``): ``standby``, ``stage``,
 ``ready``, ``busy`` / ``beat`` / ``idle``, ``fenced``, ``recycled``,
 ``error``.
 """

@@ -160,6 +160,10 @@ class WorkerRuntime(object):
             if cmd == 'drain':
                 self.draining = True
                 self.recycle = bool(message.get('recycle', False))
+            elif cmd == 'undrain':
+                # the manager scaled back up before this loop noticed the
+                # drain: keep serving (a no-op once the loop has exited)
+                self.draining = False
             elif cmd in ('exit', 'eof'):
                 self.draining = True
                 self.recycle = False

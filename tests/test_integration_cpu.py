@@ -282,3 +282,25 @@ def test_shared_daemon_serves_two_autoscalers(resp_server, tmp_path):
             daemon.wait(20)
         except subprocess.TimeoutExpired:
             daemon.kill()
+
+
+def test_scale_up_during_drain_cancels_it(stack):
+    s, client, manager, scaler, events = stack(WARM_POOL='1',
+                                               extra_env={
+                                                   'POLL_BLOCK_S': '1.0'})
+    wait_for(lambda: manager.standbys and all(
+        p.booted for p in manager.standbys.values()))
+    manager.patch_namespaced_deployment('worker', 'default',
+                                        {'spec': {'replicas': 1}})
+    wait_for(lambda: manager.list_namespaced_deployment('default')
+             .items[0].status.available_replicas == 1)
+    wid = manager.status()['resources'][0]['workers'][0]['id']
+    manager.patch_namespaced_deployment('worker', 'default',
+                                        {'spec': {'replicas': 0}})
+    manager.patch_namespaced_deployment('worker', 'default',
+                                        {'spec': {'replicas': 1}})
+    assert any(e['ev'] == 'worker_undrain' for e in events.records)
+    enqueue(client, 1)
+    wait_for(lambda: client.hget('predict:job0', 'status') == 'done')
+    assert client.hget('predict:job0', 'worker') == wid   # never left
+    assert not any(e['ev'] == 'worker_exit' for e in events.records)
