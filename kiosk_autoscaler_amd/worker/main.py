@@ -59,7 +59,12 @@ def main(argv=None):
     parser.add_argument('--assign', default=None)
     parser.add_argument('--pin', default=None,
                         help='standby: JSON {gpu, slot, cpus, preinit}')
+    parser.add_argument('--standalone', action='store_true',
+                        help='run as a plain pod/service (no manager): '
+                             'config from the environment, drain on SIGTERM')
     args = parser.parse_args(argv)
+    if args.standalone:
+        return _standalone(args.backend)
     _die_with_parent()
 
     logging.basicConfig(
@@ -129,6 +134,42 @@ def main(argv=None):
     sys.stdout.flush()
     sys.stderr.flush()
     os._exit(code)
+
+
+def _standalone(backend):
+    """Worker as a Kubernetes pod (``GPUMGR=k8s``) or any supervisor: the
+    GPU is whatever the device plugin exposed, the worker id is the pod's
+    hostname (the kiosk consumer convention for ``processing-<q>:<host>``),
+    SIGTERM (a scale-down) finishes the in-flight key and exits 0, and a
+    ``job`` worker exits when the queue is empty."""
+    import signal
+    import socket
+    logging.basicConfig(
+        level=logging.INFO, stream=sys.stderr,
+        format='[%(asctime)s]:[%(levelname)s]:[%(name)s]: %(message)s')
+    from .channel import Channel
+    if backend == 'auto':
+        try:
+            import torch
+            backend = 'hip' if torch.cuda.device_count() > 0 else 'cpu'
+        except ImportError:
+            backend = 'cpu'
+    os.environ.setdefault('FENCE', 'none')   # no manager to run epochs
+    _preload(backend)
+    channel = Channel(None, None)
+    assignment = {
+        'cmd': 'assign', 'gpu': '', 'slot': 0,
+        'worker_id': os.environ.get('WORKER_ID') or socket.gethostname(),
+        'kind': os.environ.get('RESOURCE_TYPE', 'deployment'),
+        'template': {}, 'recycle': False}
+
+    def on_sigterm(signum, frame):
+        channel.commands.put({'cmd': 'drain', 'reason': 'SIGTERM'})
+    signal.signal(signal.SIGTERM, on_sigterm)
+    code, _ = _serve(assignment, backend, channel)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    return code
 
 
 def _wait_for_assignment(channel, pin, preload_ns, backend, preinit):

@@ -117,3 +117,63 @@ def test_missing_package_is_a_clear_error(monkeypatch):
     with pytest.raises(ActuatorError) as info:
         gpumgr.connect('k8s')
     assert info.value.status == 503 and 'kubernetes' in str(info.value)
+
+
+def _standalone(resp_server, tmp_path, **env):
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    full = dict(os.environ, PYTHONPATH=root, REDIS_HOST=resp_server.host,
+                REDIS_PORT=str(resp_server.port), QUEUES='predict',
+                REDIS_INTERVAL='0', MOCK_WORK_MS='10')
+    full.update(env)
+    return subprocess.Popen(
+        [sys.executable, '-m', 'kiosk_autoscaler_amd.worker.main',
+         '--standalone', '--backend', 'cpu'], env=full, cwd=str(tmp_path),
+        stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+
+
+def _wait(pred, timeout=30):
+    import time
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        if pred():
+            return True
+        time.sleep(0.05)
+    raise AssertionError('timeout')
+
+
+@pytest.mark.slow
+def test_standalone_worker_pod_drains_on_sigterm(resp_server, tmp_path):
+    """The worker as a plain Kubernetes pod (GPUMGR=k8s deployments):
+    hostname-named processing keys, graceful exit 0 on SIGTERM."""
+    import signal
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    proc = _standalone(resp_server, tmp_path, WORKER_ID='pod-a')
+    try:
+        for i in range(3):
+            client.hset('predict:k%d' % i, mapping={'status': 'new'})
+            client.lpush('predict', 'predict:k%d' % i)
+        _wait(lambda: all(client.hget('predict:k%d' % i, 'status') == 'done'
+                          for i in range(3)))
+        assert client.hget('predict:k0', 'worker') == 'pod-a'
+        proc.send_signal(signal.SIGTERM)
+        assert proc.wait(20) == 0
+        assert not list(client.scan_iter(match='processing-predict:*'))
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+
+
+@pytest.mark.slow
+def test_standalone_job_pod_completes(resp_server, tmp_path):
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    client.lpush('predict', 'plain-item')
+    proc = _standalone(resp_server, tmp_path, WORKER_ID='job-a',
+                       RESOURCE_TYPE='job', JOB_IDLE_EXIT_S='0.3')
+    assert proc.wait(30) == 0          # the Job's pod completes
+    assert client.llen('predict') == 0
