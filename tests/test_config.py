@@ -54,3 +54,26 @@ def test_cast_bool():
     assert not cast_bool('off') and not cast_bool('0')
     with pytest.raises(ValueError):
         cast_bool('maybe')
+
+
+def test_k8s_manifests_are_valid_settings():
+    """deploy/k8s/*.yaml parse, and the autoscaler container's environment
+    is a complete Settings (GPUMGR=k8s)."""
+    import os
+    import yaml
+    from kiosk_autoscaler_amd.config import Config, Settings
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    docs = []
+    for name in ('autoscaler.yaml', 'worker.yaml'):
+        with open(os.path.join(root, 'deploy', 'k8s', name)) as handle:
+            docs.extend(yaml.safe_load_all(handle))
+    scaler = [d for d in docs if d['kind'] == 'Deployment' and
+              d['metadata']['name'] == 'segmentation-autoscaler'][0]
+    env = {e['name']: e['value'] for e in
+           scaler['spec']['template']['spec']['containers'][0]['env']}
+    s = Settings(Config(environ=env, use_files=False))
+    assert s.GPUMGR == 'k8s' and s.MAX_PODS == 8
+    worker = [d for d in docs if d['metadata']['name'] ==
+              'segmentation-consumer'][0]
+    assert worker['spec']['template']['spec']['containers'][0][
+        'resources']['limits']['amd.com/gpu'] == 1
