@@ -30,6 +30,8 @@ from .utils.events import NULL as NULL_EVENTS
 class Autoscaler(object):
     """Read Redis and scale GPU worker processes when required.
 
+    Reference: ``autoscaler/autoscaler.py:41-58`` (class, constructor).
+
     Args:
         redis_client: Redis client (``RedisClient`` proxy, ``Redis`` or fake).
         queues: delimiter-joined queue names.
@@ -72,7 +74,9 @@ class Autoscaler(object):
 
     # -- C6 ------------------------------------------------------------------
     def tally_queues(self):
-        """Update ``redis_keys[q] = LLEN q + #keys('processing-q:*')``."""
+        """Update ``redis_keys[q] = LLEN q + #keys('processing-q:*')``.
+
+        Reference: ``autoscaler/autoscaler.py:60-77``."""
         start = self._clock()
         for queue in self.redis_keys:
             self.logger.debug('Tallying items in queue `%s`.', queue)
@@ -111,7 +115,8 @@ class Autoscaler(object):
 
     # -- C7-C9: actuator access ------------------------------------------------
     def get_actuator(self):
-        """The ``get_apps_v1_client``/``get_batch_v1_client`` analog."""
+        """The ``get_apps_v1_client``/``get_batch_v1_client`` analog
+        (``autoscaler/autoscaler.py:79-87``)."""
         if self.actuator is None:
             from .gpumgr import connect
             self.actuator = connect()
@@ -130,6 +135,7 @@ class Autoscaler(object):
         return result
 
     def list_namespaced_deployment(self, namespace):
+        """Reference: ``autoscaler/autoscaler.py:89-104``."""
         items = self._timed('list_namespaced_deployment',
                             self.get_actuator().list_namespaced_deployment,
                             namespace).items
@@ -139,6 +145,7 @@ class Autoscaler(object):
         return items
 
     def list_namespaced_job(self, namespace):
+        """Reference: ``autoscaler/autoscaler.py:106-119``."""
         items = self._timed('list_namespaced_job',
                             self.get_actuator().list_namespaced_job,
                             namespace).items
@@ -147,11 +154,13 @@ class Autoscaler(object):
         return items
 
     def patch_namespaced_deployment(self, name, namespace, body):
+        """Reference: ``autoscaler/autoscaler.py:121-134``."""
         return self._timed('patch_namespaced_deployment',
                            self.get_actuator().patch_namespaced_deployment,
                            name, namespace, body)
 
     def patch_namespaced_job(self, name, namespace, body):
+        """Reference: ``autoscaler/autoscaler.py:136-151``."""
         return self._timed('patch_namespaced_job',
                            self.get_actuator().patch_namespaced_job,
                            name, namespace, body)
@@ -164,7 +173,9 @@ class Autoscaler(object):
 
     def get_current_pods(self, namespace, resource_type, name,
                          only_running=False):
-        """Declared worker count (or READY count with ``only_running``)."""
+        """Declared worker count (or READY count with ``only_running``).
+
+        Reference: ``autoscaler/autoscaler.py:153-195``."""
         self._check_type(resource_type)
         if resource_type == 'deployment':
             items = self.list_namespaced_deployment(namespace)
@@ -186,6 +197,7 @@ class Autoscaler(object):
 
     # -- C11 / C12 -------------------------------------------------------------
     def clip_pod_count(self, desired_pods, min_pods, max_pods, current_pods):
+        """Reference: ``autoscaler/autoscaler.py:197-213``."""
         clipped = policies.clip_pod_count(desired_pods, min_pods, max_pods,
                                           current_pods)
         if clipped != desired_pods:
@@ -195,12 +207,14 @@ class Autoscaler(object):
 
     def get_desired_pods(self, key, keys_per_pod, min_pods, max_pods,
                          current_pods):
+        """Reference: ``autoscaler/autoscaler.py:215-219`` (floor)."""
         return self.clip_pod_count(self.redis_keys[key] // keys_per_pod,
                                    min_pods, max_pods, current_pods)
 
     # -- C13 -----------------------------------------------------------------
     def scale_resource(self, desired_pods, current_pods, resource_type,
                        namespace, name):
+        """Reference: ``autoscaler/autoscaler.py:221-242``."""
         if resource_type not in self.managed_resource_types:
             raise ValueError('Cannot scale resource type: %s' % resource_type)
         if desired_pods == current_pods:
@@ -243,7 +257,9 @@ class Autoscaler(object):
 
     def scale(self, namespace, resource_type, name, min_pods=0, max_pods=1,
               keys_per_pod=1):
-        """One reconcile tick.  Returns the target replica count."""
+        """One reconcile tick.  Returns the target replica count.
+
+        Reference: ``autoscaler/autoscaler.py:244-273``."""
         self.tally_queues()
         self.logger.debug('Scaling %s `%s.%s`.', resource_type, namespace,
                           name)
