@@ -30,7 +30,7 @@ from .utils.events import NULL as NULL_EVENTS
 class Autoscaler(object):
     """Read Redis and scale GPU worker processes when required.
 
-    Reference: ``autoscaler/autoscaler.py:41-58`` (class, constructor).
+    Reference: ``autoscaler/autoscaler.py:37-58`` (class, constructor).
 
     Args:
         redis_client: Redis client (``RedisClient`` proxy, ``Redis`` or fake).
@@ -154,13 +154,13 @@ class Autoscaler(object):
         return items
 
     def patch_namespaced_deployment(self, name, namespace, body):
-        """Reference: ``autoscaler/autoscaler.py:121-134``."""
+        """Reference: ``autoscaler/autoscaler.py:121-135``."""
         return self._timed('patch_namespaced_deployment',
                            self.get_actuator().patch_namespaced_deployment,
                            name, namespace, body)
 
     def patch_namespaced_job(self, name, namespace, body):
-        """Reference: ``autoscaler/autoscaler.py:136-151``."""
+        """Reference: ``autoscaler/autoscaler.py:137-151``."""
         return self._timed('patch_namespaced_job',
                            self.get_actuator().patch_namespaced_job,
                            name, namespace, body)
