@@ -260,6 +260,7 @@ class Autoscaler(object):
         """One reconcile tick.  Returns the target replica count.
 
         Reference: ``autoscaler/autoscaler.py:244-273``."""
+        tick_start = self._clock()
         self.tally_queues()
         self.logger.debug('Scaling %s `%s.%s`.', resource_type, namespace,
                           name)
@@ -271,7 +272,9 @@ class Autoscaler(object):
                           str(resource_type).capitalize(), name, namespace,
                           current_pods, desired_pods)
         self.events.emit('tick', keys=dict(self.redis_keys),
-                         current=current_pods, desired=desired_pods)
+                         in_progress=dict(self.in_progress),
+                         current=current_pods, desired=desired_pods,
+                         tick_s=self._clock() - tick_start)
         self.last_decision = desired_pods
         try:
             self.scale_resource(desired_pods, current_pods, resource_type,

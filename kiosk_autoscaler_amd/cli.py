@@ -78,6 +78,10 @@ def build(settings=None, redis_client=None, actuator=None, events=None):
             manager.start()
             gpumgr.set_embedded(manager)
             actuator = manager
+    if settings.METRICS_PORT:
+        from .utils import metrics
+        metrics.attach(events, settings.METRICS_PORT, manager=manager,
+                       addr=settings.METRICS_ADDR)
     scaler = Autoscaler(redis_client=redis_client, queues=settings.QUEUES,
                         queue_delim=settings.QUEUE_DELIMITER,
                         actuator=actuator, policy=settings.SCALE_POLICY,

@@ -164,6 +164,8 @@ EXTRA_DEFAULTS = (
     ('WORKER_TIMEOUT', float, 0.0),         # s without progress while busy -> kill (0 = off)
     ('START_TIMEOUT', float, 0.0),          # s from assignment to READY -> kill (0 = off)
     ('WORKER_RECYCLE', bool, True),         # drained worker -> back to the warm pool
+    ('METRICS_PORT', int, 0),               # Prometheus /metrics port (0 = off)
+    ('METRICS_ADDR', str, '0.0.0.0'),
     ('DEBUG', bool, True),
     ('LOG_FILE', str, 'autoscaler.log'),
 )

@@ -749,6 +749,12 @@ class GpuManager(object):
                 worker.resource.fence_wanted = True
                 worker.resource.consecutive_failures = 0
                 self._publish_worker(worker)
+                self.events.emit('worker_up', worker=worker.id,
+                                 gpu=worker.slot.index,
+                                 from_pool=worker.from_pool,
+                                 resource=worker.resource.name,
+                                 ready_s=(worker.t_ready -
+                                          worker.t_assigned) / 1e9)
                 logger.info('Worker %s READY on GPU %s after %.3f s.',
                             worker.id, worker.slot.index,
                             (worker.t_ready - worker.t_assigned) / 1e9)

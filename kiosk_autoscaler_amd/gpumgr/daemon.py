@@ -231,6 +231,10 @@ def main(argv=None):
         events = EventLog(path=settings.EVENT_LOG or None, source='gpumgr')
     manager = build_manager(settings, redis_client=redis,
                             events=events).start()
+    if settings.METRICS_PORT:
+        from ..utils import metrics
+        metrics.attach(events, settings.METRICS_PORT, manager=manager,
+                       addr=settings.METRICS_ADDR)
     server = ManagerServer(manager, args.socket).start()
     logger.info('GPU manager listening on %s', args.socket)
     try:

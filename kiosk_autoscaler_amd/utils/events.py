@@ -35,6 +35,9 @@ class EventLog(object):
         self._fh = None
         self.records = []
         self.keep = False
+        # in-process consumers of every record (e.g. the Prometheus
+        # exporter); an observer's failure never reaches the emitter
+        self.observers = []
 
     def emit(self, _event, t_ns=None, **fields):
         record = {"ev": _event, 't': now_ns() if t_ns is None else int(t_ns),
@@ -53,6 +56,11 @@ class EventLog(object):
                 self.redis_client.rpush(self.redis_key, line)
             except Exception:  # pylint: disable=broad-except
                 pass  # observability must never take the control loop down
+        for observer in list(self.observers):
+            try:
+                observer(record)
+            except Exception:  # pylint: disable=broad-except
+                pass
         return record
 
     def close(self):

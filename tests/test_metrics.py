@@ -1,0 +1,56 @@
+"""Prometheus exporter (METRICS_PORT): event-fed counters/histograms and the
+scrape-time manager collector."""
+import urllib.request
+
+import pytest
+
+pytest.importorskip('prometheus_client')
+
+from kiosk_autoscaler_amd import gpumgr  # noqa: E402
+from kiosk_autoscaler_amd.gpumgr import gpus  # noqa: E402
+from kiosk_autoscaler_amd.utils import metrics  # noqa: E402
+from kiosk_autoscaler_amd.utils.events import EventLog  # noqa: E402
+
+
+def test_exporter_counts_events_and_serves_http():
+    from prometheus_client import generate_latest
+    slots = [gpus.GpuSlot(i, '', kind='cpu') for i in range(3)]
+    manager = gpumgr.GpuManager(slots, fence=False)
+    manager.register('deployment', 'ns', 'w',
+                     gpumgr.WorkerTemplate(queues=['q'], backend='cpu'))
+    events = EventLog(source='test')
+    # port 0 = an ephemeral port here (METRICS_PORT=0 itself means "off")
+    exporter = metrics.PrometheusExporter(0, addr='127.0.0.1',
+                                          manager=manager)
+    events.observers.append(exporter.observe)
+    events.emit('tick', keys={'q': 4}, in_progress={'q': 1}, current=1,
+                desired=3, tick_s=0.002)
+    events.emit('scale', current=1, desired=3)
+    events.emit('worker_up', ready_s=0.009, from_pool=True)
+    events.emit('worker_exit', code=0, recycled=True)
+    events.emit('worker_exit', code=-9, killed='no progress')
+    events.emit('requeue', items=2)
+    events.emit('fence_done', transport='rccl', wall_s=0.05)
+    text = generate_latest(exporter.registry).decode()
+    for line in ('kiosk_queue_keys{queue="q"} 4.0',
+                 'kiosk_in_progress_keys{queue="q"} 1.0',
+                 'kiosk_desired_workers 3.0',
+                 'kiosk_scale_events_total{direction="up"} 1.0',
+                 'kiosk_worker_ready_seconds_count{from_pool="true"} 1.0',
+                 'kiosk_worker_exits_total{outcome="recycled"} 1.0',
+                 'kiosk_worker_exits_total{outcome="killed"} 1.0',
+                 'kiosk_requeued_items_total 2.0',
+                 'kiosk_fence_epochs_total{transport="rccl"} 1.0',
+                 'kiosk_gpu_slots 3.0',
+                 'kiosk_workers{resource="w",state="ready"} 0.0'):
+        assert line in text, line
+    if exporter.port:
+        body = urllib.request.urlopen(
+            'http://127.0.0.1:%d/metrics' % exporter.port, timeout=5).read()
+        assert b'kiosk_ticks_total 1.0' in body
+
+
+def test_disabled_is_free():
+    events = EventLog(source='test')
+    assert metrics.attach(events, port=0) is None
+    assert events.observers == []
