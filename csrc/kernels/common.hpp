@@ -44,12 +44,16 @@ __device__ __forceinline__ void wait_vmcnt0() {
 }
 
 // tanh-approximated GELU: 0.5 x (1 + tanh u) = x * sigmoid(2u)
-// = x / (1 + exp(-2u)), u = sqrt(2/pi) (x + 0.044715 x^3).  One v_exp_f32
-// and one v_rcp_f32 (~1 ulp) instead of an IEEE division sequence; the
-// limits are exact (exp -> inf gives x * 0, exp -> 0 gives x).
+// = x / (1 + exp(-2u)), u = sqrt(2/pi) (x + 0.044715 x^3).  With log2(e)
+// folded into the polynomial, -2u log2(e) = x (k0 + k1 x^2): 3 VALU, one
+// v_exp_f32 (2^z), one add, one v_rcp_f32 (~1 ulp), one mul -- no IEEE
+// division, no separate scaling multiply.  Limits are exact (2^z -> inf
+// gives x * 0, 2^z -> 0 gives x).
 __device__ __forceinline__ float gelu_tanh(float x) {
-  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * u));
+  constexpr float k0 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+  constexpr float k1 = k0 * 0.044715f;
+  const float z = x * __builtin_fmaf(x * x, k1, k0);
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z));
 }
 
 // Bijective XCD-aware remap of a linear workgroup id: consecutive remapped

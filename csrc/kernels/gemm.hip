@@ -191,7 +191,7 @@ int gemm_pick_variant(int M, int N, int K, bool have_workspace) {
   // (needs a workspace), else the 256x128 ring, else the 128x128 kernel
   const int rows = (M + 255) / 256;
   if (gemm256_shape_ok(M, N, K, 256) && rows * (N / 256) >= 256)
-    return GEMM_256;
+    return gemm256w4_shape_ok(M, N, K) ? GEMM_256W4 : GEMM_256;
   if (have_workspace && gemm256_shape_ok(M, N, K, 256) &&
       gemm256_splits(M, N, K) > 1)
     return GEMM_256_SPLITK;
@@ -226,6 +226,9 @@ hipError_t launch_gemm_variant(const uint16_t* A, const uint16_t* B,
     return launch_gemm256(A, B, C, bias, R, M, N, K, epilogue, stream,
                           variant == GEMM_256 ? 256 : 128);
   }
+  if (variant == GEMM_256W4)
+    return launch_gemm256(A, B, C, bias, R, M, N, K, epilogue, stream, 256,
+                          4);
   return launch_gemm(A, B, C, bias, R, M, N, K, epilogue, stream);
 }
 

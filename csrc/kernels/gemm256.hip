@@ -29,6 +29,7 @@
 //    lane -> 8-B stores, float4 bias).
 //  * XCD-aware bijective workgroup remap + 4-tile-row grouping.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -37,16 +38,15 @@ namespace kiosk {
 namespace {
 
 constexpr int BM = 256, BKH = 32;
-constexpr int kWaves = 8;
 constexpr int kRowBytes = BKH * 2;                 // 64 B per row per half
 constexpr int kSlots = 4;
 constexpr int kGroupM = 4;
 
 // Per-BN geometry.  LDS slot = A[256][32] + B[BN][32]; an operand half is
 // rows/16 DMA pieces of 16 rows x 64 B spread over the 8 waves.
-template <int BN>
+template <int BN, int kWaves = 8>
 struct Geo {
-  static constexpr int kWavesM = BN == 256 ? 2 : 4;
+  static constexpr int kWavesM = kWaves == 4 ? 2 : (BN == 256 ? 2 : 4);
   static constexpr int kWavesN = kWaves / kWavesM;
   static constexpr int TM = BM / kWavesM / 16;     // 16-row tiles per wave
   static constexpr int TN = BN / kWavesN / 16;     // 16-col tiles per wave
@@ -111,6 +111,51 @@ constexpr int per_quarter(int n, int q) {
   return c;
 }
 
+// MFMA with the accumulator pinned to AGPRs.  The 4-wave layout keeps a
+// 128x128 fp32 tile per wave (256 registers): with the builtin, hipcc
+// splits the AV register class badly (operands land in AGPRs, ~200 VGPRs
+// spill); the "a" constraint keeps every accumulator in the AGPR file and
+// every operand in VGPRs.  Hazards (cdna_hip_programming.md §5.7): the
+// operands come from ds_read (hipcc waits lgkmcnt for asm operands), an
+// accumulate chain into the same AGPRs needs no wait states, and the
+// epilogue's first AGPR read is padded by mfma_drain().
+__device__ __forceinline__ void mfma_agpr(f32x4& acc, const bf16x8& a,
+                                          const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+               : "+a"(acc)
+               : "v"(a), "v"(b));
+}
+
+// First K-step of a tile: C = 0 as the inline constant, so the zeroed
+// accumulators never exist in VGPRs (a zero-initialised array held there
+// across the prologue costs 256 VGPRs and spills).
+__device__ __forceinline__ void mfma_agpr_first(f32x4& acc, const bf16x8& a,
+                                                const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
+               : "=a"(acc)
+               : "v"(a), "v"(b));
+}
+
+__device__ __forceinline__ void mfma_drain() {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+}
+
+// Diagnostic builds only (tools/gemm_ablate.hip): bit 0 drops the in-loop
+// DMA, bit 1 the in-loop LDS reads, bit 2 the per-step wait + barrier of
+// the 4-wave kernel.  Results are wrong in such builds; 0 in the product.
+#ifndef KIOSK_GEMM_ABLATE
+#define KIOSK_GEMM_ABLATE 0
+#endif
+// 4-wave kernel schedule (A/B in profiles/r1_gemm/gemm_w4_variants.jsonl):
+// SCHED 1 = one DMA piece per 8 MFMAs and one LDS read per 4 (vs blocks
+// per quarter: +2.9 % at 8192^3), BUF 1 = buffer_load ... lds (+0.6 %).
+#ifndef KIOSK_W4_SCHED
+#define KIOSK_W4_SCHED 1
+#endif
+#ifndef KIOSK_W4_BUF
+#define KIOSK_W4_BUF 1
+#endif
+
 // Counted waits go through the builtin (not inline asm) so hipcc's waitcnt
 // pass sees them and adds no conservative lgkmcnt(0) of its own.  gfx9
 // encoding: vmcnt[3:0] | expcnt[6:4] (7 = no wait) | lgkmcnt[11:8] |
@@ -121,7 +166,7 @@ constexpr int waitcnt_vm(int vm) {
 
 // (A 4-wave 128x128-per-wave layout with the accumulators in AGPRs was
 // tried: hipcc spills ~270 registers inside the loop.)
-template <int EPI, int BN>
+template <int EPI, int BN, int kWaves>
 __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
     uint16_t* __restrict__ C, const float* __restrict__ bias,
@@ -143,7 +188,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   const int m0 = (first_m + in_group % gsize) * BM;
   const int n0 = (in_group / gsize) * BN;
 
-  using G = Geo<BN>;
+  using G = Geo<BN, kWaves>;
   constexpr int TM = G::TM, TN = G::TN, kSlotBytes = G::kSlotBytes;
   constexpr int kLoadsPerHalf = G::kLoadsPerHalf;
   constexpr int kWaitHalf1 = waitcnt_vm(3 * kLoadsPerHalf);
@@ -154,12 +199,24 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   const int wm = wave / G::kWavesN, wn = wave % G::kWavesN;
 
   f32x4 acc[TM][TN];
+  if constexpr (kWaves != 4) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   const int halves = K / BKH;
+  // epilogue bias, loaded before the k-loop: its latency is hidden and the
+  // tail starts on the arithmetic (lane l owns columns 4(l >> 4)..+3 of
+  // each of its 16-wide column tiles)
+  float4 bias_pre[TN];
+  if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESIDUAL) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      bias_pre[j] = *reinterpret_cast<const float4*>(
+          bias + n0 + wn * (TN * 16) + j * 16 + (lane >> 4) * 4);
+  }
   // Stage half h into its ring slot.  Past the end the source is clamped to
   // the last half (an L2 hit into a slot nobody reads again), so the
   // pipeline has the same shape -- and the same counted wait -- every step.
@@ -233,6 +290,98 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
             slot + slot_off(arow + (r - TN) * 16, chunk));
     }
   };
+  // 4-wave step: same wait/barrier/restage protocol; program order is the
+  // schedule (asm MFMAs are side-effecting, so hipcc keeps each DMA issue
+  // and LDS read where it is written among the MFMAs).  `first` (a
+  // std::integral_constant) selects the C = 0 form.
+  //
+  // DMA piece p of a step: p < 4 -> A piece wave * 4 + p, else B piece
+  // wave * 4 + p - 4.  KIOSK_W4_BUF: LDS-DMA through a buffer descriptor
+  // (32-bit per-lane offset, k0 in the scalar offset) instead of 64-bit
+  // per-lane global addresses.
+  int voff[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int piece = wave * 4 + (p & 3);
+    const int r = piece * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ swz(r);
+    const int base = p < 4 ? m0 : n0, rows = p < 4 ? M : N;
+    int grow = base + r;
+    grow = grow < rows ? grow : rows - 1;
+    voff[p] = (grow * lda + c * 8) * 2;
+  }
+  const auto rsrc_a = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(A), 0, 0x7fffffff, 0x00020000);
+  const auto rsrc_b = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(B), 0, 0x7fffffff, 0x00020000);
+  auto dma4 = [&](int h, int p) {
+    char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
+    const int k0 = min(h, halves - 1) * BKH;
+    char* lds = slot + (p < 4 ? 0 : G::kABytes) + (wave * 4 + (p & 3)) * 1024;
+    if constexpr (KIOSK_W4_BUF) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          p < 4 ? rsrc_a : rsrc_b, (lds_void_t*)lds, 16, voff[p], k0 * 2, 0,
+          0);
+    } else {
+      const uint16_t* g = p < 4 ? A : B;
+      glds16(reinterpret_cast<const char*>(g) + voff[p] + k0 * 2, lds);
+    }
+  };
+  auto read4 = [&](int h, int r, bf16x8 (&wb)[TN], bf16x8 (&xa)[TM]) {
+    const char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
+    if (r < TN)
+      wb[r] = *reinterpret_cast<const bf16x8*>(
+          slot + G::kABytes + slot_off(brow + r * 16, chunk));
+    else
+      xa[r - TN] = *reinterpret_cast<const bf16x8*>(
+          slot + slot_off(arow + (r - TN) * 16, chunk));
+  };
+  auto step4 = [&](auto first, int h, const bf16x8 (&wb)[TN],
+                   const bf16x8 (&xa)[TM], bf16x8 (&wb_next)[TN],
+                   bf16x8 (&xa_next)[TM]) {
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!(KIOSK_GEMM_ABLATE & 4)) {
+      __builtin_amdgcn_s_waitcnt(kWaitHalf2);
+      __builtin_amdgcn_s_barrier();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    auto mfma_t = [&](int i, int j) {
+      if constexpr (decltype(first)::value)
+        mfma_agpr_first(acc[i][j], wb[j], xa[i]);
+      else
+        mfma_agpr(acc[i][j], wb[j], xa[i]);
+    };
+    if constexpr (KIOSK_W4_SCHED == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (!(KIOSK_GEMM_ABLATE & 1)) {
+          dma4(h + 4, 2 * q);
+          dma4(h + 4, 2 * q + 1);
+        }
+        if constexpr (!(KIOSK_GEMM_ABLATE & 2)) {
+#pragma unroll
+          for (int r = 4 * q; r < 4 * q + 4; ++r)
+            read4(h + 1, r, wb_next, xa_next);
+        }
+#pragma unroll
+        for (int i = q * TM / 4; i < (q + 1) * TM / 4; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) mfma_t(i, j);
+      }
+    } else {
+      // one DMA piece every 8 MFMAs, one LDS read every 4 (after MFMA
+      // t with t % 8 == 0, resp. t % 4 == 2): each issue sits in an MFMA
+      // gap instead of a block of them stalling the matrix pipe
+#pragma unroll
+      for (int t = 0; t < TM * TN; ++t) {
+        mfma_t(t / TN, t % TN);
+        if constexpr (!(KIOSK_GEMM_ABLATE & 1))
+          if (t % 8 == 0) dma4(h + 4, t / 8);
+        if constexpr (!(KIOSK_GEMM_ABLATE & 2))
+          if (t % 4 == 2) read4(h + 1, t / 4, wb_next, xa_next);
+      }
+    }
+  };
   auto step = [&](int h, const bf16x8 (&wb)[TN], const bf16x8 (&xa)[TM],
                   bf16x8 (&wb_next)[TN], bf16x8 (&xa_next)[TM]) {
     __builtin_amdgcn_sched_barrier(0);
@@ -279,12 +428,21 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   __builtin_amdgcn_sched_barrier(0);
   bf16x8 wb0[TN], xa0[TM], wb1[TN], xa1[TM];
   read_frags(0, wb0, xa0);
+  if constexpr (kWaves == 4) {
+    step4(std::true_type(), 0, wb0, xa0, wb1, xa1);
+    for (int h = 1; h < halves; h += 2) {
+      step4(std::false_type(), h, wb1, xa1, wb0, xa0);
+      if (h + 1 < halves)
+        step4(std::false_type(), h + 1, wb0, xa0, wb1, xa1);
+    }
+  } else
   for (int h = 0; h < halves; h += 2) {
     step(h, wb0, xa0, wb1, xa1);
     if (h + 1 < halves) step(h + 1, wb1, xa1, wb0, xa0);
   }
   // drain the tail DMAs before the workgroup's LDS can be released
   __builtin_amdgcn_s_waitcnt(kWaitAll);
+  if constexpr (kWaves == 4) mfma_drain();
 
   // Epilogue.  Lane l holds row (l & 15), columns 4g..4g+3 (g = l >> 4) of
   // every 16x16 tile.  Lanes l and l ^ 16 (same row, column groups g and
@@ -292,10 +450,10 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   // op), so every lane then owns 8 consecutive columns and issues one 16-B
   // store where it issued two 8-B ones: the epilogue is store-issue-bound
   // (guide T21).
-  auto finish = [&](int m, int nb, const f32x4& a, float (&v)[4]) {
+  auto finish = [&](int m, int nb, int j, const f32x4& a, float (&v)[4]) {
     v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
     if (EPI != EPI_NONE) {
-      const float4 b = *reinterpret_cast<const float4*>(bias + nb);
+      const float4 b = bias_pre[j];
       v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
     }
     if (EPI == EPI_BIAS_GELU) {
@@ -337,8 +495,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     for (int jp = 0; jp < TN; jp += 2) {
       const int base = n0 + wn * (TN * 16) + jp * 16;
       float v0[4], v1[4];
-      finish(m, base + g * 4, acc[i][jp], v0);
-      finish(m, base + 16 + g * 4, acc[i][jp + 1], v1);
+      finish(m, base + g * 4, jp, acc[i][jp], v0);
+      finish(m, base + 16 + g * 4, jp + 1, acc[i][jp + 1], v1);
       // v_permlane16_swap(X, Y) swaps the odd 16-lane rows of X with the
       // even rows of Y.  With X = this lane's tile-jp half and Y = its
       // tile-(jp+1) half, even rows end with {own jp, partner's jp} and odd
@@ -354,45 +512,45 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   }
 }
 
-template <int EPI, int BN>
+template <int EPI, int BN, int W>
 hipError_t configure256() {
   return hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&gemm256_kernel<EPI, BN>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, Geo<BN>::kLdsBytes);
+      reinterpret_cast<const void*>(&gemm256_kernel<EPI, BN, W>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, Geo<BN, W>::kLdsBytes);
 }
 
-template <int BN>
+template <int BN, int W>
 hipError_t configure256_all() {
-  hipError_t err = configure256<EPI_NONE, BN>();
-  if (err == hipSuccess) err = configure256<EPI_BIAS_GELU, BN>();
-  if (err == hipSuccess) err = configure256<EPI_BIAS_RESIDUAL, BN>();
-  if (err == hipSuccess) err = configure256<EPI_PARTIAL, BN>();
+  hipError_t err = configure256<EPI_NONE, BN, W>();
+  if (err == hipSuccess) err = configure256<EPI_BIAS_GELU, BN, W>();
+  if (err == hipSuccess) err = configure256<EPI_BIAS_RESIDUAL, BN, W>();
+  if (err == hipSuccess) err = configure256<EPI_PARTIAL, BN, W>();
   return err;
 }
 
-template <int BN>
+template <int BN, int W>
 hipError_t launch256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                      const float* bias, const uint16_t* R, int M, int N,
                      int K, int lda, int splits, int epilogue,
                      hipStream_t stream) {
   const int blocks = ((M + BM - 1) / BM) * (N / BN);
-  const dim3 grid(blocks, splits), block(64 * kWaves);
-  const int lds = Geo<BN>::kLdsBytes;
+  const dim3 grid(blocks, splits), block(64 * W);
+  const int lds = Geo<BN, W>::kLdsBytes;
   switch (epilogue) {
     case EPI_NONE:
-      hipLaunchKernelGGL((gemm256_kernel<EPI_NONE, BN>), grid, block, lds,
+      hipLaunchKernelGGL((gemm256_kernel<EPI_NONE, BN, W>), grid, block, lds,
                          stream, A, B, C, bias, R, M, N, K, lda);
       break;
     case EPI_BIAS_GELU:
-      hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_GELU, BN>), grid, block,
+      hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_GELU, BN, W>), grid, block,
                          lds, stream, A, B, C, bias, R, M, N, K, lda);
       break;
     case EPI_BIAS_RESIDUAL:
-      hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_RESIDUAL, BN>), grid,
+      hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_RESIDUAL, BN, W>), grid,
                          block, lds, stream, A, B, C, bias, R, M, N, K, lda);
       break;
     case EPI_PARTIAL:
-      hipLaunchKernelGGL((gemm256_kernel<EPI_PARTIAL, BN>), grid, block,
+      hipLaunchKernelGGL((gemm256_kernel<EPI_PARTIAL, BN, W>), grid, block,
                          lds, stream, A, B, C, bias, R, M, N, K, lda);
       break;
     default:
@@ -486,8 +644,9 @@ hipError_t launch_reduce(const float* P, int splits, int M, int N,
 }  // namespace
 
 hipError_t gemm256_prepare() {
-  hipError_t err = configure256_all<256>();
-  if (err == hipSuccess) err = configure256_all<128>();
+  hipError_t err = configure256_all<256, 8>();
+  if (err == hipSuccess) err = configure256_all<128, 8>();
+  if (err == hipSuccess) err = configure256_all<256, 4>();
   return err;
 }
 
@@ -496,14 +655,29 @@ bool gemm256_shape_ok(int M, int N, int K, int bn) {
          K % BKH == 0 && K >= BKH;
 }
 
+// The 4-wave kernel addresses A and B through buffer descriptors with
+// 32-bit byte offsets.
+bool gemm256w4_shape_ok(int M, int N, int K) {
+  return gemm256_shape_ok(M, N, K, 256) &&
+         static_cast<size_t>(M > N ? M : N) * K * 2 < 0x7fff0000ull;
+}
+
 hipError_t launch_gemm256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                           const float* bias, const uint16_t* R, int M, int N,
-                          int K, int epilogue, hipStream_t stream, int bn) {
-  if (!gemm256_shape_ok(M, N, K, bn) || epilogue == EPI_PARTIAL)
+                          int K, int epilogue, hipStream_t stream, int bn,
+                          int waves) {
+  if (!gemm256_shape_ok(M, N, K, bn) || epilogue == EPI_PARTIAL ||
+      (waves != 8 && !(waves == 4 && bn == 256)) ||
+      (waves == 4 && !gemm256w4_shape_ok(M, N, K)))
     return hipErrorInvalidValue;
+  if (waves == 4)
+    return launch256<256, 4>(A, B, C, bias, R, M, N, K, K, 1, epilogue,
+                             stream);
   if (bn == 128)
-    return launch256<128>(A, B, C, bias, R, M, N, K, K, 1, epilogue, stream);
-  return launch256<256>(A, B, C, bias, R, M, N, K, K, 1, epilogue, stream);
+    return launch256<128, 8>(A, B, C, bias, R, M, N, K, K, 1, epilogue,
+                             stream);
+  return launch256<256, 8>(A, B, C, bias, R, M, N, K, K, 1, epilogue,
+                           stream);
 }
 
 int gemm256_splits(int M, int N, int K) {
@@ -532,7 +706,7 @@ hipError_t launch_gemm256_splitk(const uint16_t* A, const uint16_t* B,
       workspace == nullptr ||
       workspace_bytes < static_cast<size_t>(splits) * M * N * sizeof(float))
     return hipErrorInvalidValue;
-  hipError_t err = launch256<256>(A, B, reinterpret_cast<uint16_t*>(workspace),
+  hipError_t err = launch256<256, 8>(A, B, reinterpret_cast<uint16_t*>(workspace),
                                   nullptr, nullptr, M, N, K / splits, K,
                                   splits, EPI_PARTIAL, stream);
   if (err != hipSuccess) return err;

@@ -31,14 +31,15 @@ hipError_t launch_gemm(const uint16_t* A, const uint16_t* B, uint16_t* C,
 bool gemm_shape_ok(int M, int N, int K);
 hipError_t gemm_prepare();  // call once before launching / capturing
 
-// Kernel variants: 0 = auto (256x256 ring kernel when it yields >= 256
-// tiles, else split-K 256x256 when a workspace is given, else the 256x128
+// Kernel variants: 0 = auto (256x256 ring kernel -- the 4-wave one where
+// its 32-bit offsets reach -- when it yields >= 256 tiles, else split-K 256x256 when a workspace is given, else the 256x128
 // ring when that fills the chip, else 128x128), 1 = 128x128 two-barrier,
 // 2 = 256x256 LDS ring, 3 = 256x128 LDS ring, 4 = split-K 256x256 (fp32
-// partials in `workspace` + one fused reduce/epilogue kernel).
+// partials in `workspace` + one fused reduce/epilogue kernel), 5 = 256x256
+// ring with 4 waves of 128x128 outputs (accumulators in AGPRs).
 enum GemmVariant {
   GEMM_AUTO = 0, GEMM_128 = 1, GEMM_256 = 2, GEMM_256x128 = 3,
-  GEMM_256_SPLITK = 4
+  GEMM_256_SPLITK = 4, GEMM_256W4 = 5
 };
 hipError_t launch_gemm_variant(const uint16_t* A, const uint16_t* B,
                                uint16_t* C, const float* bias,
@@ -51,11 +52,12 @@ int gemm_pick_variant(int M, int N, int K, bool have_workspace = false);
 size_t gemm_workspace_bytes(int M, int N, int K);
 // 256 x bn ring kernel (gemm256.hip), bn = 256 or 128
 bool gemm256_shape_ok(int M, int N, int K, int bn = 256);
+bool gemm256w4_shape_ok(int M, int N, int K);
 hipError_t gemm256_prepare();
 hipError_t launch_gemm256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                           const float* bias, const uint16_t* R, int M, int N,
                           int K, int epilogue, hipStream_t stream,
-                          int bn = 256);
+                          int bn = 256, int waves = 8);
 int gemm256_splits(int M, int N, int K);
 size_t gemm256_splitk_workspace(int M, int N, int K);
 hipError_t launch_gemm256_splitk(const uint16_t* A, const uint16_t* B,

@@ -73,6 +73,9 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
                                bn),
                 "preinit gemm256");
     }
+    check_hip(launch_gemm256(a, b, c, bias, r, 64, 256, 64, epi, stream, 256,
+                             4),
+              "preinit gemm256 4-wave");
     // split-K partial kernel + this epilogue's reduce kernel
     check_hip(launch_gemm256_splitk(a, b, c, bias, r, 64, 256, 64, epi, 2, ws,
                                     ws_bytes, stream),

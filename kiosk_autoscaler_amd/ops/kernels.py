@@ -24,7 +24,8 @@ def _check_bf16(t, name):
         raise ValueError('%s must be a contiguous bf16 CUDA tensor' % name)
 
 
-VARIANTS = {'auto': 0, '128': 1, '256': 2, '256x128': 3, '256splitk': 4}
+VARIANTS = {'auto': 0, '128': 1, '256': 2, '256x128': 3, '256splitk': 4,
+            '256w4': 5}
 
 
 def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
@@ -37,7 +38,8 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
     ring when that does, else 128x128; split-K 256x256 where the grid alone
     would leave CUs idle), ``'128'``, ``'256'``, ``'256x128'`` or
     ``'256splitk'`` (fp32 partials in a temporary workspace + one fused
-    reduce/epilogue kernel)."""
+    reduce/epilogue kernel) or ``'256w4'`` (256x256 ring, 4 waves of
+    128x128 outputs)."""
     import torch
     mod = native.load()
     _check_bf16(a, 'a')
@@ -51,8 +53,8 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
             raise ValueError('split-K does not apply to M=%d N=%d K=%d '
                              '(the 256x256 grid already fills the chip, or '
                              'K is too short)' % (M, N, K))
-    elif variant in ('256', '256x128'):
-        bn = 256 if variant == '256' else 128
+    elif variant in ('256', '256x128', '256w4'):
+        bn = 128 if variant == '256x128' else 256
         if M < 1 or N % bn or K % 32 or K < 32:
             raise ValueError('the 256x%d kernel needs N %% %d == 0 and '
                              'K %% 32 == 0 (M=%d N=%d K=%d)'

@@ -175,11 +175,11 @@ def test_fence_warmup_and_preinit(mod):
                                    (2048, 1024, 4096), (1, 256, 64),
                                    (520, 384, 160)])
 @pytest.mark.parametrize('epilogue', ['none', 'gelu', 'residual'])
-@pytest.mark.parametrize('variant', ['256', '256x128'])
+@pytest.mark.parametrize('variant', ['256', '256x128', '256w4'])
 def test_gemm256_ring_kernel(mod, M, N, K, epilogue, variant):
     """The 256x256 / 256x128 LDS-ring kernels against the fp32 reference
     (odd half counts exercise the clamped tail staging)."""
-    if variant == '256' and N % 256:
+    if variant in ('256', '256w4') and N % 256:
         pytest.skip('N not a multiple of 256')
     from kiosk_autoscaler_amd.ops import kernels
     a = rand_bf16(M, K, seed=11)
@@ -202,13 +202,22 @@ def test_gemm256_identity(mod):
     from kiosk_autoscaler_amd.ops import kernels
     M = K = 512
     N = 768
+    for n in (768, 1024):
+        a = torch.eye(M, K, device='cuda', dtype=torch.bfloat16)
+        b = (torch.arange(n * K, device='cuda', dtype=torch.float32)
+             .reshape(n, K) % 241 - 120).to(torch.bfloat16)
+        if n % 256 == 0:
+            c = kernels.gemm(a, b, variant='256w4')
+            assert torch.equal(c, b.t().contiguous()[:M]), n
     a = torch.eye(M, K, device='cuda', dtype=torch.bfloat16)
     b = (torch.arange(N * K, device='cuda', dtype=torch.float32)
          .reshape(N, K) % 241 - 120).to(torch.bfloat16)
-    for variant in ('256', '256x128'):
+    for variant in ('256', '256x128', '256w4'):
+        if variant == '256w4' and N % 256:
+            continue
         c = kernels.gemm(a, b, variant=variant)
         assert torch.equal(c, b.t().contiguous()[:M]), variant
-    assert mod.gemm_pick_variant(2048, 16384, 4096) == 2
+    assert mod.gemm_pick_variant(2048, 16384, 4096) == 5
     assert mod.gemm_pick_variant(2048, 4096, 16384) == 3
     assert mod.gemm_pick_variant(256, 1024, 1024) == 1
 
@@ -258,7 +267,7 @@ def test_gemm_splitk(mod, M, N, K, epilogue):
 def test_splitk_dispatch(mod):
     assert mod.gemm_pick_variant(2048, 4096, 16384, True) == 4
     assert mod.gemm_pick_variant(2048, 4096, 16384, False) == 3
-    assert mod.gemm_pick_variant(2048, 16384, 4096, True) == 2
+    assert mod.gemm_pick_variant(2048, 16384, 4096, True) == 5
     assert mod.gemm_workspace_bytes(2048, 16384, 4096) == 0
     assert mod.gemm_workspace_bytes(2048, 4096, 16384) == \
         2 * 2048 * 4096 * 4

@@ -39,6 +39,17 @@ def main():
         def ours_256():
             kernels.gemm(a, b, out=out, variant='256')
 
+        def ours_256w4():
+            kernels.gemm(a, b, out=out, variant='256w4')
+
+        def ours_256_gelu():
+            kernels.gemm(a, b, bias=bias, epilogue='gelu', out=out,
+                         variant='256')
+
+        def ours_256w4_gelu():
+            kernels.gemm(a, b, bias=bias, epilogue='gelu', out=out,
+                         variant='256w4')
+
         def ours_256x128():
             kernels.gemm(a, b, out=out, variant='256x128')
 
@@ -56,6 +67,9 @@ def main():
                'torch_gelu': theirs, 'torch': theirs_plain}
         if N % 256 == 0:
             fns['native256'] = ours_256
+            fns['native256w4'] = ours_256w4
+            fns['native256_gelu'] = ours_256_gelu
+            fns['native256w4_gelu'] = ours_256w4_gelu
         fns['native256x128'] = ours_256x128
         if mod.gemm_workspace_bytes(M, N, K):
             fns['native256splitk'] = ours_splitk
@@ -78,8 +92,8 @@ def main():
         ref = (a.float() @ b.float().t())
         summary = {'shape': [M, N, K]}
         for name, fn in (('128', ours_plain), ('256', ours_256),
-                         ('256x128', ours_256x128)):
-            if name == '256' and N % 256:
+                         ('256w4', ours_256w4), ('256x128', ours_256x128)):
+            if name in ('256', '256w4') and N % 256:
                 continue
             out.zero_()
             fn()
