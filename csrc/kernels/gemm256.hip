@@ -52,7 +52,9 @@ struct Geo {
   static constexpr int TN = BN / kWavesN / 16;     // 16-col tiles per wave
   static constexpr int kABytes = BM * kRowBytes;   // 16 KiB
   static constexpr int kSlotBytes = (BM + BN) * kRowBytes;
-  static constexpr int kLdsBytes = kSlots * kSlotBytes;
+  // the 4-wave kernel's ring: 5 units of one operand x 64-deep K-step
+  static constexpr int kLdsBytes =
+      kWaves == 4 ? 5 * BM * 128 : kSlots * kSlotBytes;
   static constexpr int kPiecesA = BM / 16 / kWaves;
   static constexpr int kPiecesB = BN / 16 / kWaves;
   static constexpr int kLoadsPerHalf = kPiecesA + kPiecesB;  // glds/wave
@@ -140,22 +142,11 @@ __device__ __forceinline__ void mfma_drain() {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 }
 
-// Diagnostic builds only (tools/gemm_ablate.hip): bit 0 drops the in-loop
-// DMA, bit 1 the in-loop LDS reads, bit 2 the per-step wait + barrier of
-// the 4-wave kernel.  Results are wrong in such builds; 0 in the product.
+// Diagnostic builds only (tools/gemm_ablate.hip): bit 0 drops the 4-wave
+// kernel's in-loop DMA, bit 1 its in-loop LDS reads.  Results are wrong in such builds; 0 in the product.
 #ifndef KIOSK_GEMM_ABLATE
 #define KIOSK_GEMM_ABLATE 0
 #endif
-// 4-wave kernel schedule (A/B in profiles/r1_gemm/gemm_w4_variants.jsonl):
-// SCHED 1 = one DMA piece per 8 MFMAs and one LDS read per 4 (vs blocks
-// per quarter: +2.9 % at 8192^3), BUF 1 = buffer_load ... lds (+0.6 %).
-#ifndef KIOSK_W4_SCHED
-#define KIOSK_W4_SCHED 1
-#endif
-#ifndef KIOSK_W4_BUF
-#define KIOSK_W4_BUF 1
-#endif
-
 // Counted waits go through the builtin (not inline asm) so hipcc's waitcnt
 // pass sees them and adds no conservative lgkmcnt(0) of its own.  gfx9
 // encoding: vmcnt[3:0] | expcnt[6:4] (7 = no wait) | lgkmcnt[11:8] |
@@ -164,8 +155,6 @@ constexpr int waitcnt_vm(int vm) {
   return (vm & 0xF) | (((vm >> 4) & 3) << 14) | 0x0070;
 }
 
-// (A 4-wave 128x128-per-wave layout with the accumulators in AGPRs was
-// tried: hipcc spills ~270 registers inside the loop.)
 template <int EPI, int BN, int kWaves>
 __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
@@ -290,96 +279,109 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
             slot + slot_off(arow + (r - TN) * 16, chunk));
     }
   };
-  // 4-wave step: same wait/barrier/restage protocol; program order is the
-  // schedule (asm MFMAs are side-effecting, so hipcc keeps each DMA issue
-  // and LDS read where it is written among the MFMAs).  `first` (a
-  // std::integral_constant) selects the C = 0 form.
-  //
-  // DMA piece p of a step: p < 4 -> A piece wave * 4 + p, else B piece
-  // wave * 4 + p - 4.  KIOSK_W4_BUF: LDS-DMA through a buffer descriptor
-  // (32-bit per-lane offset, k0 in the scalar offset) instead of 64-bit
-  // per-lane global addresses.
-  int voff[8];
+  // ---- 4-wave main loop (kWaves == 4) --------------------------------
+  // Each DMA piece moves 8 whole 128-B rows (one 64-deep K-step of 8 rows:
+  // full cache lines; 32-deep half rows cost +6..9 % -- half-line requests,
+  // profiles/r1_gemm/gemm_w4_variants.jsonl).  LDS is a ring of 5 units of
+  // 32 KiB, one operand (A or B) of one 64-deep step each: group g = 2T + op
+  // (op 0 = A, 1 = B, step T) lives in unit g % 5.  The k-loop runs in
+  // 32-deep half-steps h (fragments of half h in registers, half h + 1 read
+  // from LDS during it); half-step h issues group h + 4 into unit
+  // (h + 4) % 5 = (h - 1) % 5, whose data was last read in half-step h - 2
+  // (h even) or h - 1 (h odd), both before the barrier opening half-step h.
+  // At the start of half-step h, groups 0 .. h + 3 are issued; the reads of
+  // half h + 1 need step (h + 1) / 2 resident: groups up to h + 1 (h even,
+  // 2 groups = 16 pieces may stay in flight) or h + 2 (h odd, 8 in flight).
+  // Every group thus has >= 1 half-step (~1000 MFMA cycles) to land; the
+  // half-steps-in-flight probe shows that is enough.  LDS rows are 128 B
+  // with 16-B chunk c of row r at c ^ ((r >> 1) & 7): every ds_read_b128
+  // lane group then covers 16 distinct bank slots.
+  auto mainloop_w4 = [&](int steps) {
+    constexpr int kUnit = BM * 128;
+    int voff_a[8], voff_b[8];
 #pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const int piece = wave * 4 + (p & 3);
-    const int r = piece * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ swz(r);
-    const int base = p < 4 ? m0 : n0, rows = p < 4 ? M : N;
-    int grow = base + r;
-    grow = grow < rows ? grow : rows - 1;
-    voff[p] = (grow * lda + c * 8) * 2;
-  }
-  const auto rsrc_a = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(A), 0, 0x7fffffff, 0x00020000);
-  const auto rsrc_b = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(B), 0, 0x7fffffff, 0x00020000);
-  auto dma4 = [&](int h, int p) {
-    char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
-    const int k0 = min(h, halves - 1) * BKH;
-    char* lds = slot + (p < 4 ? 0 : G::kABytes) + (wave * 4 + (p & 3)) * 1024;
-    if constexpr (KIOSK_W4_BUF) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          p < 4 ? rsrc_a : rsrc_b, (lds_void_t*)lds, 16, voff[p], k0 * 2, 0,
-          0);
-    } else {
-      const uint16_t* g = p < 4 ? A : B;
-      glds16(reinterpret_cast<const char*>(g) + voff[p] + k0 * 2, lds);
+    for (int p = 0; p < 8; ++p) {
+      const int r = (wave * 8 + p) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int ra = m0 + r < M ? m0 + r : M - 1;
+      const int rb = n0 + r < N ? n0 + r : N - 1;
+      voff_a[p] = (ra * lda + c * 8) * 2;
+      voff_b[p] = (rb * lda + c * 8) * 2;
     }
-  };
-  auto read4 = [&](int h, int r, bf16x8 (&wb)[TN], bf16x8 (&xa)[TM]) {
-    const char* slot = smem + (h & (kSlots - 1)) * kSlotBytes;
-    if (r < TN)
-      wb[r] = *reinterpret_cast<const bf16x8*>(
-          slot + G::kABytes + slot_off(brow + r * 16, chunk));
-    else
-      xa[r - TN] = *reinterpret_cast<const bf16x8*>(
-          slot + slot_off(arow + (r - TN) * 16, chunk));
-  };
-  auto step4 = [&](auto first, int h, const bf16x8 (&wb)[TN],
-                   const bf16x8 (&xa)[TM], bf16x8 (&wb_next)[TN],
-                   bf16x8 (&xa_next)[TM]) {
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!(KIOSK_GEMM_ABLATE & 4)) {
-      __builtin_amdgcn_s_waitcnt(kWaitHalf2);
-      __builtin_amdgcn_s_barrier();
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    auto mfma_t = [&](int i, int j) {
-      if constexpr (decltype(first)::value)
-        mfma_agpr_first(acc[i][j], wb[j], xa[i]);
+    const auto rsrc_a = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(A), 0, 0x7fffffff, 0x00020000);
+    const auto rsrc_b = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(B), 0, 0x7fffffff, 0x00020000);
+    // piece p of group g (past the last step the source is clamped to it:
+    // same pipeline shape, same counted waits, every step)
+    auto dma = [&](int g, int p) {
+      const int t = min(g >> 1, steps - 1);
+      char* lds = smem + (g % 5) * kUnit + (wave * 8 + p) * 1024;
+      if (g & 1)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_b, (lds_void_t*)lds, 16,
+                                                 voff_b[p], t * 128, 0, 0);
       else
-        mfma_agpr(acc[i][j], wb[j], xa[i]);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)lds, 16,
+                                                 voff_a[p], t * 128, 0, 0);
     };
-    if constexpr (KIOSK_W4_SCHED == 0) {
+    // fragment r of half h: r < TN -> B tile r, else A tile r - TN
+    const int fr = lane & 15;
+    const int lane_a = (wm * 128 + fr) * 128, lane_b = (wn * 128 + fr) * 128;
+    const int sw = (fr >> 1) & 7;
+    auto read = [&](auto hh, int t, int r, bf16x8 (&wb)[TN],
+                    bf16x8 (&xa)[TM]) {
+      const int chunk = (decltype(hh)::value * 4 + (lane >> 4)) ^ sw;
+      if (r < TN)
+        wb[r] = *reinterpret_cast<const bf16x8*>(
+            smem + ((2 * t + 1) % 5) * kUnit + lane_b + r * 2048 + chunk * 16);
+      else
+        xa[r - TN] = *reinterpret_cast<const bf16x8*>(
+            smem + ((2 * t) % 5) * kUnit + lane_a + (r - TN) * 2048 +
+            chunk * 16);
+    };
+    // half-step h = 2t + odd
+    auto half = [&](auto first, auto odd, int t, const bf16x8 (&wb)[TN],
+                    const bf16x8 (&xa)[TM], bf16x8 (&wb_next)[TN],
+                    bf16x8 (&xa_next)[TM]) {
+      constexpr bool kOdd = decltype(odd)::value;
+      const int h = 2 * t + kOdd;
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(kOdd ? 8 : 16));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // half h + 1: step t (h even, second half) or t + 1 (h odd, first)
+      const int tn = kOdd ? t + 1 : t;
+      using HH = std::integral_constant<int, kOdd ? 0 : 1>;
+      // one DMA piece every 8 MFMAs, one LDS read every 4: each issue sits
+      // in an MFMA gap, none stalls the matrix pipe behind a block of them
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if constexpr (!(KIOSK_GEMM_ABLATE & 1)) {
-          dma4(h + 4, 2 * q);
-          dma4(h + 4, 2 * q + 1);
-        }
-        if constexpr (!(KIOSK_GEMM_ABLATE & 2)) {
-#pragma unroll
-          for (int r = 4 * q; r < 4 * q + 4; ++r)
-            read4(h + 1, r, wb_next, xa_next);
-        }
-#pragma unroll
-        for (int i = q * TM / 4; i < (q + 1) * TM / 4; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) mfma_t(i, j);
-      }
-    } else {
-      // one DMA piece every 8 MFMAs, one LDS read every 4 (after MFMA
-      // t with t % 8 == 0, resp. t % 4 == 2): each issue sits in an MFMA
-      // gap instead of a block of them stalling the matrix pipe
-#pragma unroll
-      for (int t = 0; t < TM * TN; ++t) {
-        mfma_t(t / TN, t % TN);
+      for (int u = 0; u < TM * TN; ++u) {
+        if constexpr (decltype(first)::value)
+          mfma_agpr_first(acc[u / TN][u % TN], wb[u % TN], xa[u / TN]);
+        else
+          mfma_agpr(acc[u / TN][u % TN], wb[u % TN], xa[u / TN]);
         if constexpr (!(KIOSK_GEMM_ABLATE & 1))
-          if (t % 8 == 0) dma4(h + 4, t / 8);
+          if (u % 8 == 0) dma(h + 4, u / 8);
         if constexpr (!(KIOSK_GEMM_ABLATE & 2))
-          if (t % 4 == 2) read4(h + 1, t / 4, wb_next, xa_next);
+          if (u % 4 == 2) read(HH(), tn, u / 4, wb_next, xa_next);
       }
+    };
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int p = 0; p < 8; ++p) dma(g, p);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(16));
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 wb0[TN], xa0[TM], wb1[TN], xa1[TM];
+#pragma unroll
+    for (int r = 0; r < TM + TN; ++r)
+      read(std::integral_constant<int, 0>(), 0, r, wb0, xa0);
+    half(std::true_type(), std::false_type(), 0, wb0, xa0, wb1, xa1);
+    half(std::false_type(), std::true_type(), 0, wb1, xa1, wb0, xa0);
+    for (int t = 1; t < steps; ++t) {
+      half(std::false_type(), std::false_type(), t, wb0, xa0, wb1, xa1);
+      half(std::false_type(), std::true_type(), t, wb1, xa1, wb0, xa0);
     }
   };
   auto step = [&](int h, const bf16x8 (&wb)[TN], const bf16x8 (&xa)[TM],
@@ -421,24 +423,20 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     }
   };
 
-#pragma unroll
-  for (int h = 0; h < kSlots; ++h) stage(h);
-  __builtin_amdgcn_s_waitcnt(kWaitHalf1);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  bf16x8 wb0[TN], xa0[TM], wb1[TN], xa1[TM];
-  read_frags(0, wb0, xa0);
   if constexpr (kWaves == 4) {
-    step4(std::true_type(), 0, wb0, xa0, wb1, xa1);
-    for (int h = 1; h < halves; h += 2) {
-      step4(std::false_type(), h, wb1, xa1, wb0, xa0);
-      if (h + 1 < halves)
-        step4(std::false_type(), h + 1, wb0, xa0, wb1, xa1);
+    mainloop_w4(K / 64);
+  } else {
+#pragma unroll
+    for (int h = 0; h < kSlots; ++h) stage(h);
+    __builtin_amdgcn_s_waitcnt(kWaitHalf1);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 wb0[TN], xa0[TM], wb1[TN], xa1[TM];
+    read_frags(0, wb0, xa0);
+    for (int h = 0; h < halves; h += 2) {
+      step(h, wb0, xa0, wb1, xa1);
+      if (h + 1 < halves) step(h + 1, wb1, xa1, wb0, xa0);
     }
-  } else
-  for (int h = 0; h < halves; h += 2) {
-    step(h, wb0, xa0, wb1, xa1);
-    if (h + 1 < halves) step(h + 1, wb1, xa1, wb0, xa0);
   }
   // drain the tail DMAs before the workgroup's LDS can be released
   __builtin_amdgcn_s_waitcnt(kWaitAll);
@@ -655,10 +653,10 @@ bool gemm256_shape_ok(int M, int N, int K, int bn) {
          K % BKH == 0 && K >= BKH;
 }
 
-// The 4-wave kernel addresses A and B through buffer descriptors with
-// 32-bit byte offsets.
+// The 4-wave kernel consumes K in 64-deep steps and addresses A and B
+// through buffer descriptors with 32-bit byte offsets.
 bool gemm256w4_shape_ok(int M, int N, int K) {
-  return gemm256_shape_ok(M, N, K, 256) &&
+  return gemm256_shape_ok(M, N, K, 256) && K % 64 == 0 &&
          static_cast<size_t>(M > N ? M : N) * K * 2 < 0x7fff0000ull;
 }
 

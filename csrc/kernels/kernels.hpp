@@ -22,6 +22,9 @@ constexpr int kGemmBK = 64;
 constexpr int kGemmThreads = 256;
 constexpr int kGemmLdsBytes = 2 * 2 * kGemmBM * kGemmBK * 2;  // 64 KiB
 constexpr int kGemmBlocksPerCU = 2;
+// LDS of the largest GEMM block (the 4-wave 256x256 kernel's 5-unit ring):
+// the warm-start kernel pre-allocates and zeroes this much per CU
+constexpr int kGemmRingLdsBytes = 5 * 256 * 128;  // 160 KiB
 
 // C[M,N] (bf16) = epilogue(A[M,K] . B[N,K]^T); fp32 accumulate.
 // Requires N % 128 == 0, K % 64 == 0; any M >= 1.

@@ -60,6 +60,7 @@ PYBIND11_MODULE(_kiosk_hip, m) {
   m.attr("gemm_tile") = py::make_tuple(kiosk::kGemmBM, kiosk::kGemmBN,
                                        kiosk::kGemmBK);
   m.attr("gemm_lds_bytes") = kiosk::kGemmLdsBytes;
+  m.attr("gemm_ring_lds_bytes") = kiosk::kGemmRingLdsBytes;
   m.attr("sum_blocks") = kiosk::kSumBlocks;
 
   m.def("gemm_shape_ok", &kiosk::gemm_shape_ok);
@@ -175,7 +176,7 @@ PYBIND11_MODULE(_kiosk_hip, m) {
             return warm_to_dict(r);
           },
           py::arg("iters") = 4096,
-          py::arg("lds_bytes") = 2 * kiosk::kGemmLdsBytes)
+          py::arg("lds_bytes") = kiosk::kGemmRingLdsBytes)
       .def("prepare", &kiosk::Engine::prepare, py::arg("rows"),
            py::call_guard<py::gil_scoped_release>())
       .def(

@@ -82,7 +82,7 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
               "preinit gemm256 split-K");
   }
   check_hip(launch_partial_sums(c, elems, sums, stream), "preinit sums");
-  check_hip(launch_warmstart(a, elems, rec, 1, 1, 2 * kGemmLdsBytes, stream),
+  check_hip(launch_warmstart(a, elems, rec, 1, 1, kGemmRingLdsBytes, stream),
             "preinit warmstart");
   check_hip(hipStreamSynchronize(stream), "preinit sync");
   check_hip(hipFree(scratch), "hipFree(preinit)");

@@ -55,10 +55,11 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
                              'K is too short)' % (M, N, K))
     elif variant in ('256', '256x128', '256w4'):
         bn = 128 if variant == '256x128' else 256
-        if M < 1 or N % bn or K % 32 or K < 32:
+        kq = 64 if variant == '256w4' else 32
+        if M < 1 or N % bn or K % kq or K < kq:
             raise ValueError('the 256x%d kernel needs N %% %d == 0 and '
-                             'K %% 32 == 0 (M=%d N=%d K=%d)'
-                             % (bn, bn, M, N, K))
+                             'K %% %d == 0 (M=%d N=%d K=%d)'
+                             % (bn, bn, kq, M, N, K))
     elif not mod.gemm_shape_ok(M, N, K):
         raise ValueError('unsupported GEMM shape M=%d N=%d K=%d (need N %% 128'
                          ' == 0, K %% 64 == 0)' % (M, N, K))
