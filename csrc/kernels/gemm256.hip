@@ -704,9 +704,16 @@ hipError_t launch_gemm256_splitk(const uint16_t* A, const uint16_t* B,
       workspace == nullptr ||
       workspace_bytes < static_cast<size_t>(splits) * M * N * sizeof(float))
     return hipErrorInvalidValue;
-  hipError_t err = launch256<256, 8>(A, B, reinterpret_cast<uint16_t*>(workspace),
-                                  nullptr, nullptr, M, N, K / splits, K,
-                                  splits, EPI_PARTIAL, stream);
+  // the 4-wave kernel where its 64-deep steps and 32-bit offsets fit
+  const bool w4 = (K / splits) % 64 == 0 &&
+                  static_cast<size_t>(M > N ? M : N) * K * 2 < 0x7fff0000ull;
+  hipError_t err =
+      w4 ? launch256<256, 4>(A, B, reinterpret_cast<uint16_t*>(workspace),
+                             nullptr, nullptr, M, N, K / splits, K, splits,
+                             EPI_PARTIAL, stream)
+         : launch256<256, 8>(A, B, reinterpret_cast<uint16_t*>(workspace),
+                             nullptr, nullptr, M, N, K / splits, K, splits,
+                             EPI_PARTIAL, stream);
   if (err != hipSuccess) return err;
   return launch_reduce(workspace, splits, M, N, bias, R, C, epilogue, stream);
 }

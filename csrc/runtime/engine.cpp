@@ -80,6 +80,12 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
     check_hip(launch_gemm256_splitk(a, b, c, bias, r, 64, 256, 64, epi, 2, ws,
                                     ws_bytes, stream),
               "preinit gemm256 split-K");
+    // K = 128 in two 64-deep slices: the 4-wave partial kernel (B spans
+    // the b, c views: it reads scratch it does not write before the reduce)
+    if (epi == 0)
+      check_hip(launch_gemm256_splitk(a, b, c, bias, r, 64, 256, 128, epi, 2,
+                                      ws, ws_bytes, stream),
+                "preinit gemm256 4-wave split-K");
   }
   check_hip(launch_partial_sums(c, elems, sums, stream), "preinit sums");
   check_hip(launch_warmstart(a, elems, rec, 1, 1, kGemmRingLdsBytes, stream),
