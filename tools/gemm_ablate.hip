@@ -62,11 +62,9 @@ int main(int argc, char** argv) {
     ms /= iters;
     if (r > 0 && ms < best) best = ms;
   }
-  printf("{\"ablate\": %d, \"sched\": %d, \"buf\": %d, \"waves\": %d, "
-         "\"shape\": [%d, %d, %d], "
+  printf("{\"ablate\": %d, \"waves\": %d, \"shape\": [%d, %d, %d], "
          "\"ms\": %.4f, \"tflops\": %.1f}\n",
-         KIOSK_GEMM_ABLATE, KIOSK_W4_SCHED, KIOSK_W4_BUF, waves, M, N, K,
-         best,
+         KIOSK_GEMM_ABLATE, waves, M, N, K, best,
          2.0 * M * N * K / (best * 1e-3) / 1e12);
   return 0;
 }
