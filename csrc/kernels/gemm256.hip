@@ -147,6 +147,11 @@ __device__ __forceinline__ void mfma_drain() {
 #ifndef KIOSK_GEMM_ABLATE
 #define KIOSK_GEMM_ABLATE 0
 #endif
+// 1: every DMA and LDS-read issue of a half-step inside its first 48 MFMAs
+// (+0.5..1.4 % over one per 8 / per 4 across all 64)
+#ifndef KIOSK_W4_SPREAD
+#define KIOSK_W4_SPREAD 1
+#endif
 // Counted waits go through the builtin (not inline asm) so hipcc's waitcnt
 // pass sees them and adds no conservative lgkmcnt(0) of its own.  gfx9
 // encoding: vmcnt[3:0] | expcnt[6:4] (7 = no wait) | lgkmcnt[11:8] |
@@ -328,16 +333,27 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     const int fr = lane & 15;
     const int lane_a = (wm * 128 + fr) * 128, lane_b = (wn * 128 + fr) * 128;
     const int sw = (fr >> 1) & 7;
+    // per-lane parts of the two halves' read addresses (row + swizzled
+    // chunk); the unit base is wave-uniform and the tile offset r * 2048 an
+    // immediate, so each read is one ds_read_b128 with offset:N
+    const int lane_a0 = lane_a + (((lane >> 4) ^ sw) << 4);
+    const int lane_a1 = lane_a + (((4 + (lane >> 4)) ^ sw) << 4);
+    const int lane_b0 = lane_b + (((lane >> 4) ^ sw) << 4);
+    const int lane_b1 = lane_b + (((4 + (lane >> 4)) ^ sw) << 4);
     auto read = [&](auto hh, int t, int r, bf16x8 (&wb)[TN],
                     bf16x8 (&xa)[TM]) {
-      const int chunk = (decltype(hh)::value * 4 + (lane >> 4)) ^ sw;
-      if (r < TN)
-        wb[r] = *reinterpret_cast<const bf16x8*>(
-            smem + ((2 * t + 1) % 5) * kUnit + lane_b + r * 2048 + chunk * 16);
-      else
-        xa[r - TN] = *reinterpret_cast<const bf16x8*>(
-            smem + ((2 * t) % 5) * kUnit + lane_a + (r - TN) * 2048 +
-            chunk * 16);
+      constexpr bool kHi = decltype(hh)::value != 0;
+      if (r < TN) {
+        const char* base = smem + __builtin_amdgcn_readfirstlane(
+                                      ((2 * t + 1) % 5) * kUnit) +
+                           (kHi ? lane_b1 : lane_b0);
+        wb[r] = *reinterpret_cast<const bf16x8*>(base + r * 2048);
+      } else {
+        const char* base = smem + __builtin_amdgcn_readfirstlane(
+                                      ((2 * t) % 5) * kUnit) +
+                           (kHi ? lane_a1 : lane_a0);
+        xa[r - TN] = *reinterpret_cast<const bf16x8*>(base + (r - TN) * 2048);
+      }
     };
     // half-step h = 2t + odd
     auto half = [&](auto first, auto odd, int t, const bf16x8 (&wb)[TN],
@@ -360,10 +376,20 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
           mfma_agpr_first(acc[u / TN][u % TN], wb[u % TN], xa[u / TN]);
         else
           mfma_agpr(acc[u / TN][u % TN], wb[u % TN], xa[u / TN]);
-        if constexpr (!(KIOSK_GEMM_ABLATE & 1))
-          if (u % 8 == 0) dma(h + 4, u / 8);
-        if constexpr (!(KIOSK_GEMM_ABLATE & 2))
-          if (u % 4 == 2) read(HH(), tn, u / 4, wb_next, xa_next);
+        if constexpr (KIOSK_W4_SPREAD == 0) {
+          if constexpr (!(KIOSK_GEMM_ABLATE & 1))
+            if (u % 8 == 0) dma(h + 4, u / 8);
+          if constexpr (!(KIOSK_GEMM_ABLATE & 2))
+            if (u % 4 == 2) read(HH(), tn, u / 4, wb_next, xa_next);
+        } else {
+          // all issues in the first 48 MFMAs: the last LDS read has 16
+          // MFMAs (~256 cycles) to return before the next half-step's
+          // lgkmcnt(0) + barrier
+          if constexpr (!(KIOSK_GEMM_ABLATE & 1))
+            if (u % 6 == 0 && u < 48) dma(h + 4, u / 6);
+          if constexpr (!(KIOSK_GEMM_ABLATE & 2))
+            if (u % 3 == 1 && u < 48) read(HH(), tn, u / 3, wb_next, xa_next);
+        }
       }
     };
 #pragma unroll
