@@ -160,11 +160,16 @@ constexpr int waitcnt_vm(int vm) {
   return (vm & 0xF) | (((vm >> 4) & 3) << 14) | 0x0070;
 }
 
-template <int EPI, int BN, int kWaves>
+// kFused (4-wave split-K): every K-slice block writes its fp32 partial
+// tile to P[blockIdx.y]; the block that arrives last at its tile's counter
+// adds the other slices' partials to its registers and runs the epilogue
+// (no separate reduce launch, no partial-plane round trip for one slice).
+template <int EPI, int BN, int kWaves, int kFused = 0>
 __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
     uint16_t* __restrict__ C, const float* __restrict__ bias,
-    const uint16_t* __restrict__ R, int M, int N, int K, int lda) {
+    const uint16_t* __restrict__ R, int M, int N, int K, int lda,
+    float* __restrict__ P, int* __restrict__ cnt) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // split-K: blockIdx.y picks a K/gridDim.y slice (K is the slice length,
   // lda the full row stride); EPI_PARTIAL writes fp32 partials per slice
@@ -466,7 +471,16 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   }
   // drain the tail DMAs before the workgroup's LDS can be released
   __builtin_amdgcn_s_waitcnt(kWaitAll);
-  if constexpr (kWaves == 4) mfma_drain();
+  if constexpr (kWaves == 4) {
+    mfma_drain();
+    // every accumulator is re-defined after the drain, so no read of one
+    // (epilogue or spill) can be scheduled between its last MFMA and the
+    // wait states hipcc does not insert for asm MFMAs
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" : "+a"(acc[i][j]));
+  }
 
   // Epilogue.  Lane l holds row (l & 15), columns 4g..4g+3 (g = l >> 4) of
   // every 16x16 tile.  Lanes l and l ^ 16 (same row, column groups g and
@@ -476,6 +490,12 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   // (guide T21).
   auto finish = [&](int m, int nb, int j, const f32x4& a, float (&v)[4]) {
     v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    if constexpr (kFused) {
+      const float4 q = *reinterpret_cast<const float4*>(
+          P + static_cast<size_t>(split ^ 1) * M * N +
+          static_cast<size_t>(m) * N + nb);
+      v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+    }
     if (EPI != EPI_NONE) {
       const float4 b = bias_pre[j];
       v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
@@ -498,6 +518,49 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   };
   const int g = lane >> 4;
   const bool odd = (g & 1) != 0;
+  if constexpr (kFused) {
+    // In-launch split-K combine (cdna_hip_programming.md §5, projection
+    // GEMM item 2): plain 16-B partial stores -> every wave vmcnt(0) ->
+    // barrier -> one lane: agent-scope release fence, vmcnt(0), relaxed
+    // agent-scope ticket; the block drawing splits - 1 acquires and reads
+    // the other slices.  Correct for any placement of a tile's slices;
+    // the counters are zeroed by a memset ahead of every launch.
+    const size_t plane = static_cast<size_t>(M) * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * (TM * 16) + i * 16 + (lane & 15);
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nb = n0 + wn * (TN * 16) + j * 16 + g * 4;
+        *reinterpret_cast<float4*>(P + split * plane +
+                                   static_cast<size_t>(m) * N + nb) =
+            float4{acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      }
+      // one row of tiles at a time: bounds the AGPR -> VGPR copies
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* last = reinterpret_cast<int*>(smem);   // the one LDS array
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int ticket = __hip_atomic_fetch_add(
+          cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int is_last = ticket == static_cast<int>(gridDim.y) - 1;
+      if (is_last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *last = is_last;
+    }
+    __syncthreads();
+    if (!*last) return;
+    // the reducer adds its own and the other slice's partial tile by tile
+    // in the epilogue below (two K slices only: the host launches the
+    // fused path for splits == 2)
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     // m is the same for lanes l and l ^ 16, so a skipped row skips both
@@ -519,8 +582,22 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     for (int jp = 0; jp < TN; jp += 2) {
       const int base = n0 + wn * (TN * 16) + jp * 16;
       float v0[4], v1[4];
-      finish(m, base + g * 4, jp, acc[i][jp], v0);
-      finish(m, base + 16 + g * 4, jp + 1, acc[i][jp + 1], v1);
+      if constexpr (kFused) {
+        // the reducer re-reads its own partial (L2-warm) instead of
+        // keeping 256 accumulators live across the ticket
+        const size_t own = static_cast<size_t>(split) * M * N +
+                           static_cast<size_t>(m) * N;
+        const float4 p0 = *reinterpret_cast<const float4*>(P + own + base +
+                                                           g * 4);
+        const float4 p1 = *reinterpret_cast<const float4*>(P + own + base +
+                                                           16 + g * 4);
+        finish(m, base + g * 4, jp, f32x4{p0.x, p0.y, p0.z, p0.w}, v0);
+        finish(m, base + 16 + g * 4, jp + 1, f32x4{p1.x, p1.y, p1.z, p1.w},
+               v1);
+      } else {
+        finish(m, base + g * 4, jp, acc[i][jp], v0);
+        finish(m, base + 16 + g * 4, jp + 1, acc[i][jp + 1], v1);
+      }
       // v_permlane16_swap(X, Y) swaps the odd 16-lane rows of X with the
       // even rows of Y.  With X = this lane's tile-jp half and Y = its
       // tile-(jp+1) half, even rows end with {own jp, partner's jp} and odd
@@ -563,24 +640,44 @@ hipError_t launch256(const uint16_t* A, const uint16_t* B, uint16_t* C,
   switch (epilogue) {
     case EPI_NONE:
       hipLaunchKernelGGL((gemm256_kernel<EPI_NONE, BN, W>), grid, block, lds,
-                         stream, A, B, C, bias, R, M, N, K, lda);
+                         stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr);
       break;
     case EPI_BIAS_GELU:
       hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_GELU, BN, W>), grid, block,
-                         lds, stream, A, B, C, bias, R, M, N, K, lda);
+                         lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr);
       break;
     case EPI_BIAS_RESIDUAL:
       hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_RESIDUAL, BN, W>), grid,
-                         block, lds, stream, A, B, C, bias, R, M, N, K, lda);
+                         block, lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr);
       break;
     case EPI_PARTIAL:
       hipLaunchKernelGGL((gemm256_kernel<EPI_PARTIAL, BN, W>), grid, block,
-                         lds, stream, A, B, C, bias, R, M, N, K, lda);
+                         lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr);
       break;
     default:
       return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+template <int EPI>
+hipError_t launch_fused4(const uint16_t* A, const uint16_t* B, uint16_t* C,
+                         const float* bias, const uint16_t* R, int M, int N,
+                         int K, int lda, int splits, float* P, int* cnt,
+                         hipStream_t stream) {
+  const int blocks = ((M + BM - 1) / BM) * (N / 256);
+  constexpr int lds = Geo<256, 4>::kLdsBytes;
+  hipLaunchKernelGGL((gemm256_kernel<EPI, 256, 4, 1>), dim3(blocks, splits),
+                     dim3(256), lds, stream, A, B, C, bias, R, M, N, K, lda, P,
+                     cnt);
+  return hipGetLastError();
+}
+
+template <int EPI>
+hipError_t configure_fused4() {
+  return hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&gemm256_kernel<EPI, 256, 4, 1>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256, 4>::kLdsBytes);
 }
 
 // out = epi(sum_s P[s]) over `splits` fp32 partial planes of M x N; each
@@ -671,6 +768,9 @@ hipError_t gemm256_prepare() {
   hipError_t err = configure256_all<256, 8>();
   if (err == hipSuccess) err = configure256_all<128, 8>();
   if (err == hipSuccess) err = configure256_all<256, 4>();
+  if (err == hipSuccess) err = configure_fused4<EPI_NONE>();
+  if (err == hipSuccess) err = configure_fused4<EPI_BIAS_GELU>();
+  if (err == hipSuccess) err = configure_fused4<EPI_BIAS_RESIDUAL>();
   return err;
 }
 
@@ -716,9 +816,31 @@ int gemm256_splits(int M, int N, int K) {
   return s;
 }
 
+// Off by default: measured 6 % slower than partial planes + the reduce
+// kernel at 2048x4096x16384 (profiles/r1_gemm/gemm_w4_splitk_fused_ab.jsonl;
+// the last slice's serial combine leaves half the CUs idle, the reduce
+// kernel streams on all of them).
+bool g_splitk_fused = false;
+
+void gemm_set_splitk_fused(bool on) { g_splitk_fused = on; }
+
+// the fused 4-wave split-K path: two 64-deep-aligned slices, 32-bit
+// operand offsets
+bool splitk_w4(int M, int N, int K, int splits) {
+  return splits == 2 && (K / splits) % 64 == 0 &&
+         static_cast<size_t>(M > N ? M : N) * K * 2 < 0x7fff0000ull;
+}
+
+// fp32 partial planes, then (4-wave path) one ticket counter per tile
+size_t splitk_counter_offset(int M, int N, int splits) {
+  return static_cast<size_t>(splits) * M * N * sizeof(float);
+}
+
 size_t gemm256_splitk_workspace(int M, int N, int K) {
   const int s = gemm256_splits(M, N, K);
-  return s > 1 ? static_cast<size_t>(s) * M * N * sizeof(float) : 0;
+  if (s <= 1) return 0;
+  const size_t tiles = static_cast<size_t>((M + BM - 1) / BM) * (N / 256);
+  return splitk_counter_offset(M, N, s) + ((tiles * 4 + 255) / 256) * 256;
 }
 
 hipError_t launch_gemm256_splitk(const uint16_t* A, const uint16_t* B,
@@ -730,16 +852,41 @@ hipError_t launch_gemm256_splitk(const uint16_t* A, const uint16_t* B,
       workspace == nullptr ||
       workspace_bytes < static_cast<size_t>(splits) * M * N * sizeof(float))
     return hipErrorInvalidValue;
-  // the 4-wave kernel where its 64-deep steps and 32-bit offsets fit
-  const bool w4 = (K / splits) % 64 == 0 &&
-                  static_cast<size_t>(M > N ? M : N) * K * 2 < 0x7fff0000ull;
-  hipError_t err =
-      w4 ? launch256<256, 4>(A, B, reinterpret_cast<uint16_t*>(workspace),
-                             nullptr, nullptr, M, N, K / splits, K, splits,
-                             EPI_PARTIAL, stream)
-         : launch256<256, 8>(A, B, reinterpret_cast<uint16_t*>(workspace),
-                             nullptr, nullptr, M, N, K / splits, K, splits,
-                             EPI_PARTIAL, stream);
+  if (splitk_w4(M, N, K, splits) && !g_splitk_fused) {
+    // A/B reference: 4-wave partial planes + the separate reduce kernel
+    hipError_t err = launch256<256, 4>(
+        A, B, reinterpret_cast<uint16_t*>(workspace), nullptr, nullptr, M, N,
+        K / splits, K, splits, EPI_PARTIAL, stream);
+    if (err != hipSuccess) return err;
+    return launch_reduce(workspace, splits, M, N, bias, R, C, epilogue,
+                         stream);
+  }
+  if (splitk_w4(M, N, K, splits)) {
+    // 4-wave kernel, combined in-launch by each tile's last K-slice block
+    const size_t tiles = static_cast<size_t>((M + BM - 1) / BM) * (N / 256);
+    const size_t off = splitk_counter_offset(M, N, splits);
+    if (workspace_bytes < off + tiles * 4) return hipErrorInvalidValue;
+    int* cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + off);
+    hipError_t err = hipMemsetAsync(cnt, 0, tiles * 4, stream);
+    if (err != hipSuccess) return err;
+    switch (epilogue) {
+      case EPI_NONE:
+        return launch_fused4<EPI_NONE>(A, B, C, bias, R, M, N, K / splits, K,
+                                       splits, workspace, cnt, stream);
+      case EPI_BIAS_GELU:
+        return launch_fused4<EPI_BIAS_GELU>(A, B, C, bias, R, M, N, K / splits,
+                                            K, splits, workspace, cnt, stream);
+      case EPI_BIAS_RESIDUAL:
+        return launch_fused4<EPI_BIAS_RESIDUAL>(A, B, C, bias, R, M, N,
+                                                K / splits, K, splits,
+                                                workspace, cnt, stream);
+      default:
+        return hipErrorInvalidValue;
+    }
+  }
+  hipError_t err = launch256<256, 8>(A, B, reinterpret_cast<uint16_t*>(workspace),
+                                     nullptr, nullptr, M, N, K / splits, K,
+                                     splits, EPI_PARTIAL, stream);
   if (err != hipSuccess) return err;
   return launch_reduce(workspace, splits, M, N, bias, R, C, epilogue, stream);
 }

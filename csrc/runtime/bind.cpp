@@ -61,6 +61,10 @@ PYBIND11_MODULE(_kiosk_hip, m) {
                                        kiosk::kGemmBK);
   m.attr("gemm_lds_bytes") = kiosk::kGemmLdsBytes;
   m.attr("gemm_ring_lds_bytes") = kiosk::kGemmRingLdsBytes;
+  m.def("gemm_set_splitk_fused", &kiosk::gemm_set_splitk_fused,
+        py::arg("on"),
+        "4-wave split-K: combine in-launch (True) or via the reduce kernel "
+        "(False, the default)");
   m.attr("sum_blocks") = kiosk::kSumBlocks;
 
   m.def("gemm_shape_ok", &kiosk::gemm_shape_ok);

@@ -44,7 +44,8 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   // 128x128 operands + bias + output + sums + warm-start record
   const size_t elems = 128 * 128;
   char* scratch = nullptr;
-  const size_t ws_bytes = 2 * 64 * 256 * sizeof(float);   // split-K probe
+  // split-K probe: 2 partial planes + the 4-wave path's ticket counter
+  const size_t ws_bytes = 2 * 64 * 256 * sizeof(float) + 256;
   const size_t bytes =
       4 * elems * 2 + 128 * 4 + kSumBlocks * 4 + 4096 + ws_bytes;
   check_hip(hipMalloc(reinterpret_cast<void**>(&scratch), bytes),
@@ -80,12 +81,12 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
     check_hip(launch_gemm256_splitk(a, b, c, bias, r, 64, 256, 64, epi, 2, ws,
                                     ws_bytes, stream),
               "preinit gemm256 split-K");
-    // K = 128 in two 64-deep slices: the 4-wave partial kernel (B spans
-    // the b, c views: it reads scratch it does not write before the reduce)
-    if (epi == 0)
-      check_hip(launch_gemm256_splitk(a, b, c, bias, r, 64, 256, 128, epi, 2,
-                                      ws, ws_bytes, stream),
-                "preinit gemm256 4-wave split-K");
+    // K = 128 in two 64-deep slices: the 4-wave fused split-K kernel (B
+    // spans the b, c views; the output tile c is written only by the last
+    // slice, after both slices have read their operands)
+    check_hip(launch_gemm256_splitk(a, b, c, bias, r, 64, 256, 128, epi, 2,
+                                    ws, ws_bytes, stream),
+              "preinit gemm256 4-wave split-K");
   }
   check_hip(launch_partial_sums(c, elems, sums, stream), "preinit sums");
   check_hip(launch_warmstart(a, elems, rec, 1, 1, kGemmRingLdsBytes, stream),

@@ -243,12 +243,24 @@ def test_spin_kernel_and_roctx(mod):
 
 
 @pytest.mark.parametrize('M,N,K', [(2048, 1024, 4096), (512, 512, 16384),
-                                   (300, 512, 8192)])
+                                   (300, 512, 8192), (777, 1024, 4096)])
 @pytest.mark.parametrize('epilogue', ['none', 'gelu', 'residual'])
-def test_gemm_splitk(mod, M, N, K, epilogue):
-    """Split-K 256x256: fp32 partial planes + fused reduce/epilogue."""
+@pytest.mark.parametrize('fused', [True, False])
+def test_gemm_splitk(mod, M, N, K, epilogue, fused):
+    """Split-K 256x256: two 64-deep-aligned slices run the 4-wave kernel,
+    combined through fp32 partial planes + the reduce/epilogue kernel (the
+    default) or in-launch by each tile's last slice (``fused``); more
+    slices use the 8-wave kernel + reduce."""
     from kiosk_autoscaler_amd.ops import kernels
     assert mod.gemm_workspace_bytes(M, N, K) > 0
+    mod.gemm_set_splitk_fused(fused)
+    try:
+        _check_splitk(mod, kernels, M, N, K, epilogue)
+    finally:
+        mod.gemm_set_splitk_fused(False)
+
+
+def _check_splitk(mod, kernels, M, N, K, epilogue):
     a = rand_bf16(M, K, seed=21)
     b = rand_bf16(N, K, scale=0.05, seed=22)
     bias = torch.randn(N, device='cuda')
@@ -272,5 +284,6 @@ def test_splitk_dispatch(mod):
     assert mod.gemm_pick_variant(2048, 4096, 16384, False) == 3
     assert mod.gemm_pick_variant(2048, 16384, 4096, True) == 5
     assert mod.gemm_workspace_bytes(2048, 16384, 4096) == 0
+    # two fp32 partial planes + one ticket counter per 256x256 tile
     assert mod.gemm_workspace_bytes(2048, 4096, 16384) == \
-        2 * 2048 * 4096 * 4
+        2 * 2048 * 4096 * 4 + 512

@@ -56,6 +56,11 @@ def main():
         def ours_splitk():
             kernels.gemm(a, b, out=out, variant='256splitk')
 
+        def ours_splitk_fused():
+            mod.gemm_set_splitk_fused(True)
+            kernels.gemm(a, b, out=out, variant='256splitk')
+            mod.gemm_set_splitk_fused(False)
+
         def theirs():
             torch.nn.functional.gelu(torch.addmm(bias.to(torch.bfloat16), a,
                                                  b.t()), approximate='tanh')
@@ -73,6 +78,7 @@ def main():
         fns['native256x128'] = ours_256x128
         if mod.gemm_workspace_bytes(M, N, K):
             fns['native256splitk'] = ours_splitk
+            fns['native256splitk_fused'] = ours_splitk_fused
 
         results = {k: [] for k in fns}
         for fn in fns.values():
