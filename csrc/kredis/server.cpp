@@ -186,6 +186,7 @@ bool Server::alive(Db& d, const std::string& key) {
   if (e != d.expires.end() && now_ms() >= e->second) {
     d.expires.erase(e);
     d.keys.erase(key);
+    ++d.version;
     return false;
   }
   return d.keys.count(key) > 0;
@@ -204,7 +205,9 @@ Value* Server::lookup(Db& d, const std::string& key, Value::Type type,
 }
 
 Value& Server::create(Db& d, const std::string& key, Value::Type type) {
-  Value& v = d.keys[key];
+  auto ins = d.keys.try_emplace(key);
+  if (ins.second) ++d.version;
+  Value& v = ins.first->second;
   v = Value();
   v.type = type;
   return v;
@@ -220,12 +223,15 @@ void Server::drop_if_empty(Db& d, const std::string& key) {
   if (empty) {
     d.keys.erase(it);
     d.expires.erase(key);
+    ++d.version;
   }
 }
 
 bool Server::remove(Db& d, const std::string& key) {
   d.expires.erase(key);
-  return d.keys.erase(key) > 0;
+  if (d.keys.erase(key) == 0) return false;
+  ++d.version;
+  return true;
 }
 
 #define WRONG_OR(expr)         \
@@ -268,10 +274,11 @@ void Server::register_commands() {
   t["FLUSHDB"] = [this](Client& c, const Args&, Reply& r) {
     db(c).keys.clear();
     db(c).expires.clear();
+    ++db(c).version;
     r.simple("OK");
   };
   t["FLUSHALL"] = [this](Client&, const Args&, Reply& r) {
-    for (auto& d : dbs_) { d.keys.clear(); d.expires.clear(); }
+    for (auto& d : dbs_) { d.keys.clear(); d.expires.clear(); ++d.version; }
     r.simple("OK");
   };
   t["TIME"] = [](Client&, const Args&, Reply& r) {
@@ -385,6 +392,7 @@ void Server::register_commands() {
     remove(d, a[1]);
     remove(d, a.at(2));
     d.keys[a[2]] = std::move(v);
+    ++d.version;
     if (had) d.expires[a[2]] = deadline;
     if (d.keys[a[2]].type == Value::LIST) touched_list(a[2]);
     r.simple("OK");
@@ -402,9 +410,16 @@ void Server::register_commands() {
       else { r.error("ERR syntax error"); return; }
     }
     Db& d = db(c);
-    std::vector<std::string> keys;
-    for (auto& kv : d.keys) keys.push_back(kv.first);
-    std::sort(keys.begin(), keys.end());
+    if (d.sorted_version != d.version) {
+      d.sorted.clear();
+      d.sorted.reserve(d.keys.size());
+      for (auto& kv : d.keys) d.sorted.push_back(kv.first);
+      std::sort(d.sorted.begin(), d.sorted.end());
+      d.sorted_version = d.version;
+    }
+    // alive() below may expire keys (bumping the version) but only SCAN
+    // rebuilds `sorted`, so this reference stays valid for the call
+    const std::vector<std::string>& keys = d.sorted;
     static const char* names[] = {"string", "list", "hash", "set"};
     std::vector<std::string> out;
     size_t end = std::min(keys.size(), static_cast<size_t>(cursor + count));

@@ -30,6 +30,11 @@ struct Value {
 struct Db {
   std::unordered_map<std::string, Value> keys;
   std::unordered_map<std::string, int64_t> expires;   // monotonic ms
+  // SCAN walks the keys in sorted order; the sorted copy is rebuilt only
+  // when the key set changed (version bumps on every insert / removal)
+  uint64_t version = 0;
+  uint64_t sorted_version = ~0ull;
+  std::vector<std::string> sorted;
 };
 
 // RESP reply builder.

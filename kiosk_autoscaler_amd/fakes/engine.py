@@ -412,13 +412,17 @@ class RedisEngine(object):
             else:
                 return ReplyError('ERR syntax error')
             i += 2
-        keys = sorted(self._live_keys(session))
+        # cursor = position in the sorted keyspace; expiry is checked only
+        # for the keys of this window (not a full sweep per call)
+        keys = sorted(self._dbs[session.db])
         window = keys[cursor:cursor + count]
         nxt = cursor + count if cursor + count < len(keys) else 0
         out = []
         types = {bytes: b'string', list: b'list', dict: b'hash', set: b'set'}
         for key in window:
             if match is not None and not glob_match(match, key):
+                continue
+            if not self._alive(session, key):
                 continue
             if kind is not None and types[type(self._db(session)[key])] != kind:
                 continue

@@ -159,3 +159,17 @@ def test_util_sampler_degrades_without_driver():
     assert gpu_util.mean_busy({'a': {'gfx_busy_pct': 10.0, 'samples': 1},
                                'b': {'gfx_busy_pct': 30.0, 'samples': 2}}) \
         == 20.0
+
+
+def test_bench_tick_inproc_runs():
+    """tools/bench_tick.py (control-plane tick cost) on the in-proc fake."""
+    proc = subprocess.run(
+        [sys.executable, os.path.join(ROOT, 'tools', 'bench_tick.py'),
+         '--ticks', '20', '--modes', 'inproc'],
+        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+        timeout=300)
+    assert proc.returncode == 0, proc.stderr[-2000:]
+    rows = [json.loads(l) for l in proc.stdout.splitlines()
+            if l.startswith('{')]
+    assert {r['tally'] for r in rows} == {'reference', 'atomic'}
+    assert all(r['mean_ms'] > 0 for r in rows)
