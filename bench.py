@@ -417,6 +417,12 @@ def main():
                 'amdsmi_gfx_busy_pct': _r(gpu_util.mean_busy(util)),
                 'fence': {k: _r(v) for k, v in summary['fence'].items()},
                 'reference_sim_latency_s': _r(ref['latency_mean_s']),
+                # same arrival trace, reference policy, ideal zero-delay
+                # actuator: the like-for-like comparison (BASELINE.md's
+                # 3.13 s comes from a different trace)
+                'vs_reference_sim_same_trace': (
+                    round(value / ref['latency_mean_s'], 4)
+                    if value is not None and ref['latency_mean_s'] else None),
                 'reference_sim_gpu_idle_pct': _r(ref['gpu_idle_pct']),
             }
             print(json.dumps(line), flush=True)
