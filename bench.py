@@ -360,8 +360,13 @@ def main():
             events = drain_redis(svc.redis)
             summary = metrics.summarize(events, episodes)
             ref = reference_sim(episodes, args)
+            from kiosk_autoscaler_amd.bench import sim
+            derived = sim.derived_baseline(
+                args.lam_per_gpu * args.gpus, args.gpus, args.kpp,
+                args.queues.split(','), args.interval, args.service_ms / 1e3)
             value = summary['latency_mean_s']
             detail = {'summary': summary, 'reference_sim': ref,
+                      'derived_baseline': derived,
                       'args': vars(args), 'amdsmi': util,
                       'amdsmi_error': getattr(sampler, 'error', None)}
             with open(os.path.join(OUT_DIR, 'bench_detail_n%d.json' %
@@ -424,6 +429,10 @@ def main():
                     round(value / ref['latency_mean_s'], 4)
                     if value is not None and ref['latency_mean_s'] else None),
                 'reference_sim_gpu_idle_pct': _r(ref['gpu_idle_pct']),
+                # BASELINE.md's method (1200 s, 60/60 on/off, 5 seeds) at
+                # this N's lambda and MAX_PODS: the per-N reference curve
+                'derived_baseline_latency_s': _r(derived['latency_mean_s']),
+                'derived_baseline_gpu_idle_pct': _r(derived['gpu_idle_pct']),
             }
             print(json.dumps(line), flush=True)
     finally:

@@ -187,6 +187,28 @@ def baseline_table(seeds=(0, 1, 2, 3, 4), duration=1200.0, on=60.0,
     return out
 
 
+def derived_baseline(lam, max_pods, keys_per_pod=1, queues=('predict',),
+                     interval=5.0, service_s=1.0, seeds=(0, 1, 2, 3, 4),
+                     duration=1200.0, on=60.0, off=60.0):
+    """BASELINE.md §3's method (reference policy, ideal actuator, 1200 s of
+    60 s on / 60 s off Poisson, mean of 5 seeds) at an arbitrary lambda and
+    MAX_PODS -- the per-N reference number bench.py reports next to its own
+    measurement (BASELINE.md only quotes MAX_PODS=1 and 8)."""
+    results = []
+    for seed in seeds:
+        arrivals = poisson_on_off(lam, on, off, duration, seed, tuple(queues))
+        results.append(simulate(arrivals, interval=interval,
+                                service_s=service_s, max_pods=max_pods,
+                                keys_per_pod=keys_per_pod,
+                                queues=tuple(queues)))
+    return {
+        'latency_mean_s': _mean([r['cold_start_mean_s'] for r in results
+                                 if r['cold_start_mean_s'] is not None]),
+        'gpu_idle_pct': _mean([r['gpu_idle_pct'] for r in results
+                               if r['gpu_idle_pct'] is not None]),
+    }
+
+
 if __name__ == '__main__':
     import json
     print(json.dumps(baseline_table(), indent=1))
