@@ -155,6 +155,17 @@ def _mean(values):
     return sum(values) / len(values) if values else None
 
 
+def _phase(k, n, interval):
+    """Stratified tick phase of seed ``k`` of ``n``.
+
+    The on/off period (120 s) is a multiple of INTERVAL, so with the tick
+    grid pinned at t = 0 every burst of a run starts at the same phase (just
+    after a tick: cold starts near INTERVAL, a biased estimate).  Each seed
+    therefore gets its own phase, (k + 0.5) / n x INTERVAL -- the same
+    stratification bench.py applies to its episodes."""
+    return (k + 0.5) / n * interval
+
+
 def baseline_table(seeds=(0, 1, 2, 3, 4), duration=1200.0, on=60.0,
                    off=60.0):
     """Re-derive BASELINE.md §3 rows (means over seeds)."""
@@ -176,10 +187,13 @@ def baseline_table(seeds=(0, 1, 2, 3, 4), duration=1200.0, on=60.0,
     out = {}
     for name, kwargs, lam, _ in rows:
         results = []
-        for seed in seeds:
+        for k, seed in enumerate(seeds):
             arrivals = poisson_on_off(lam, on, off, duration, seed,
                                       kwargs.get('queues', ('predict',)))
-            results.append(simulate(arrivals, **kwargs))
+            results.append(simulate(
+                arrivals, first_tick=_phase(k, len(seeds),
+                                            kwargs.get('interval', 5.0)),
+                **kwargs))
         out[name] = {key: _mean([r[key] for r in results
                                  if r[key] is not None])
                      for key in ('cold_start_mean_s', 'cold_start_max_s',
@@ -195,9 +209,10 @@ def derived_baseline(lam, max_pods, keys_per_pod=1, queues=('predict',),
     MAX_PODS -- the per-N reference number bench.py reports next to its own
     measurement (BASELINE.md only quotes MAX_PODS=1 and 8)."""
     results = []
-    for seed in seeds:
+    for k, seed in enumerate(seeds):
         arrivals = poisson_on_off(lam, on, off, duration, seed, tuple(queues))
         results.append(simulate(arrivals, interval=interval,
+                                first_tick=_phase(k, len(seeds), interval),
                                 service_s=service_s, max_pods=max_pods,
                                 keys_per_pod=keys_per_pod,
                                 queues=tuple(queues)))

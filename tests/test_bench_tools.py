@@ -47,6 +47,20 @@ def test_sim_reproduces_baseline_order_of_magnitude():
     assert 2.5 < lat < 4.6 and 55 < idle < 75
 
 
+def test_derived_baseline_phase_stratified():
+    """bench.py's per-N reference number: BASELINE.md §3 row 1 (MAX=1,
+    lam=0.5: 3.25 s, 1.96 s queue wait, 33.3 % idle) within seed noise, and
+    no tick-phase lock (a grid pinned at t=0 put every burst just after a
+    tick: ~4.5 s at MAX=8, lam=2)."""
+    row1 = sim.derived_baseline(0.5, 1, seeds=(0, 1, 2))
+    assert 2.8 < row1['latency_mean_s'] < 3.6
+    assert 28 < row1['gpu_idle_pct'] < 38
+    row2 = sim.derived_baseline(2.0, 8, seeds=(0, 1, 2), duration=600.0)
+    assert row2['latency_mean_s'] < 4.0
+    assert [sim._phase(k, 4, 5.0) for k in range(4)] == [
+        0.625, 1.875, 3.125, 4.375]
+
+
 def test_strict_policy_cuts_idle():
     arrivals = sim.poisson_on_off(2.0, 60, 60, 600, seed=3)
     ref = sim.simulate(arrivals, max_pods=8)
