@@ -141,7 +141,9 @@ def gpu_idle(events, t_lo, t_hi):
         elif ev == 'key_done':
             begin = starts.pop((worker, e.get('item')), None)
             if begin is not None:
-                busy[worker].append((begin, e['t']))
+                # a key that paused for a fence init was not busy meanwhile
+                begin += int(float(e.get('paused_ms') or 0.0) * 1e6)
+                busy[worker].append((min(begin, e['t']), e['t']))
     alive_total = busy_total = 0
     for worker, t_a in assigned.items():
         t_x = exited.get(worker, t_hi)

@@ -89,7 +89,7 @@ class CpuMlpEngine(object):
         return {'ms': (time.perf_counter() - t0) * 1e3,
                 'checksum': float(x.sum())}
 
-    def forward_for(self, rows, service_ms, seed):
+    def forward_for(self, rows, service_ms, seed, pause=None):
         # the mock has no real pass time: sleep the requested service time
         self._service_ms = float(service_ms)
         return self.forward(rows, 1, seed)
@@ -142,13 +142,29 @@ class HipMlpEngine(object):
         return dict(self.engine.forward(int(rows), int(max(1, passes)),
                                         int(seed)))
 
-    def forward_for(self, rows, service_ms, seed, chunk_ms=25.0):
+    def forward_for(self, rows, service_ms, seed, chunk_ms=25.0, pause=None):
         """Run real forward passes until ``service_ms`` of wall time is
-        spent (chunks of ~``chunk_ms``; the per-pass estimate adapts)."""
+        spent (chunks of ~``chunk_ms``; the per-pass estimate adapts).
+
+        ``pause`` = ``(event, max_ms)``: while ``event`` is clear (a fence
+        epoch is initialising its communicator) stop issuing chunks, for at
+        most ``max_ms`` in total.  RCCL's init waits for the device to go
+        idle, so under back-to-back chunks it otherwise finishes only when
+        the key does (~1 s instead of ~45 ms, profiles/r1_final_check).
+        The paused time is not counted as service."""
         t0 = time.perf_counter()
-        total = {'ms': 0.0, 'gpu_ms': 0.0, 'checksum': 0.0, 'passes': 0}
+        total = {'ms': 0.0, 'gpu_ms': 0.0, 'checksum': 0.0, 'passes': 0,
+                 'paused_ms': 0.0}
         per_pass = self.pass_ms.get(rows) or self.measure(rows)
+        budget_s = pause[1] / 1e3 if pause is not None else 0.0
         while True:
+            if budget_s > 0.0 and not pause[0].is_set():
+                tp = time.perf_counter()
+                pause[0].wait(budget_s)
+                waited = time.perf_counter() - tp
+                budget_s -= waited
+                t0 += waited
+                total['paused_ms'] += waited * 1e3
             left = service_ms - (time.perf_counter() - t0) * 1e3
             if left <= per_pass * 0.5:
                 break

@@ -244,6 +244,11 @@ class FenceAgent(object):
         self._queue = queue.Queue()
         self._aborted = set()
         self.completed = []
+        # cleared while an epoch is in flight: the serving loop waits on it
+        # (bounded, FENCE_YIELD_MS) so communicator init does not queue
+        # behind a whole key of back-to-back forward passes
+        self.idle = threading.Event()
+        self.idle.set()
         self._thread = threading.Thread(target=self._run, name='fence',
                                         daemon=True)
         self._thread.start()
@@ -283,12 +288,15 @@ class FenceAgent(object):
             epoch = message.get('epoch')
             if epoch in self._aborted:
                 continue
+            self.idle.clear()
             try:
                 report = self.run_epoch(message)
             except Exception as err:  # pylint: disable=broad-except
                 logger.warning('fence epoch %s failed: %s', epoch, err)
                 report = {'epoch': epoch, 'ok': False, 'detail': str(err),
                           'transport': self.transport.name}
+            finally:
+                self.idle.set()
             self.completed.append(report)
             if self.events is not None:
                 self.events.emit('fence_rank', worker=self.worker_id,

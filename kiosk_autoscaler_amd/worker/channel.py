@@ -20,6 +20,10 @@ class Channel(object):
         self._lock = threading.Lock()
         self._buf = b''
         self.commands = queue.Queue()
+        # cmd -> callable run on the reader thread instead of queueing: fence
+        # commands must reach the fence agent while the main thread is
+        # inside a key (it only drains ``commands`` between keys)
+        self.direct = {}
         self._reader = None
 
     def emit(self, ev, **fields):
@@ -65,6 +69,11 @@ class Channel(object):
         def pump():
             while True:
                 message = self._read_line()
+                handler = (self.direct.get(message.get('cmd'))
+                           if message is not None else None)
+                if handler is not None:
+                    handler(message)
+                    continue
                 self.commands.put(message if message is not None
                                   else {'cmd': 'eof'})
                 if message is None:

@@ -63,6 +63,8 @@ class WorkerConfig(object):
         self.warm_start = env.get('WARM_START', '1').lower() not in (
             '0', 'false', 'no', 'off')
         self.fence = env.get('FENCE', 'auto')
+        # max ms a key's forward passes pause for an in-flight fence init
+        self.fence_yield_ms = _env_float(env, 'FENCE_YIELD_MS', 250.0)
         # how long an idle worker blocks in BLMOVE: bounds drain latency
         self.poll_block = _env_float(env, 'POLL_BLOCK_S', 0.1)
         self.job_idle_exit = _env_float(env, 'JOB_IDLE_EXIT_S', 1.0)
@@ -189,6 +191,10 @@ class WorkerRuntime(object):
                          stages=self.stages)
         if self.fence_factory is not None:
             self.fence_agent = self.fence_factory(self)
+            direct = getattr(self.channel, 'direct', None)
+            if direct is not None and self.fence_agent is not None:
+                for cmd in ('fence', 'fence_abort'):
+                    direct[cmd] = self.fence_agent.submit
 
     def run(self):
         cfg = self.config
@@ -235,6 +241,8 @@ class WorkerRuntime(object):
                     self._process(consumer, items)
                 idle_since = time.monotonic()
         finally:
+            for cmd in ('fence', 'fence_abort'):
+                getattr(self.channel, 'direct', {}).pop(cmd, None)
             if self.fence_agent is not None and not self.fence_agent.close():
                 self.recycle = False    # a collective may still be running
             if self.engine is not None:
@@ -274,8 +282,11 @@ class WorkerRuntime(object):
         if service_ms > 0:
             # a fixed per-key GPU service time (the benchmark's S): run real
             # forward passes until that much GPU time has been spent
+            pause = None
+            if self.fence_agent is not None and cfg.fence_yield_ms > 0:
+                pause = (self.fence_agent.idle, cfg.fence_yield_ms)
             result = self.engine.forward_for(rows, service_ms,
-                                             jobs[0][3]['seed'])
+                                             jobs[0][3]['seed'], pause=pause)
         else:
             result = self.engine.forward(rows, passes, jobs[0][3]['seed'])
         t_done = time.monotonic_ns()
@@ -297,6 +308,7 @@ class WorkerRuntime(object):
             self.keys_done += 1
             self._emit_event('key_done', item=item, queue=queue, t_ns=t_done,
                              gpu=cfg.slot, compute_ms=result['ms'],
+                             paused_ms=result.get('paused_ms', 0.0),
                              batch=len(jobs))
 
 
