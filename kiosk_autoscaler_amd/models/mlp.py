@@ -151,12 +151,16 @@ class HipMlpEngine(object):
         most ``max_ms`` in total.  RCCL's init waits for the device to go
         idle, so under back-to-back chunks it otherwise finishes only when
         the key does (~1 s instead of ~45 ms, profiles/r1_final_check).
-        The paused time is not counted as service."""
+        The paused time is not counted as service.  An optional third
+        element, ``busy_chunk_ms``, shrinks the chunks instead while the
+        event is clear (after any pause budget is spent), so each device
+        sync inside the init waits for at most one short chunk."""
         t0 = time.perf_counter()
         total = {'ms': 0.0, 'gpu_ms': 0.0, 'checksum': 0.0, 'passes': 0,
                  'paused_ms': 0.0}
         per_pass = self.pass_ms.get(rows) or self.measure(rows)
         budget_s = pause[1] / 1e3 if pause is not None else 0.0
+        busy_chunk = pause[2] if pause is not None and len(pause) > 2 else 0.0
         while True:
             if budget_s > 0.0 and not pause[0].is_set():
                 tp = time.perf_counter()
@@ -168,7 +172,10 @@ class HipMlpEngine(object):
             left = service_ms - (time.perf_counter() - t0) * 1e3
             if left <= per_pass * 0.5:
                 break
-            n = max(1, int(min(left, chunk_ms) / per_pass))
+            chunk = chunk_ms
+            if busy_chunk > 0.0 and not pause[0].is_set():
+                chunk = min(chunk_ms, busy_chunk)
+            n = max(1, int(min(left, chunk) / per_pass))
             out = self.engine.forward(int(rows), n, int(seed))
             per_pass = 0.7 * per_pass + 0.3 * (out['gpu_ms'] / n)
             total['gpu_ms'] += out['gpu_ms']

@@ -64,7 +64,9 @@ class WorkerConfig(object):
             '0', 'false', 'no', 'off')
         self.fence = env.get('FENCE', 'auto')
         # max ms a key's forward passes pause for an in-flight fence init
-        self.fence_yield_ms = _env_float(env, 'FENCE_YIELD_MS', 250.0)
+        self.fence_yield_ms = _env_float(env, 'FENCE_YIELD_MS', 0.0)
+        # forward chunk size (ms) while a fence epoch is in flight (0 = off)
+        self.fence_chunk_ms = _env_float(env, 'FENCE_YIELD_CHUNK_MS', 2.0)
         # how long an idle worker blocks in BLMOVE: bounds drain latency
         self.poll_block = _env_float(env, 'POLL_BLOCK_S', 0.1)
         self.job_idle_exit = _env_float(env, 'JOB_IDLE_EXIT_S', 1.0)
@@ -283,8 +285,10 @@ class WorkerRuntime(object):
             # a fixed per-key GPU service time (the benchmark's S): run real
             # forward passes until that much GPU time has been spent
             pause = None
-            if self.fence_agent is not None and cfg.fence_yield_ms > 0:
-                pause = (self.fence_agent.idle, cfg.fence_yield_ms)
+            if self.fence_agent is not None and (cfg.fence_yield_ms > 0 or
+                                                 cfg.fence_chunk_ms > 0):
+                pause = (self.fence_agent.idle, cfg.fence_yield_ms,
+                         cfg.fence_chunk_ms)
             result = self.engine.forward_for(rows, service_ms,
                                              jobs[0][3]['seed'], pause=pause)
         else:

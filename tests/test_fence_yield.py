@@ -131,3 +131,13 @@ def test_channel_routes_fence_commands_off_the_main_thread():
     os.close(w)
     assert chan.commands.get(timeout=2.0)['cmd'] == 'eof'
     os.close(r)
+
+
+def test_short_chunks_while_fence_busy_without_pausing():
+    eng = _engine()
+    idle = threading.Event()          # fence in flight for ~40 ms
+    threading.Timer(0.04, idle.set).start()
+    out = eng.forward_for(64, 80.0, 0, chunk_ms=20.0, pause=(idle, 0.0, 2.0))
+    assert out['paused_ms'] == 0.0
+    sizes = [n for _, n in eng.engine.calls]
+    assert sizes[0] <= 2 and max(sizes) >= 10
