@@ -2,32 +2,42 @@
 """Headline benchmark: scale-up latency (first key -> GPU-ready) and GPU-idle %
 of the MI355X autoscaler under bursty Poisson load (BASELINE.json metric).
 
-One *step* = one on/off episode of BASELINE config 4 ("bursty Poisson
-arrivals, scale 0 <-> N"): with no worker alive, the first key is enqueued,
-Poisson arrivals continue for ``--on`` seconds, the queue drains, the
-autoscaler scales back to zero and the standby pool refills.  The whole
-product runs for real: ``scale.py`` (the reference-compatible CLI, embedded
-GPU manager) spawns PyTorch-ROCm workers pinned to MI355X GPUs, each builds
-its random-init model in HBM, runs the gfx950 warm-start kernel, publishes
-READY and serves keys with the MFMA MLP (1 s of GPU work per key, S of
-BASELINE.md §3), and READY-set changes are fenced with RCCL.
+One *step* = one **cold-start cycle** (BASELINE config 4 in miniature): with
+the stack scaled to zero, the first key is enqueued at a controlled phase of
+the ``INTERVAL`` tick grid, Poisson arrivals at the config's rate continue
+for ``--on`` seconds, the queue drains and the autoscaler scales back to
+zero.  The whole product runs for real: ``scale.py`` (the
+reference-compatible CLI, embedded GPU manager) hands the work to
+PyTorch-ROCm workers pinned to MI355X GPUs; each builds its random-init
+model in HBM, runs the gfx950 warm-start kernel, publishes READY and serves
+keys with the MFMA MLP (1 s of GPU work per key, S of BASELINE.md §3), and
+READY-set changes are fenced with RCCL.  Warmup cycles carry one key each.
 
-Phase control: the reference's cold-start number is dominated by where the
-first key lands in the ``INTERVAL`` tick grid.  Timed episode
-``i`` enqueues its first key ``(i + 0.5) / K * INTERVAL`` before the next
-tick (stratified sampling of the uniform phase: same expectation as random
-phase, far lower variance at small K).  The reference policy with an ideal
-(zero-delay) actuator is simulated on the identical arrival trace and
-reported beside the measured numbers (``reference_sim``).
+Phase control: the reference's cold-start latency is set by where the
+first key lands in the tick grid.  Timed cycle ``i`` enqueues
+its first key ``(i + 0.5) / K * INTERVAL`` before the predicted next tick
+(stratified sampling of the uniform phase).
+
+Comparison (``vs_baseline``): the reference policy with an ideal,
+zero-delay actuator is simulated on the *identical* arrival trace and the
+*identical* tick instants the live loop used (``reference_sim``).  This is
+the same-N, same-lambda figure: the measured value can only exceed it by
+the real actuation time (tick -> PATCH -> standby -> READY).  BASELINE.md's
+N=8 row (3.13 s) comes from a different trace and N and is reported for
+context only (``derived_baseline_*``).
+
+Accounting that the headline does not hide: ``standby_gpu_s`` (GPU-seconds
+held by standbys that own a HIP context) and ``cold_spawn_*`` (one
+``WARM_POOL=0`` cycle after the timed region: spawn -> import -> HIP
+context -> weights -> warm-start -> READY).
 
 Contract: ``python bench.py --gpus N --steps K --warmup W`` (torchrun with
 N ranks for N > 1; rank 0 drives, every rank brackets the K timed steps with
 barrier + torch.cuda.synchronize(), elapsed = max over ranks).  Scaling is
 weak: arrival rate = ``--lam-per-gpu`` x N (0.25/s per GPU -> 2/s at N = 8,
-exactly BASELINE config 4) in 60 s bursts (``--on``, config 4's "60 s on");
-config 4's 60 s off period is shortened to "until the stack has scaled to
-zero, then ``--off`` s", because nothing is measured while no worker is
-alive.  Rank 0 prints one JSON line.
+BASELINE config 4).  ``--budget-s`` bounds the whole run: a step that would
+not fit is not started, ``steps`` then reports the cycles actually timed,
+and one JSON line is printed by rank 0 on every path, errors included.
 """
 import argparse
 import json
@@ -37,7 +47,9 @@ import socket
 import subprocess
 import sys
 import time
+import traceback
 
+T_PROCESS_START = time.monotonic()
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -46,15 +58,17 @@ from kiosk_autoscaler_amd.bench import gpu_util  # noqa: E402  (no torch)
 METRIC = ('scale-up latency (s) first-key->GPU-ready + GPU-idle-% at fixed '
           'QPS, 1/2/4/8 GPU')
 # BASELINE.md §3, QUEUES=predict, MAX_PODS=8, KEYS_PER_POD=1, lam=2/s,
-# INTERVAL=5 (BASELINE config 4 at N=8): 3.13 s cold start, 65.6 % idle.
-BASELINE_LATENCY_S = 3.13
-BASELINE_IDLE_PCT = 65.6
+# INTERVAL=5: 3.13 s cold start, 65.6 % idle (context only, see docstring)
+BASELINE_N8_LATENCY_S = 3.13
+BASELINE_N8_IDLE_PCT = 65.6
 # KIOSK_BENCH_OUT redirects the detail/event files (tests use a tmp dir)
 OUT_DIR = os.environ.get('KIOSK_BENCH_OUT') or os.path.join(ROOT, 'gpurun_out')
+TICK_KEY = 'kiosk:autoscaler:tick'
 
 
 def log(msg):
-    sys.stderr.write('[bench %s] %s\n' % (time.strftime('%H:%M:%S'), msg))
+    sys.stderr.write('[bench %s +%.0fs] %s\n' % (
+        time.strftime('%H:%M:%S'), time.monotonic() - T_PROCESS_START, msg))
     sys.stderr.flush()
 
 
@@ -87,6 +101,12 @@ def wait_for(predicate, timeout, step=0.05, what='condition'):
     raise TimeoutError('timed out waiting for %s' % what)
 
 
+TORCHRUN_VARS = ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'LOCAL_WORLD_SIZE',
+                 'GROUP_RANK', 'GROUP_WORLD_SIZE', 'ROLE_RANK', 'ROLE_NAME',
+                 'ROLE_WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT',
+                 'OMP_NUM_THREADS_SET')
+
+
 class Services(object):
     """kredis-server + the autoscaler CLI (embedded GPU manager)."""
 
@@ -95,6 +115,9 @@ class Services(object):
         self.n = n_gpus
         self.procs = []
         self.port = free_port()
+        self.scaler_proc = None
+        self.stdout = None
+        self.pool = n_gpus
         os.makedirs(OUT_DIR, exist_ok=True)
 
     def start(self):
@@ -113,6 +136,13 @@ class Services(object):
         self.redis = StrictRedis(host='127.0.0.1', port=self.port,
                                  decode_responses=True)
         wait_for(lambda: self._ping(), 20, what='redis')
+        self.start_scaler(self.n, pool=self.n, timeout=args.pool_timeout)
+        return self
+
+    def start_scaler(self, n_gpus, pool, timeout, tag='bench'):
+        args = self.args
+        self.pool = pool
+        self.redis.delete(TICK_KEY, 'kiosk:pool')
         # the autoscaler and its workers are not torchrun ranks: keep the
         # launcher's rendezvous variables out of their environment
         env = {k: v for k, v in os.environ.items()
@@ -120,36 +150,51 @@ class Services(object):
         env.update({
             'REDIS_HOST': '127.0.0.1', 'REDIS_PORT': str(self.port),
             'REDIS_INTERVAL': '1', 'QUEUES': args.queues,
-            'RESOURCE_NAME': 'bench-worker', 'RESOURCE_NAMESPACE': 'bench',
+            'RESOURCE_NAME': 'bench-worker', 'RESOURCE_NAMESPACE': tag,
             'RESOURCE_TYPE': args.resource_type,
-            'MIN_PODS': '0', 'MAX_PODS': str(self.n),
+            'MIN_PODS': '0', 'MAX_PODS': str(n_gpus),
             'KEYS_PER_POD': str(args.kpp), 'INTERVAL': str(args.interval),
             'SCALE_POLICY': args.policy,
             'SCALE_DOWN_DELAY': str(args.scale_down_delay),
             'IDLE_INTERVAL': str(args.idle_interval),
-            'GPU_IDS': ','.join(str(i) for i in range(self.n)),
-            'WORKER_BACKEND': args.backend, 'WARM_POOL': str(self.n),
+            'GPU_IDS': ','.join(str(i) for i in range(n_gpus)),
+            'WORKER_BACKEND': args.backend, 'WARM_POOL': str(pool),
             'FENCE': args.fence, 'MODEL_DIM': str(args.dim),
             'MODEL_HIDDEN': str(args.hidden), 'MODEL_LAYERS': str(args.layers),
             'ROWS_PER_KEY': str(args.rows), 'EVENT_LOG': 'redis',
-            'TICK_KEY': 'kiosk:autoscaler:tick', 'DEBUG': '0',
-            'LOG_FILE': os.path.join(OUT_DIR, 'bench_autoscaler.log'),
+            'TICK_KEY': TICK_KEY, 'DEBUG': '0',
+            'LOG_FILE': os.path.join(OUT_DIR, '%s_autoscaler.log' % tag),
             'JOB_IDLE_EXIT_S': '0.5',
             'PYTHONPATH': ROOT + os.pathsep + env.get('PYTHONPATH', ''),
         })
         if args.backend == 'cpu':
             env['MOCK_WORK_MS'] = '0'
-        self.stdout = open(os.path.join(OUT_DIR, 'bench_autoscaler.out'), 'w')
+        self.stdout = open(os.path.join(OUT_DIR, '%s_autoscaler.out' % tag),
+                           'w')
         self.scaler_proc = subprocess.Popen(
             [sys.executable, os.path.join(ROOT, 'scale.py')], env=env,
             stdout=self.stdout, stderr=subprocess.STDOUT,
             start_new_session=True)
         self.procs.append(self.scaler_proc)
-        wait_for(lambda: self.redis.get('kiosk:autoscaler:tick'), 60,
+        wait_for(lambda: self._alive() and self.redis.get(TICK_KEY), 120,
                  what='first autoscaler tick')
-        wait_for(self.pool_ready, args.pool_timeout, step=0.2,
-                 what='standby pool boot')
-        return self
+        if pool:
+            wait_for(self.pool_ready, timeout, step=0.2,
+                     what='standby pool boot')
+
+    def stop_scaler(self):
+        proc = self.scaler_proc
+        if proc is not None and proc.poll() is None:
+            proc.send_signal(signal.SIGTERM)
+            try:
+                proc.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                os.killpg(proc.pid, signal.SIGKILL)
+                proc.wait(timeout=10)
+        self.scaler_proc = None
+        if self.stdout is not None:
+            self.stdout.close()
+            self.stdout = None
 
     def _ping(self):
         try:
@@ -157,15 +202,21 @@ class Services(object):
         except Exception:  # pylint: disable=broad-except
             return False
 
-    def pool_ready(self):
+    def _alive(self):
         if self.scaler_proc.poll() is not None:
             raise RuntimeError('autoscaler exited with %s (see %s)' % (
                 self.scaler_proc.returncode, self.stdout.name))
+        return True
+
+    def pool_ready(self):
+        self._alive()
+        if not self.pool:
+            return True
         value = self.redis.get('kiosk:pool')
         if not value:
             return False
         booted, _total = (int(v) for v in value.split())
-        return booted >= self.n
+        return booted >= self.pool
 
     def idle(self):
         if any(True for _ in self.redis.scan_iter(match='kiosk:worker:*')):
@@ -179,20 +230,13 @@ class Services(object):
         return self.pool_ready()
 
     def next_tick_ns(self):
-        start, end, _ = (int(v) for v in
-                         self.redis.get('kiosk:autoscaler:tick').split())
+        start, end, _ = (int(v) for v in self.redis.get(TICK_KEY).split())
         period = int(self.args.interval * 1e9) + (end - start)
         nxt = end + int(self.args.interval * 1e9)
         return nxt, period
 
     def stop(self):
-        if getattr(self, 'scaler_proc', None) is not None and \
-                self.scaler_proc.poll() is None:
-            self.scaler_proc.send_signal(signal.SIGTERM)
-            try:
-                self.scaler_proc.wait(timeout=60)
-            except subprocess.TimeoutExpired:
-                os.killpg(self.scaler_proc.pid, signal.SIGKILL)
+        self.stop_scaler()
         for proc in self.procs:
             if proc.poll() is None:
                 try:
@@ -200,20 +244,42 @@ class Services(object):
                     proc.wait(timeout=10)
                 except (OSError, subprocess.TimeoutExpired):
                     proc.kill()
-        if getattr(self, 'stdout', None):
-            self.stdout.close()
 
 
-def run_episode(svc, gen, args, delay_s, tag):
-    """One on/off episode whose first key lands ``delay_s`` before a tick."""
-    wait_for(svc.idle, args.idle_timeout, step=0.1, what='idle before ' + tag)
+class Budget(object):
+    """Wall-clock guard for the whole run (process start -> JSON line)."""
+
+    def __init__(self, budget_s, reserve_s):
+        self.deadline = T_PROCESS_START + budget_s
+        self.reserve = reserve_s
+        self.cycle_max = 0.0
+
+    def left(self):
+        return self.deadline - time.monotonic()
+
+    def fits(self, estimate):
+        return self.left() - self.reserve >= estimate
+
+    def note(self, seconds):
+        self.cycle_max = max(self.cycle_max, seconds)
+
+
+def run_cycle(svc, gen, args, delay_s, on_s, tag, budget):
+    """One cold-start cycle whose first key lands ``delay_s`` before a tick.
+
+    Never raises on a slow drain: with a policy that strands keys (job +
+    floor division) the cycle is recorded as stranded, its keys are cleared
+    and the next cycle starts from zero workers again."""
+    t_begin = time.monotonic()
+    wait_for(svc.idle, max(5.0, min(args.idle_timeout, budget.left())),
+             step=0.05, what='idle before ' + tag)
     nxt, period = svc.next_tick_ns()
     now = time.monotonic_ns()
     target = nxt - int(delay_s * 1e9)
     while target < now + int(0.05e9):
         nxt += period
         target = nxt - int(delay_s * 1e9)
-    keys = gen.on_window(target, args.on)
+    keys = gen.on_window(target, on_s)
     t_first = keys[0][2]
     items = [k[0] for k in keys]
 
@@ -222,49 +288,114 @@ def run_episode(svc, gen, args, delay_s, tag):
         for item in items:
             pipe.hget(item, 'status')
         return all(s == 'done' for s in pipe.execute())
-    wait_for(all_done, args.drain_timeout, step=0.1, what='drain ' + tag)
+    stranded = False
+    try:
+        wait_for(all_done, max(5.0, min(args.drain_timeout,
+                                        budget.left() - budget.reserve)),
+                 step=0.05, what='drain ' + tag)
+    except TimeoutError:
+        stranded = True
+        log('%s: keys not served in time (policy stranded them?); clearing'
+            % tag)
+        for queue in args.queues.split(','):
+            svc.redis.delete(queue)
     t_done = time.monotonic_ns()
-    wait_for(svc.idle, args.idle_timeout, step=0.1, what='scale-down ' + tag)
+    wait_for(svc.idle, max(5.0, min(args.idle_timeout, budget.left())),
+             step=0.05, what='scale-down ' + tag)
     t_idle = time.monotonic_ns()
-    off_left = args.off - (t_idle - t_done) / 1e9
-    if off_left > 0:
-        time.sleep(off_left)
+    if args.off > 0:
+        time.sleep(args.off)
+    elapsed = time.monotonic() - t_begin
+    budget.note(elapsed)
     log('%s: %d keys, delay %.2fs, drained %.1fs after first key, idle '
-        '%.1fs' % (tag, len(keys), delay_s, (t_done - t_first) / 1e9,
-                   (t_idle - t_first) / 1e9))
+        '%.1fs, cycle %.1fs%s' % (
+            tag, len(keys), delay_s, (t_done - t_first) / 1e9,
+            (t_idle - t_first) / 1e9, elapsed,
+            ' STRANDED' if stranded else ''))
     return {'t_first': t_first, 't_end': t_idle, 'keys': keys,
-            'delay_s': delay_s, 'tick_ns': nxt}
+            'delay_s': delay_s, 'tick_ns': nxt, 'stranded': stranded,
+            'cycle_s': elapsed}
 
 
-def reference_sim(episodes, args):
-    """The reference policy + ideal actuator on each episode's trace."""
+def tick_instants(events):
+    """Instants (ns) the live loop read the queues: tick emit - tick time."""
+    out = []
+    for e in events:
+        if e.get('ev') == 'tick':
+            out.append(e['t'] - int(float(e.get('tick_s') or 0.0) * 1e9))
+    return sorted(out)
+
+
+def reference_sim(episodes, events, args, same_grid=True):
+    """The reference policy + ideal actuator on each episode's trace, at the
+    live loop's tick instants (``same_grid``) or on an ideal grid."""
     from kiosk_autoscaler_amd.bench import sim
+    ticks = tick_instants(events)
     results = []
     for ep in episodes:
-        offset = args.interval - ep['delay_s']
-        arrivals = [((t - ep['t_first']) / 1e9 + offset, q)
+        base = ep['t_first']
+        if same_grid:
+            grid = [(t - base) / 1e9 for t in ticks
+                    if base - 2 * args.interval * 1e9 <= t <= ep['t_end']]
+            grid = [t for t in grid if t > -args.interval]
+            offset = 0.0
+        else:
+            grid = None
+            offset = args.interval - ep['delay_s']
+        # shift so every instant is >= 0 (the sim's clock starts at 0)
+        shift = args.interval
+        arrivals = [((t - base) / 1e9 + shift + offset, q)
                     for _, q, t in ep['keys']]
+        kwargs = {'horizon': (ep['t_end'] - base) / 1e9 + shift +
+                  3 * args.interval}
+        if grid:
+            kwargs['tick_times'] = [t + shift for t in grid]
+        else:
+            kwargs['first_tick'] = shift if same_grid else 0.0
         results.append(sim.simulate(
             arrivals, interval=args.interval, service_s=args.service_ms / 1e3,
-            ready_delay=0.0, max_pods=args.n_gpus, keys_per_pod=args.kpp,
+            ready_delay=0.0, max_pods=args.gpus, keys_per_pod=args.kpp,
             queues=args.queues.split(','), policy='reference',
-            tick_s=0.0, first_tick=0.0))
-    lat = [r['cold_start_mean_s'] for r in results if r['cold_start_mean_s']]
-    idle = [r['gpu_idle_pct'] for r in results if r['gpu_idle_pct']]
+            tick_s=0.0, dt=0.001, **kwargs))
+    lat = [r['cold_start_mean_s'] for r in results
+           if r['cold_start_mean_s'] is not None]
+    idle = [r['gpu_idle_pct'] for r in results if r['gpu_idle_pct'] is not None]
     return {'latency_mean_s': sum(lat) / len(lat) if lat else None,
             'gpu_idle_pct': sum(idle) / len(idle) if idle else None,
+            'grid': 'live tick instants' if same_grid else 'ideal',
             'ready_delay_s': 0.0}
+
+
+def cold_spawn_cycle(svc, gen, args, budget):
+    """One ``WARM_POOL=0`` cycle on GPU 0 after the timed region: the worker
+    process is spawned by the scale-up (no standby), so READY includes
+    interpreter + torch import, HIP context, weights and warm-start."""
+    from kiosk_autoscaler_amd.bench import metrics
+    from kiosk_autoscaler_amd.utils.events import drain_redis
+    svc.stop_scaler()
+    drain_redis(svc.redis)
+    svc.start_scaler(1, pool=0, timeout=60, tag='cold')
+    episode = run_cycle(svc, gen, args, 0.5 * args.interval, 0.0,
+                        'cold-spawn', budget)
+    events = drain_redis(svc.redis)
+    per = metrics.episode_metrics(events, episode)
+    return {'latency_s': per.get('latency_s'),
+            'actuation_s': per.get('actuation_s'),
+            'from_pool': per.get('from_pool'),
+            'stages_ms': per.get('stages_ms')}
 
 
 def parse_args():
     p = argparse.ArgumentParser(description=__doc__.split('\n')[0])
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=3)
+    p.add_argument('--steps', type=int, default=4)
     p.add_argument('--warmup', type=int, default=1)
     p.add_argument('--interval', type=float, default=5.0)
     p.add_argument('--lam-per-gpu', type=float, default=0.25)
-    p.add_argument('--on', type=float, default=60.0)
-    p.add_argument('--off', type=float, default=2.0)
+    p.add_argument('--on', type=float, default=4.0,
+                   help='burst length of a timed cycle (s)')
+    p.add_argument('--off', type=float, default=0.0,
+                   help='extra pause after a cycle has scaled to zero (s)')
     p.add_argument('--service-ms', type=int, default=1000)
     p.add_argument('--queues', default='predict')
     p.add_argument('--kpp', type=int, default=1)
@@ -281,16 +412,14 @@ def parse_args():
     p.add_argument('--layers', type=int, default=4)
     p.add_argument('--rows', type=int, default=2048)
     p.add_argument('--seed', type=int, default=2024)
-    p.add_argument('--pool-timeout', type=float, default=240.0)
-    p.add_argument('--idle-timeout', type=float, default=120.0)
-    p.add_argument('--drain-timeout', type=float, default=300.0)
+    p.add_argument('--budget-s', type=float, default=480.0,
+                   help='wall-clock budget of the whole run (s)')
+    p.add_argument('--cold-cycles', type=int, default=1,
+                   help='WARM_POOL=0 cycles after the timed region (0 = off)')
+    p.add_argument('--pool-timeout', type=float, default=300.0)
+    p.add_argument('--idle-timeout', type=float, default=60.0)
+    p.add_argument('--drain-timeout', type=float, default=120.0)
     return p.parse_args()
-
-
-TORCHRUN_VARS = ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'LOCAL_WORLD_SIZE',
-                 'GROUP_RANK', 'GROUP_WORLD_SIZE', 'ROLE_RANK', 'ROLE_NAME',
-                 'ROLE_WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT',
-                 'OMP_NUM_THREADS_SET')
 
 
 def main():
@@ -298,34 +427,39 @@ def main():
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local_rank = int(os.environ.get('LOCAL_RANK', 0))
-    args.n_gpus = args.gpus
+    budget = Budget(args.budget_s, reserve_s=max(15.0, 2 * args.interval))
+    line = None
     svc = None
-    if rank == 0:
-        # everything that forks runs before this process touches the GPU
-        svc = Services(args, args.gpus).start()
-        log('services up: redis :%d, standby pool booted' % svc.port)
-    import torch
     dist = None
-    if world > 1:
-        import datetime
-        import torch.distributed as dist
-        dist.init_process_group('gloo', rank=rank, world_size=world,
-                                timeout=datetime.timedelta(hours=3))
-    use_cuda = torch.cuda.is_available() and args.backend == 'hip'
-    if use_cuda:
-        torch.cuda.set_device(local_rank)
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    def sync():
-        if use_cuda:
-            torch.cuda.synchronize()
-
+    error = None
     episodes = []
+    elapsed = 0.0
     try:
+        if rank == 0:
+            # everything that forks runs before this process touches the GPU
+            svc = Services(args, args.gpus).start()
+            log('services up: redis :%d, standby pool booted' % svc.port)
+        import torch
+        if world > 1:
+            import datetime
+            import torch.distributed as dist
+            dist.init_process_group(
+                'gloo', rank=rank, world_size=world,
+                timeout=datetime.timedelta(seconds=args.budget_s + 300))
+        use_cuda = torch.cuda.is_available() and args.backend == 'hip'
+        if use_cuda:
+            torch.cuda.set_device(local_rank)
+
+        def barrier():
+            if dist is not None:
+                dist.barrier()
+
+        def sync():
+            if use_cuda:
+                torch.cuda.synchronize()
+
         barrier()
+        gen = None
         if rank == 0:
             from kiosk_autoscaler_amd.bench.loadgen import LoadGenerator
             gen = LoadGenerator(svc.redis, args.queues.split(','),
@@ -333,19 +467,26 @@ def main():
                                 service_ms=args.service_ms, rows=args.rows,
                                 seed=args.seed)
             for w in range(args.warmup):
-                run_episode(svc, gen, args, 0.5 * args.interval,
-                            'warmup %d' % w)
-        sampler = None
-        if rank == 0:
-            sampler = start_util_sampler(args.gpus)
+                if w and not budget.fits(budget.cycle_max + 3 * args.interval):
+                    log('budget: skipping warmup %d..' % w)
+                    break
+                run_cycle(svc, gen, args, 0.5 * args.interval, 0.0,
+                          'warmup %d' % w, budget)
+        sampler = start_util_sampler(args.gpus) if rank == 0 else None
         barrier()
         sync()
         t0 = time.perf_counter()
         if rank == 0:
             for i in range(args.steps):
+                estimate = max(budget.cycle_max, 2 * args.interval) + \
+                    args.on + (args.interval if args.cold_cycles else 0.0)
+                if i and not budget.fits(estimate):
+                    log('budget: stopping after %d of %d steps (%.0f s left)'
+                        % (i, args.steps, budget.left()))
+                    break
                 delay = (i + 0.5) / args.steps * args.interval
-                episodes.append(run_episode(svc, gen, args, delay,
-                                            'step %d' % i))
+                episodes.append(run_cycle(svc, gen, args, delay, args.on,
+                                          'step %d' % i, budget))
         sync()
         barrier()
         elapsed = time.perf_counter() - t0
@@ -355,91 +496,144 @@ def main():
             dist.all_reduce(tensor, op=dist.ReduceOp.MAX)
             elapsed = float(tensor.item())
         if rank == 0:
-            from kiosk_autoscaler_amd.bench import metrics
-            from kiosk_autoscaler_amd.utils.events import drain_redis
-            events = drain_redis(svc.redis)
-            summary = metrics.summarize(events, episodes)
-            ref = reference_sim(episodes, args)
-            from kiosk_autoscaler_amd.bench import sim
-            derived = sim.derived_baseline(
-                args.lam_per_gpu * args.gpus, args.gpus, args.kpp,
-                args.queues.split(','), args.interval, args.service_ms / 1e3)
-            value = summary['latency_mean_s']
-            detail = {'summary': summary, 'reference_sim': ref,
-                      'derived_baseline': derived,
-                      'args': vars(args), 'amdsmi': util,
-                      'amdsmi_error': getattr(sampler, 'error', None)}
-            with open(os.path.join(OUT_DIR, 'bench_detail_n%d.json' %
-                                   args.gpus), 'w') as handle:
-                json.dump(detail, handle, indent=1, default=str)
-            with open(os.path.join(OUT_DIR, 'bench_events_n%d.jsonl' %
-                                   args.gpus), 'w') as handle:
-                for event in events:
-                    handle.write(json.dumps(event) + '\n')
-            line = {
-                'metric': METRIC,
-                'value': round(value, 4) if value is not None else None,
-                'unit': 's',
-                'n_gpus': args.gpus,
-                'steps': args.steps,
-                'warmup': args.warmup,
-                'ms_per_step': round(elapsed * 1e3 / max(1, args.steps), 1),
-                'higher_is_better': False,
-                'scaling': 'weak',
-                'vs_baseline': (round(value / BASELINE_LATENCY_S, 4)
-                                if value is not None else None),
-                'dtype': 'bf16',
-                'data': 'synthetic Poisson on/off keys; random-init weights',
-                'config': {
-                    'model': 'kiosk-mlp %dx(%d->%d->%d) bf16' % (
-                        args.layers, args.dim, args.hidden, args.dim),
-                    'global_batch': args.rows, 'seq_len': 1,
-                    'parallelism': 'replica-dp%d' % args.gpus,
-                    'queues': args.queues, 'interval_s': args.interval,
-                    'lambda_per_s': args.lam_per_gpu * args.gpus,
-                    'on_s': args.on,
-                    'off': 'until scaled to zero, then %g s' % args.off,
-                    'service_s': args.service_ms / 1e3,
-                    'max_pods': args.gpus, 'keys_per_pod': args.kpp,
-                    'policy': args.policy, 'resource_type': args.resource_type,
-                    'idle_interval_s': args.idle_interval,
-                },
-                'gpu_idle_pct': _r(summary['gpu_idle_pct']),
-                'baseline_gpu_idle_pct': BASELINE_IDLE_PCT,
-                'cold_starts': summary['cold_starts'],
-                'first_key_latency_mean_s': _r(
-                    summary['first_key_latency_mean_s']),
-                'latency_p50_s': _r(summary['latency_p50_s']),
-                'latency_max_s': _r(summary['latency_max_s']),
-                'decision_mean_s': _r(summary['decision_mean_s']),
-                'actuation_mean_s': _r(summary['actuation_mean_s']),
-                'first_result_mean_s': _r(summary['first_result_mean_s']),
-                'queue_wait_mean_s': _r(summary['queue_wait_mean_s']),
-                'keys_done': summary['keys_done'], 'keys': summary['keys'],
-                # hardware cross-check of the event-derived busy fraction
-                'event_busy_wall_pct': _r(100.0 * summary['gpu_busy_s'] /
-                                          max(1e-9, elapsed * args.gpus)),
-                'amdsmi_gfx_busy_pct': _r(gpu_util.mean_busy(util)),
-                'fence': {k: _r(v) for k, v in summary['fence'].items()},
-                'reference_sim_latency_s': _r(ref['latency_mean_s']),
-                # same arrival trace, reference policy, ideal zero-delay
-                # actuator: the like-for-like comparison (BASELINE.md's
-                # 3.13 s comes from a different trace)
-                'vs_reference_sim_same_trace': (
-                    round(value / ref['latency_mean_s'], 4)
-                    if value is not None and ref['latency_mean_s'] else None),
-                'reference_sim_gpu_idle_pct': _r(ref['gpu_idle_pct']),
-                # BASELINE.md's method (1200 s, 60/60 on/off, 5 seeds) at
-                # this N's lambda and MAX_PODS: the per-N reference curve
-                'derived_baseline_latency_s': _r(derived['latency_mean_s']),
-                'derived_baseline_gpu_idle_pct': _r(derived['gpu_idle_pct']),
-            }
-            print(json.dumps(line), flush=True)
+            line = report(svc, gen, args, episodes, elapsed, util, sampler,
+                          budget)
+    except Exception as err:  # pylint: disable=broad-except
+        error = '%s: %s' % (type(err).__name__, err)
+        log('FAILED: ' + error)
+        traceback.print_exc()
     finally:
         if svc is not None:
-            svc.stop()
-        if dist is not None:
-            dist.destroy_process_group()
+            try:
+                svc.stop()
+            except Exception:  # pylint: disable=broad-except
+                traceback.print_exc()
+    if rank == 0:
+        if line is None:
+            line = base_line(args, episodes, elapsed)
+        if error:
+            line['error'] = error
+        print(json.dumps(line), flush=True)
+    if dist is not None and error is None:
+        dist.destroy_process_group()
+    return 0 if error is None else 1
+
+
+def base_line(args, episodes, elapsed):
+    steps = len(episodes)
+    return {
+        'metric': METRIC,
+        'value': None,
+        'unit': 's',
+        'n_gpus': args.gpus,
+        'steps': steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(elapsed * 1e3 / steps, 1) if steps else None,
+        'higher_is_better': False,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'bf16',
+        'data': 'synthetic Poisson on/off keys; random-init weights',
+        'config': {
+            'model': 'kiosk-mlp %dx(%d->%d->%d) bf16' % (
+                args.layers, args.dim, args.hidden, args.dim),
+            'global_batch': args.rows, 'seq_len': 1,
+            'parallelism': 'replica-dp%d' % args.gpus,
+            'queues': args.queues, 'interval_s': args.interval,
+            'lambda_per_s': args.lam_per_gpu * args.gpus,
+            'step': 'cold-start cycle: first key at stratified tick phase, '
+                    '%g s Poisson burst, drain, scale to zero' % args.on,
+            'service_s': args.service_ms / 1e3,
+            'max_pods': args.gpus, 'keys_per_pod': args.kpp,
+            'policy': args.policy, 'resource_type': args.resource_type,
+            'idle_interval_s': args.idle_interval,
+        },
+        'steps_requested': args.steps,
+    }
+
+
+def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
+    from kiosk_autoscaler_amd.bench import metrics, sim
+    from kiosk_autoscaler_amd.utils.events import drain_redis
+    events = drain_redis(svc.redis)
+    summary = metrics.summarize(events, episodes) if episodes else None
+    ref = reference_sim(episodes, events, args, same_grid=True)
+    ref_ideal = reference_sim(episodes, events, args, same_grid=False)
+    cold = None
+    if args.cold_cycles and args.backend in ('hip', 'cpu') and \
+            budget.fits(2 * args.interval + 20.0):
+        try:
+            cold = cold_spawn_cycle(svc, gen, args, budget)
+        except Exception as err:  # pylint: disable=broad-except
+            cold = {'error': '%s: %s' % (type(err).__name__, err)}
+    derived = None
+    if budget.fits(30.0):
+        derived = sim.derived_baseline(
+            args.lam_per_gpu * args.gpus, args.gpus, args.kpp,
+            args.queues.split(','), args.interval, args.service_ms / 1e3)
+    line = base_line(args, episodes, elapsed)
+    if summary is None:
+        return line
+    value = summary['latency_mean_s']
+    detail = {'summary': summary, 'reference_sim': ref,
+              'reference_sim_ideal_grid': ref_ideal,
+              'derived_baseline': derived, 'cold_spawn': cold,
+              'args': vars(args), 'amdsmi': util,
+              'amdsmi_error': getattr(sampler, 'error', None),
+              'cycles_s': [ep['cycle_s'] for ep in episodes]}
+    with open(os.path.join(OUT_DIR, 'bench_detail_n%d.json' % args.gpus),
+              'w') as handle:
+        json.dump(detail, handle, indent=1, default=str)
+    with open(os.path.join(OUT_DIR, 'bench_events_n%d.jsonl' % args.gpus),
+              'w') as handle:
+        for event in events:
+            handle.write(json.dumps(event) + '\n')
+    ref_lat = ref['latency_mean_s']
+    fence = summary['fence']
+    line.update({
+        'value': _r(value),
+        # value / the reference policy with an ideal (zero-delay) actuator
+        # on the same arrival trace and the same tick instants
+        'vs_baseline': (round(value / ref_lat, 4)
+                        if value is not None and ref_lat else None),
+        'baseline_kind': 'reference policy, ideal actuator, same trace and '
+                         'tick instants (same N, same lambda)',
+        'baseline_latency_s': _r(ref_lat),
+        'baseline_gpu_idle_pct': _r(ref['gpu_idle_pct']),
+        'gpu_idle_pct': _r(summary['gpu_idle_pct']),
+        'standby_gpu_s': _r(summary['standby_gpu_s']),
+        'gpu_alive_s': _r(summary['gpu_alive_s']),
+        'gpu_busy_s': _r(summary['gpu_busy_s']),
+        'gpu_idle_incl_standby_pct': _r(summary['gpu_idle_incl_standby_pct']),
+        'cold_starts': summary['cold_starts'],
+        'first_key_latency_mean_s': _r(summary['first_key_latency_mean_s']),
+        'latency_p50_s': _r(summary['latency_p50_s']),
+        'latency_max_s': _r(summary['latency_max_s']),
+        'decision_mean_s': _r(summary['decision_mean_s']),
+        'actuation_mean_s': _r(summary['actuation_mean_s']),
+        'first_result_mean_s': _r(summary['first_result_mean_s']),
+        'queue_wait_mean_s': _r(summary['queue_wait_mean_s']),
+        'keys_done': summary['keys_done'], 'keys': summary['keys'],
+        'stranded_cycles': sum(1 for ep in episodes if ep['stranded']),
+        'cold_spawn_latency_s': _r((cold or {}).get('latency_s')),
+        'cold_spawn_actuation_s': _r((cold or {}).get('actuation_s')),
+        'event_busy_wall_pct': _r(100.0 * summary['gpu_busy_s'] /
+                                  max(1e-9, elapsed * args.gpus)),
+        'amdsmi_gfx_busy_pct': _r(gpu_util.mean_busy(util)),
+        'fence_transport': ','.join(fence['fence_transport']) or None,
+        'fence_max_ranks': fence['fence_max_ranks'],
+        'fence': {k: _r(v) for k, v in fence.items()
+                  if k not in ('fence_transport', 'fence_max_ranks')},
+        'reference_sim_ideal_grid_latency_s': _r(ref_ideal['latency_mean_s']),
+        'derived_baseline_latency_s': _r((derived or {}).get(
+            'latency_mean_s')),
+        'derived_baseline_gpu_idle_pct': _r((derived or {}).get(
+            'gpu_idle_pct')),
+        'baseline_md_n8': {'latency_s': BASELINE_N8_LATENCY_S,
+                           'gpu_idle_pct': BASELINE_N8_IDLE_PCT},
+        'wall_s': round(time.monotonic() - T_PROCESS_START, 1),
+    })
+    return line
 
 
 def start_util_sampler(n_gpus):
@@ -466,4 +660,4 @@ def _r(value, nd=4):
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

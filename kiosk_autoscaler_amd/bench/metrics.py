@@ -158,13 +158,46 @@ def gpu_idle(events, t_lo, t_hi):
             alive_total / 1e9, busy_total / 1e9)
 
 
+def standby_gpu(events, t_lo, t_hi):
+    """GPU-seconds in [t_lo, t_hi] held by standbys that own a HIP context.
+
+    A device-mode standby (``preinit`` non-empty) or a recycled worker keeps
+    its context and code objects resident while it waits for an assignment:
+    the reference at 0 replicas holds nothing, so this cost is reported next
+    to the GPU-idle % instead of being hidden in it.  An interval opens at
+    ``standby_ready`` and closes at the ``worker_assigned`` of the same pid
+    (or the window end)."""
+    open_at = {}
+    total = 0
+    for e in sorted(events, key=lambda e: e.get('t', 0)):
+        ev = e.get('ev')
+        pid = e.get('pid')
+        if ev == 'standby_ready' and (e.get('preinit') or e.get('recycled')):
+            open_at.setdefault(pid, e['t'])
+        elif ev == 'worker_assigned' and pid in open_at:
+            start = open_at.pop(pid)
+            total += max(0, min(e['t'], t_hi) - max(start, t_lo))
+        elif ev == 'standby_exit' and pid in open_at:
+            start = open_at.pop(pid)
+            total += max(0, min(e['t'], t_hi) - max(start, t_lo))
+    for start in open_at.values():
+        total += max(0, t_hi - max(start, t_lo))
+    return total / 1e9
+
+
 def fence_stats(events):
     """N4 membership fences seen in the run: transport(s), count, mean wall
     time (manager: epoch start -> rank 0 ack), communicator set-up and
-    all-reduce times reported by rank 0."""
+    all-reduce times reported by rank 0, and the largest communicator any
+    rank reported (``n`` of ``fence_rank``)."""
     done = [e for e in events if e.get('ev') == 'fence_done']
+    ranks = [e for e in events if e.get('ev') == 'fence_rank' and e.get('ok')]
     return {
         'fences': len(done),
+        'fence_max_ranks': max([int(e.get('n') or 0) for e in ranks],
+                               default=0),
+        'fence_modes': dict(collections.Counter(
+            str(e.get('mode')) for e in ranks if e.get('rank') == 0)),
         'fence_transport': sorted({str(e.get('transport')) for e in done}),
         'fence_wall_ms_mean': _mean([1e3 * e['wall_s'] for e in done
                                      if e.get('wall_s') is not None]),
@@ -178,10 +211,16 @@ def summarize(events, episodes):
     per = [episode_metrics(events, ep) for ep in episodes]
     lat = [v for p in per for v in p['cold_starts_s']]
     first = [p['latency_s'] for p in per]
-    idle, alive_s, busy_s = gpu_idle(
-        events, episodes[0]['t_first'] if episodes else 0,
-        episodes[-1]['t_end'] if episodes else 0)
+    t_lo = episodes[0]['t_first'] if episodes else 0
+    t_hi = episodes[-1]['t_end'] if episodes else 0
+    idle, alive_s, busy_s = gpu_idle(events, t_lo, t_hi)
+    standby_s = standby_gpu(events, t_lo, t_hi)
+    held = alive_s + standby_s
     return {
+        'standby_gpu_s': standby_s,
+        # idle share if standby-held GPU time counted as alive-and-idle
+        'gpu_idle_incl_standby_pct': (100.0 * (held - busy_s) / held
+                                      if held > 0 else None),
         'latency_mean_s': _mean(lat),
         'cold_starts': len(lat),
         'first_key_latency_mean_s': _mean(first),

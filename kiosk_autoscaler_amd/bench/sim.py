@@ -63,9 +63,18 @@ class _Worker(object):
 def simulate(arrivals, interval=5.0, service_s=1.0, ready_delay=0.0,
              min_pods=0, max_pods=1, keys_per_pod=1, queues=('predict',),
              policy='reference', tick_s=0.0, horizon=None, dt=0.01,
-             first_tick=0.0):
-    """Run the simulation; returns a metrics dict."""
+             first_tick=0.0, tick_times=None):
+    """Run the simulation; returns a metrics dict.
+
+    ``tick_times`` (sorted, seconds) replaces the periodic grid by an
+    observed one -- the live benchmark passes the instants its own loop
+    read the queues, so reference and measurement decide at the same
+    moments and differ only by the actuator; after the last observed tick
+    the grid continues every ``tick_s + interval``."""
     queues = list(queues)
+    observed = sorted(tick_times) if tick_times else []
+    if observed:
+        first_tick = observed[0]
     pending = {q: collections.deque() for q in queues}
     arrivals = sorted(arrivals)
     horizon = horizon if horizon is not None else (
@@ -73,6 +82,7 @@ def simulate(arrivals, interval=5.0, service_s=1.0, ready_delay=0.0,
     workers = []
     next_arrival = 0
     next_tick = first_tick
+    tick_index = 0
     cold_starts = []
     waits = []
     cold_pending = None  # arrival time of the key that found no worker
@@ -129,7 +139,11 @@ def simulate(arrivals, interval=5.0, service_s=1.0, ready_delay=0.0,
                 for w in order[:current - desired]:
                     if w.current is None:
                         w.removed = t
-            next_tick = t + tick_s + interval
+            tick_index += 1
+            if tick_index < len(observed):
+                next_tick = max(observed[tick_index], t + dt / 2)
+            else:
+                next_tick = t + tick_s + interval
         if (next_arrival >= len(arrivals) and not any(pending.values())
                 and all(w.removed is not None for w in workers)
                 and t > (arrivals[-1][0] if arrivals else 0)):
