@@ -241,6 +241,16 @@ PYBIND11_MODULE(_kiosk_hip, m) {
            }),
            py::arg("unique_id"), py::arg("nranks"), py::arg("rank"),
            py::arg("timeout") = 60.0)
+      .def(py::init<int, int, double>(), py::arg("nranks"), py::arg("rank"),
+           py::arg("timeout") = 60.0)
+      .def(
+          "connect",
+          [](kiosk::Fence& f, py::bytes uid) {
+            std::string id = uid;
+            py::gil_scoped_release release;
+            f.connect(id);
+          },
+          py::arg("unique_id"))
       .def("allreduce", &kiosk::Fence::allreduce,
            py::call_guard<py::gil_scoped_release>())
       .def(
@@ -257,6 +267,9 @@ PYBIND11_MODULE(_kiosk_hip, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("abort", &kiosk::Fence::abort,
            py::call_guard<py::gil_scoped_release>())
+      .def("request_abort", &kiosk::Fence::request_abort)
+      .def_property_readonly("abort_requested",
+                             &kiosk::Fence::abort_requested)
       .def_property_readonly("nranks", &kiosk::Fence::nranks)
       .def_property_readonly("rank", &kiosk::Fence::rank);
 }

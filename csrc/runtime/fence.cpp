@@ -133,6 +133,10 @@ double rccl_warmup(double timeout_s) {
   return (now_s() - t0) * 1e3;
 }
 
+// Polls a non-blocking communicator until its pending operation settles.
+// Never aborts: on failure, timeout or request_abort() it throws and the
+// caller aborts exactly once (the communicator may be comm_ or a shrink
+// child that is not owned yet).
 void Fence::wait_ready(void* comm, double timeout_s, const char* what) {
   const double deadline = now_s() + timeout_s;
   while (true) {
@@ -142,27 +146,37 @@ void Fence::wait_ready(void* comm, double timeout_s, const char* what) {
     if (res != ncclSuccess) state = res;
     if (state == ncclSuccess) return;
     if (state != ncclInProgress) {
-      rccl().CommAbort(static_cast<ncclComm_t>(comm));
       throw std::runtime_error(std::string(what) + " failed: " +
                                rccl().GetErrorString(state));
     }
+    if (abort_requested_.load(std::memory_order_relaxed)) {
+      throw std::runtime_error(std::string(what) + " aborted on request");
+    }
     if (now_s() > deadline) {
-      rccl().CommAbort(static_cast<ncclComm_t>(comm));
       throw std::runtime_error(std::string(what) + " timed out");
     }
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
 }
 
-Fence::Fence(const std::string& unique_id, int nranks, int rank,
-             double timeout_s)
+Fence::Fence(int nranks, int rank, double timeout_s)
     : nranks_(nranks), rank_(rank), timeout_s_(timeout_s) {
-  if (unique_id.size() != sizeof(ncclUniqueId)) {
-    throw std::invalid_argument("unique id must be 128 bytes");
-  }
   if (nranks < 1 || rank < 0 || rank >= nranks) {
     throw std::invalid_argument("bad rank / nranks");
   }
+}
+
+Fence::Fence(const std::string& unique_id, int nranks, int rank,
+             double timeout_s)
+    : Fence(nranks, rank, timeout_s) {
+  connect(unique_id);
+}
+
+void Fence::connect(const std::string& unique_id) {
+  if (unique_id.size() != sizeof(ncclUniqueId)) {
+    throw std::invalid_argument("unique id must be 128 bytes");
+  }
+  if (comm_ || stream_) throw std::runtime_error("fence already connected");
   try {
     init(unique_id);
   } catch (...) {
@@ -215,19 +229,26 @@ std::pair<std::vector<long long>, double> Fence::allreduce(
   check_hip(hipMemcpyAsync(dev_, host_, n * sizeof(long long),
                            hipMemcpyHostToDevice, stream_),
             "fence upload");
-  check_nccl(rccl().AllReduce(dev_, dev_ + 64, n, ncclInt64, ncclSum,
-                              static_cast<ncclComm_t>(comm_), stream_),
-             "ncclAllReduce");
-  wait_ready(comm_, timeout_s_, "ncclAllReduce enqueue");
+  try {
+    check_nccl(rccl().AllReduce(dev_, dev_ + 64, n, ncclInt64, ncclSum,
+                                static_cast<ncclComm_t>(comm_), stream_),
+               "ncclAllReduce");
+    wait_ready(comm_, timeout_s_, "ncclAllReduce enqueue");
+  } catch (...) {
+    abort();     // a communicator whose collective failed is never reused
+    throw;
+  }
   check_hip(hipMemcpyAsync(host_, dev_ + 64, n * sizeof(long long),
                            hipMemcpyDeviceToHost, stream_),
             "fence download");
   // bounded wait: a dead peer must not hang the worker forever
   const double deadline = now_s() + timeout_s_;
   while (hipStreamQuery(stream_) == hipErrorNotReady) {
-    if (now_s() > deadline) {
-      abort();
-      throw std::runtime_error("fence all-reduce timed out");
+    const bool late = now_s() > deadline;
+    if (late || abort_requested_.load(std::memory_order_relaxed)) {
+      abort();   // unblocks the kernel waiting on a dead peer
+      throw std::runtime_error(late ? "fence all-reduce timed out"
+                                    : "fence all-reduce aborted on request");
     }
     std::this_thread::yield();
   }
@@ -248,7 +269,12 @@ void Fence::shrink(const std::vector<int>& excluded, double timeout_s) {
                                static_cast<int>(ex.size()), &next, nullptr,
                                NCCL_SHRINK_DEFAULT),
              "ncclCommShrink");
-  wait_ready(next, timeout_s, "ncclCommShrink");
+  try {
+    wait_ready(next, timeout_s, "ncclCommShrink");
+  } catch (...) {
+    rccl().CommAbort(next);   // the child is ours to abort; the parent stays
+    throw;
+  }
   void* old = comm_;
   comm_ = next;
   int below = 0;
@@ -259,22 +285,33 @@ void Fence::shrink(const std::vector<int>& excluded, double timeout_s) {
 }
 
 void Fence::abort() {
-  if (comm_) {
-    rccl().CommAbort(static_cast<ncclComm_t>(comm_));
-    comm_ = nullptr;
-  }
+  void* comm = comm_;
+  comm_ = nullptr;   // cleared first: nothing can reach a freed communicator
+  if (comm) rccl().CommAbort(static_cast<ncclComm_t>(comm));
+}
+
+void Fence::request_abort() {
+  abort_requested_.store(true, std::memory_order_relaxed);
 }
 
 void Fence::destroy() {
   if (comm_) {
-    rccl().CommFinalize(static_cast<ncclComm_t>(comm_));
-    try {
-      wait_ready(comm_, timeout_s_, "ncclCommFinalize");
-    } catch (...) {
-      comm_ = nullptr;   // already aborted by wait_ready
+    bool finalized = false;
+    if (!abort_requested_.load(std::memory_order_relaxed)) {
+      rccl().CommFinalize(static_cast<ncclComm_t>(comm_));
+      try {
+        wait_ready(comm_, timeout_s_, "ncclCommFinalize");
+        finalized = true;
+      } catch (...) {
+      }
     }
-    if (comm_) rccl().CommDestroy(static_cast<ncclComm_t>(comm_));
-    comm_ = nullptr;
+    if (finalized) {
+      void* comm = comm_;
+      comm_ = nullptr;
+      rccl().CommDestroy(static_cast<ncclComm_t>(comm));
+    } else {
+      abort();   // a peer is gone: finalize would wait on it
+    }
   }
   if (stream_) {
     hipStreamSynchronize(stream_);

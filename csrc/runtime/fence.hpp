@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <string>
 #include <utility>
 #include <vector>
@@ -28,6 +29,10 @@ class Fence {
  public:
   // Collective: every rank calls it with the same id and nranks.
   Fence(const std::string& unique_id, int nranks, int rank, double timeout_s);
+  // Two-phase form: the object exists (so another thread can
+  // request_abort() it) before the collective connect() blocks.
+  Fence(int nranks, int rank, double timeout_s);
+  void connect(const std::string& unique_id);
   ~Fence();
   Fence(const Fence&) = delete;
   Fence& operator=(const Fence&) = delete;
@@ -39,7 +44,12 @@ class Fence {
   // Collective over the surviving ranks: drop `excluded` (old rank ids).
   void shrink(const std::vector<int>& excluded, double timeout_s);
   void destroy();
+  // Owner thread only: aborts the communicator once (idempotent).
   void abort();
+  // Any thread: makes a blocked allreduce/init/finalize of the owner
+  // thread abort and throw at its next poll (a peer died mid-collective).
+  void request_abort();
+  bool abort_requested() const { return abort_requested_.load(); }
   int nranks() const { return nranks_; }
   int rank() const { return rank_; }
 
@@ -54,6 +64,7 @@ class Fence {
   int nranks_ = 0;
   int rank_ = 0;
   double timeout_s_ = 60.0;
+  std::atomic<bool> abort_requested_{false};
 };
 
 }  // namespace kiosk

@@ -194,10 +194,18 @@ def fence_stats(events):
     ranks = [e for e in events if e.get('ev') == 'fence_rank' and e.get('ok')]
     return {
         'fences': len(done),
-        'fence_max_ranks': max([int(e.get('n') or 0) for e in ranks],
+        'fence_max_ranks': max([int(e.get('n') or 0) for e in ranks + done]
+                               + [int(e.get('n') or 0) for e in events
+                                  if e.get('ev') == 'node_comm_ready'],
                                default=0),
         'fence_modes': dict(collections.Counter(
-            str(e.get('mode')) for e in ranks if e.get('rank') == 0)),
+            str(e.get('mode')) for e in done)),
+        'node_comm_generations': sum(1 for e in events
+                                     if e.get('ev') == 'node_comm_ready'),
+        'node_comm_init_ms_max': max([float(e.get('init_ms') or 0.0)
+                                      for e in events
+                                      if e.get('ev') == 'node_comm_ready'],
+                                     default=None),
         'fence_transport': sorted({str(e.get('transport')) for e in done}),
         'fence_wall_ms_mean': _mean([1e3 * e['wall_s'] for e in done
                                      if e.get('wall_s') is not None]),

@@ -42,6 +42,7 @@ import threading
 import time
 
 from ..utils.events import NULL as NULL_EVENTS
+from .nodecomm import NODE_EVENTS, NodeComm
 from .resources import ActuatorError, ResourceList, ResourceView, \
     desired_from_body
 
@@ -133,6 +134,7 @@ class _Process(object):
         self.booted = False
         self.eof = False
         self.recycles = 0
+        self.node_ok = False    # runs a node-communicator agent
 
     @property
     def pid(self):
@@ -239,7 +241,8 @@ class GpuManager(object):
                  pool_template=None, events=None, fence=True,
                  pool_mode='device', state_ttl=3600,
                  fence_timeout=60.0, max_restart_backoff=10.0,
-                 worker_timeout=0.0, start_timeout=0.0, recycle=True):
+                 worker_timeout=0.0, start_timeout=0.0, recycle=True,
+                 fence_comm='node'):
         self.slots = list(slots)
         self.redis = redis_client
         self.pool_size = max(0, int(pool_size))
@@ -268,6 +271,15 @@ class GpuManager(object):
                                 & 0xfffff)
         self._stopping = False
         self.history = []   # exited workers, for accounting
+        # persistent node-wide communicator: needs one long-lived process
+        # per slot (a standby for every GPU, recycled workers); otherwise
+        # every epoch bootstraps its own communicator (round-1 mode)
+        self.fence_comm = fence_comm
+        self.node = None
+        if (fence and fence_comm == 'node' and self.recycle and
+                pool_template is not None and self.slots and
+                self.pool_size >= len(self.slots)):
+            self.node = NodeComm(self, fence_timeout=min(fence_timeout, 30.0))
 
     # ------------------------------------------------------------------
     # API (the kubernetes AppsV1Api / BatchV1Api analogs)
@@ -507,6 +519,8 @@ class GpuManager(object):
                     self._on_worker_messages(owner)
             self._reap_all()
             self._watchdog()
+            if self.node is not None and not self._stopping:
+                self.node.step()
             for resource in self.resources.values():
                 self._reconcile(resource)
                 self._maybe_fence(resource)
@@ -526,7 +540,8 @@ class GpuManager(object):
         elif slot is not None:
             argv += ['--pin', json.dumps({
                 'gpu': slot.visible_id, 'slot': slot.index, 'cpus': slot.cpus,
-                'preinit': self.pool_mode})]
+                'preinit': self.pool_mode,
+                'node_fence': self.node is not None})]
         env = dict(os.environ)
         env.update({k: str(v) for k, v in template.env.items()})
         env['PYTHONUNBUFFERED'] = '1'
@@ -603,6 +618,9 @@ class GpuManager(object):
             self._on_standby_message(proc, message)
 
     def _on_standby_message(self, proc, message):
+        if self.node is not None and message.get('ev') in NODE_EVENTS:
+            self.node.on_message(proc, message)
+            return
         if message.get('ev') == 'standby':
             proc.booted = True
             self._publish_pool()
@@ -661,6 +679,7 @@ class GpuManager(object):
             'template': resource.template.to_dict(),
             't_assign': time.monotonic_ns(),
             'recycle': self._recycle_ok(resource),
+            'node_fence': self.node is not None,
         }
         proc = self._take_standby(resource.template, slot)
         from_pool = proc is not None
@@ -739,7 +758,9 @@ class GpuManager(object):
                 worker.proc.eof = True
                 continue
             kind = message.get('ev')
-            if kind == 'stage':
+            if self.node is not None and kind in NODE_EVENTS:
+                self.node.on_message(worker.proc, message)
+            elif kind == 'stage':
                 worker.stages[message.get('stage')] = message.get('t')
             elif kind == 'ready':
                 if worker.state == STARTING:
@@ -906,6 +927,9 @@ class GpuManager(object):
     def _maybe_fence(self, resource):
         if not self.fence_enabled:
             return
+        if self.node is not None:
+            self._maybe_node_fence(resource)
+            return
         inflight = resource.fence_inflight
         if inflight is not None:
             epoch, members, started = inflight
@@ -949,6 +973,25 @@ class GpuManager(object):
         resource.fence_inflight = (epoch, members, time.monotonic())
         self.events.emit('fence_start', epoch=epoch, members=members)
 
+    def _maybe_node_fence(self, resource):
+        """One 72-B all-reduce over the persistent communicator; waits
+        (fence_wanted stays set) while a generation is being built or
+        another resource's epoch is in flight."""
+        if not resource.fence_wanted or not self.node.ready or \
+                self.node.inflight is not None:
+            return
+        members = sorted((w.id for w in resource.ready()),
+                         key=lambda wid: resource.workers[wid].slot.index)
+        resource.fence_wanted = False
+        if members == resource.fenced_members:
+            return
+        if not members:
+            resource.fenced_members = []
+            resource.fenced_epoch = resource.epoch
+            self._publish_active(resource)
+            return
+        self.node.fence(resource, members)
+
     def _fence_failed(self, resource):
         """Retry with a fresh communicator after an exponential backoff, so
         a persistently failing bootstrap cannot spin on RCCL inits."""
@@ -971,6 +1014,9 @@ class GpuManager(object):
                            message.get('detail'))
             self._fence_failed(resource)
             return
+        self._fence_completed(resource, epoch, members, started, message)
+
+    def _fence_completed(self, resource, epoch, members, started, message):
         resource.fence_fresh = False
         resource.fence_failures = 0
         resource.fenced_epoch = epoch
@@ -979,7 +1025,9 @@ class GpuManager(object):
                          wall_s=time.monotonic() - started,
                          transport=message.get('transport'),
                          allreduce_us=message.get('allreduce_us'),
-                         init_ms=message.get('init_ms'))
+                         init_ms=message.get('init_ms'),
+                         n=message.get('n'), mode=message.get('mode'),
+                         gen=message.get('gen'))
         self._publish_active(resource)
 
     def _publish_active(self, resource):

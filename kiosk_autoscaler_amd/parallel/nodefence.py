@@ -1,0 +1,401 @@
+"""Persistent node-wide membership communicator (SURVEY N4, round-2 design).
+
+Round 1 re-bootstrapped an RCCL communicator over the READY workers at every
+membership change (~250 ms of ``ncclCommInitRank`` per scale event at one
+rank, more at eight).  But the processes behind the GPU slots are long-lived:
+a standby becomes a worker, a drained worker is recycled back into its
+GPU's standby, and the process (HIP context, RCCL state) survives both.  So
+the communicator is built **once** over every slot's process and every
+membership change is fenced by the 72-byte all-reduce alone:
+
+* ``comm_init {gen, rank, nranks}`` -- rank 0 (lowest slot) creates the
+  communicator id and reports it (``comm_uid``); the manager relays it to the
+  other ranks; all connect.  Each rank reports ``comm_ready``.  This happens
+  at pool boot and again only after a slot's process *dies* (no grow in
+  RCCL, so a replacement process means a new generation).
+* ``fence {epoch, gen, slots}`` -- every rank contributes
+  ``{epoch, bit(own slot in slots)}`` to the int64[1 + 8] sum; standbys and
+  other resources' workers contribute zeros.  The result must equal
+  ``{epoch * nranks, membership mask}``; rank 0 acknowledges (``fenced``).
+* ``comm_abort {gen}`` -- a peer died: any blocked collective is aborted
+  (``Fence::request_abort`` is safe from the reader thread) and the
+  communicator is dropped; the next generation replaces it.
+
+Transports: :class:`RcclNodeTransport` (production, RCCL over xGMI through
+``_kiosk_hip.Fence``), :class:`GlooNodeTransport` (CPU test fake, one
+persistent gloo group per generation) and :class:`StoreNodeTransport`
+(Redis lists; mock CPU workers).
+"""
+import json
+import logging
+import os
+import queue
+import tempfile
+import threading
+import time
+import uuid
+
+from .fence import MIN_SLOTS, FenceError
+
+logger = logging.getLogger('NodeFence')
+
+NODE_COMMANDS = ('comm_init', 'comm_uid', 'comm_abort', 'fence', 'fence_abort')
+NODE_EVENTS = ('comm_uid', 'comm_ready', 'fenced', 'node_agent')
+STORE_KEY = 'kiosk:nodefence:{uid}:{epoch}'
+
+
+def node_vector(epoch, slot, member_slots, width):
+    vec = [0] * (1 + width)
+    vec[0] = int(epoch)
+    if int(slot) in set(int(s) for s in member_slots):
+        vec[1 + int(slot)] = 1
+    return vec
+
+
+def node_expected(epoch, nranks, member_slots, width):
+    vec = [0] * (1 + width)
+    vec[0] = int(epoch) * int(nranks)
+    for slot in member_slots:
+        vec[1 + int(slot)] += 1
+    return vec
+
+
+def node_width(slot_count):
+    return max(MIN_SLOTS, int(slot_count))
+
+
+# ---------------------------------------------------------------------------
+# transports: make_uid (rank 0) / connect (collective) / allreduce / abort
+# ---------------------------------------------------------------------------
+class RcclNodeTransport(object):
+    name = 'rccl'
+
+    def __init__(self, timeout=60.0, native=None):
+        if native is None:
+            from ..ops import native as native_ops
+            native = native_ops.load()
+        self.native = native
+        self.timeout = float(timeout)
+        self.comm = None
+
+    def make_uid(self, gen):
+        return self.native.fence_unique_id().hex()
+
+    def connect(self, gen, rank, nranks, uid, should_abort=None):
+        # two-phase: the object exists before the collective blocks, so a
+        # peer death can abort it from the reader thread (request_abort);
+        # an abort that raced ahead of the assignment is caught by the
+        # check right after it
+        self.comm = self.native.Fence(nranks, rank, self.timeout)
+        if should_abort is not None and should_abort():
+            self.comm.request_abort()
+        self.comm.connect(bytes.fromhex(uid))
+
+    def allreduce(self, epoch, vec):
+        result, us = self.comm.allreduce(list(vec))
+        return list(result), {'allreduce_us': us}
+
+    def request_abort(self):
+        comm = self.comm
+        if comm is not None:
+            comm.request_abort()
+
+    def close(self):
+        comm, self.comm = self.comm, None
+        if comm is not None:
+            try:
+                comm.destroy()   # aborts instead when an abort was requested
+            except Exception:  # pylint: disable=broad-except
+                pass
+
+
+class GlooNodeTransport(object):
+    """One persistent gloo group per generation over a FileStore (CPU)."""
+
+    name = 'gloo'
+
+    def __init__(self, timeout=30.0, root=None):
+        self.timeout = float(timeout)
+        self.root = root or tempfile.gettempdir()
+        self.pg = None
+        self._aborted = False
+
+    def make_uid(self, gen):
+        return os.path.join(self.root, 'kiosk-nodefence-%d-%s' % (
+            gen, uuid.uuid4().hex[:12]))
+
+    def connect(self, gen, rank, nranks, uid, should_abort=None):
+        import datetime
+        import torch.distributed as dist
+        self._aborted = bool(should_abort and should_abort())
+        store = dist.FileStore(uid, nranks)
+        self.pg = dist.ProcessGroupGloo(
+            store, rank, nranks, datetime.timedelta(seconds=self.timeout))
+
+    def allreduce(self, epoch, vec):
+        import torch
+        if self._aborted:
+            raise FenceError('communicator aborted')
+        tensor = torch.tensor(vec, dtype=torch.int64)
+        t0 = time.perf_counter()
+        self.pg.allreduce([tensor]).wait()
+        return tensor.tolist(), {'allreduce_us': (time.perf_counter() - t0)
+                                 * 1e6}
+
+    def request_abort(self):
+        self._aborted = True   # gloo cannot be interrupted: its timeout ends it
+
+    def close(self):
+        self.pg = None
+
+
+class StoreNodeTransport(object):
+    """All-reduce through Redis lists (every rank sums every vector)."""
+
+    name = 'store'
+
+    def __init__(self, redis=None, timeout=30.0):
+        self._redis = redis
+        self.timeout = float(timeout)
+        self.uid = None
+        self.nranks = 0
+        self.rank = 0
+        self._aborted = False
+
+    @property
+    def redis(self):
+        if self._redis is None:
+            from ..redisq import StrictRedis
+            self._redis = StrictRedis(
+                host=os.environ.get('REDIS_HOST', '127.0.0.1'),
+                port=int(os.environ.get('REDIS_PORT', 6379)),
+                decode_responses=True)
+        return self._redis
+
+    def make_uid(self, gen):
+        return '%d-%s' % (gen, uuid.uuid4().hex[:12])
+
+    def connect(self, gen, rank, nranks, uid, should_abort=None):
+        self.uid, self.rank, self.nranks = uid, rank, nranks
+        self._aborted = bool(should_abort and should_abort())
+
+    def allreduce(self, epoch, vec):
+        key = STORE_KEY.format(uid=self.uid, epoch=epoch)
+        t0 = time.perf_counter()
+        self.redis.rpush(key, json.dumps([self.rank, vec]))
+        if self.rank == 0:
+            self.redis.expire(key, 120)
+        deadline = time.monotonic() + self.timeout
+        while True:
+            entries = self.redis.lrange(key, 0, -1)
+            if len(set(json.loads(e)[0] for e in entries)) >= self.nranks:
+                break
+            if self._aborted:
+                raise FenceError('communicator aborted')
+            if time.monotonic() > deadline:
+                raise FenceError('store all-reduce epoch %s timed out (%d/%d)'
+                                 % (epoch, len(entries), self.nranks))
+            time.sleep(0.001)
+        total = [0] * len(vec)
+        seen = set()
+        for entry in entries:
+            rank, values = json.loads(entry)
+            if rank in seen:
+                continue
+            seen.add(rank)
+            total = [a + b for a, b in zip(total, values)]
+        return total, {'allreduce_us': (time.perf_counter() - t0) * 1e6}
+
+    def request_abort(self):
+        self._aborted = True
+
+    def close(self):
+        self.uid = None
+
+
+def choose_node_transport(kind, backend, timeout=60.0):
+    if kind in ('auto', ''):
+        kind = 'rccl' if backend == 'hip' else 'store'
+    if kind == 'rccl':
+        return RcclNodeTransport(timeout)
+    if kind == 'gloo':
+        return GlooNodeTransport(min(timeout, 30.0))
+    if kind == 'store':
+        return StoreNodeTransport(timeout=min(timeout, 30.0))
+    raise ValueError('unknown FENCE transport %r' % kind)
+
+
+# ---------------------------------------------------------------------------
+# per-process agent
+# ---------------------------------------------------------------------------
+class NodeFenceAgent(object):
+    """Lives as long as the process (standby and worker phases alike) and
+    runs node-communicator commands in order on one thread.
+
+    ``idle`` is cleared while a collective is in flight: the serving loop
+    chunks its forward passes (FENCE_YIELD_CHUNK_MS) so the all-reduce
+    kernel is not queued behind a whole key of GEMMs."""
+
+    def __init__(self, slot, transport, channel=None, events=None,
+                 uid_timeout=60.0):
+        self.slot = int(slot)
+        self.transport = transport
+        self.channel = channel
+        self.events = events
+        self.uid_timeout = float(uid_timeout)
+        self.gen = 0          # generation of the connected communicator
+        self.rank = None
+        self.nranks = 0
+        self._uids = {}
+        self._uid_cv = threading.Condition()
+        self._abort_gen = 0   # highest generation the manager aborted
+        self._aborted_epochs = set()
+        self._queue = queue.Queue()
+        self.completed = []
+        self.idle = threading.Event()
+        self.idle.set()
+        self._thread = threading.Thread(target=self._run, name='nodefence',
+                                        daemon=True)
+        self._thread.start()
+
+    # -- reader-thread side ------------------------------------------------
+    def submit(self, message):
+        cmd = message.get('cmd')
+        if cmd == 'comm_uid':
+            with self._uid_cv:
+                self._uids[int(message['gen'])] = message['uid']
+                self._uid_cv.notify_all()
+            return
+        if cmd == 'fence_abort':
+            self._aborted_epochs.add(message.get('seq'))
+            return
+        if cmd == 'comm_abort':
+            gen = int(message.get('gen', 0))
+            with self._uid_cv:
+                self._abort_gen = max(self._abort_gen, gen)
+                self._uid_cv.notify_all()
+            if gen >= self.gen:   # never the comm of a newer generation
+                self.transport.request_abort()
+        self._queue.put(message)
+
+    def _aborted(self, gen):
+        return self._abort_gen >= gen
+
+    # -- agent thread ------------------------------------------------------
+    def _emit(self, ev, **fields):
+        if self.channel is not None:
+            self.channel.emit(ev, **fields)
+
+    def _wait_uid(self, gen):
+        deadline = time.monotonic() + self.uid_timeout
+        with self._uid_cv:
+            while gen not in self._uids:
+                if self._aborted(gen):
+                    raise FenceError('generation %d aborted' % gen)
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    raise FenceError('no communicator id for generation %d'
+                                     % gen)
+                self._uid_cv.wait(min(left, 0.5))
+            return self._uids.pop(gen)
+
+    def _comm_init(self, message):
+        gen, rank = int(message['gen']), int(message['rank'])
+        nranks = int(message['nranks'])
+        self._drop()
+        t0 = time.perf_counter()
+        try:
+            if self._aborted(gen):
+                raise FenceError('generation %d aborted' % gen)
+            if rank == 0:
+                uid = self.transport.make_uid(gen)
+                self._emit('comm_uid', gen=gen, uid=uid)
+            else:
+                uid = self._wait_uid(gen)
+            self.transport.connect(gen, rank, nranks, uid,
+                                   should_abort=lambda: self._aborted(gen))
+        except Exception as err:  # pylint: disable=broad-except
+            logger.warning('communicator generation %d failed: %s', gen, err)
+            self._drop()
+            self._emit('comm_ready', gen=gen, rank=rank, ok=False,
+                       detail=str(err), transport=self.transport.name)
+            return
+        self.gen, self.rank, self.nranks = gen, rank, nranks
+        init_ms = (time.perf_counter() - t0) * 1e3
+        self._emit('comm_ready', gen=gen, rank=rank, ok=True, init_ms=init_ms,
+                   transport=self.transport.name, n=nranks)
+
+    def _drop(self):
+        self.transport.close()
+        self.rank = None
+        self.nranks = 0
+
+    def run_fence(self, message):
+        epoch = int(message['epoch'])
+        gen = int(message['gen'])
+        members = [int(s) for s in message.get('slots', [])]
+        width = node_width(message.get('width', MIN_SLOTS))
+        if self.rank is None or gen != self.gen:
+            raise FenceError('no communicator for generation %d (have %s)'
+                             % (gen, self.gen if self.rank is not None
+                                else 'none'))
+        vec = node_vector(epoch, self.slot, members, width)
+        t0 = time.perf_counter()
+        # node-wide sequence number: epochs are per resource
+        result, info = self.transport.allreduce(message.get('seq', epoch),
+                                                vec)
+        wall_ms = (time.perf_counter() - t0) * 1e3
+        expected = node_expected(epoch, self.nranks, members, width)
+        ok = list(result) == expected
+        report = {'epoch': epoch, 'seq': message.get('seq'), 'gen': gen,
+                  'ok': ok, 'rank': self.rank,
+                  'n': self.nranks, 'transport': self.transport.name,
+                  'wall_ms': wall_ms, 'init_ms': 0.0, 'mode': 'node'}
+        report.update(info)
+        if not ok:
+            report['detail'] = 'got %s expected %s' % (result, expected)
+        return report
+
+    def _run(self):
+        while True:
+            message = self._queue.get()
+            if message is None:
+                return
+            cmd = message.get('cmd')
+            if cmd == 'comm_init':
+                self._comm_init(message)
+                continue
+            if cmd == 'comm_abort':
+                if int(message.get('gen', 0)) >= self.gen:
+                    self._drop()
+                continue
+            if cmd != 'fence':
+                continue
+            epoch = message.get('epoch')
+            if message.get('seq') in self._aborted_epochs:
+                continue
+            self.idle.clear()
+            try:
+                report = self.run_fence(message)
+            except Exception as err:  # pylint: disable=broad-except
+                logger.warning('node fence epoch %s failed: %s', epoch, err)
+                report = {'epoch': epoch, 'seq': message.get('seq'),
+                          'gen': message.get('gen'),
+                          'ok': False, 'detail': str(err), 'rank': self.rank,
+                          'transport': self.transport.name, 'mode': 'node'}
+                self._drop()   # a failed collective leaves no usable comm
+            finally:
+                self.idle.set()
+            self.completed.append(report)
+            if self.events is not None:
+                self.events.emit('fence_rank', slot=self.slot, **report)
+            if report.get('rank') == 0 or not report['ok']:
+                self._emit('fenced', **report)
+
+    def close(self, timeout=5.0):
+        self._queue.put(None)
+        self._thread.join(timeout=timeout)
+        if self._thread.is_alive():
+            return False
+        self._drop()
+        return True

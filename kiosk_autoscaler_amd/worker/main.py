@@ -2,10 +2,19 @@
 
 Two start modes (both spawned by :mod:`kiosk_autoscaler_amd.gpumgr`):
 
-* **standby** (no ``--assign``): import PyTorch-ROCm and the native kernel
-  module, report ``standby`` and block on the command pipe.  No HIP call is
-  made, so the process holds no GPU and may later be pinned to any one.
+* **standby** (``--pin JSON``, no ``--assign``): pinned to its GPU before
+  anything loads, import PyTorch-ROCm and the native kernel module and --
+  with ``WARM_POOL_MODE=device``, the default -- create the HIP context,
+  load every code object and size the LDS ring (``preinit_device``).  Such a
+  standby **holds its GPU** (context + code objects, no weights); the
+  benchmark reports that time as ``standby_gpu_s``.  With
+  ``WARM_POOL_MODE=import`` it stops after the imports and holds no GPU.
+  Report ``standby`` and block on the command pipe.
 * **cold** (``--assign JSON``): the same, but start immediately.
+
+With the node communicator (``node_fence`` in the pin/assignment) the
+process also runs a :class:`~..parallel.nodefence.NodeFenceAgent` for its
+whole life, standby and worker phases alike.
 
 After assignment the process pins itself (``HIP_VISIBLE_DEVICES`` + CPU
 affinity), builds the engine and runs :class:`WorkerRuntime`.  When the
@@ -88,18 +97,25 @@ def main(argv=None):
                               'cpus': early.get('cpus')})
     preload_ns = _preload(backend)
     preinit = {}
+    node = bool((early or {}).get('node_fence')) and os.environ.get(
+        'FENCE', 'auto') not in ('none', 'off', '0')
     if pin and pin.get('preinit') == 'device' and backend == 'hip':
         from ..ops import native
         try:
             mod = native.load()
             preinit = dict(mod.preinit_device(0))
-            if os.environ.get('FENCE', 'auto') in ('auto', 'rccl'):
-                # RCCL's one-time init costs seconds: pay it while idle
+            if not node and os.environ.get('FENCE', 'auto') in ('auto',
+                                                                 'rccl'):
+                # RCCL's one-time init costs seconds: pay it while idle (with
+                # the node communicator its first generation pays it)
                 preinit['rccl_warmup_ms'] = mod.fence_warmup(60.0)
         except Exception as err:  # pylint: disable=broad-except
             channel.emit('error', message='preinit failed: %s' % err)
             return 4
 
+    node_agent = None
+    if node:
+        node_agent = _start_node_agent(channel, backend, early.get('slot', 0))
     assignment = parse_assignment(args.assign) if args.assign else None
     recycles = 0
     max_recycles = int(os.environ.get('WORKER_MAX_RECYCLES', 64))
@@ -113,7 +129,7 @@ def main(argv=None):
             if isinstance(assignment, int):     # pinned to another GPU
                 code = assignment
                 break
-        code, runtime = _serve(assignment, backend, channel)
+        code, runtime = _serve(assignment, backend, channel, node_agent)
         # Recycle: a cleanly drained (or finished job) worker has released
         # its HBM, streams and communicator but keeps its HIP context and
         # loaded code objects -- it goes back to being this GPU's standby,
@@ -122,9 +138,11 @@ def main(argv=None):
                 recycles < max_recycles):
             break
         recycles += 1
-        gc.collect()
+        # the engine's HBM is already freed: report first, collect after
+        # (the collection runs while the process waits as a standby)
         channel.emit('recycled', code=code, keys_done=runtime.keys_done,
                      recycles=recycles)
+        gc.collect()
         pin = {'gpu': assignment.get('gpu'), 'slot': assignment.get('slot'),
                'cpus': assignment.get('cpus')}
         assignment = None
@@ -134,6 +152,22 @@ def main(argv=None):
     sys.stdout.flush()
     sys.stderr.flush()
     os._exit(code)
+
+
+def _start_node_agent(channel, backend, slot):
+    """The process-lifetime member of the node communicator: it serves
+    ``comm_*`` / ``fence`` commands from the pipe's reader thread in the
+    standby and the worker phases alike."""
+    from ..parallel.nodefence import (NODE_COMMANDS, NodeFenceAgent,
+                                      choose_node_transport)
+    transport = choose_node_transport(os.environ.get('FENCE', 'auto'),
+                                      backend)
+    agent = NodeFenceAgent(slot, transport, channel=channel)
+    for cmd in NODE_COMMANDS:
+        channel.direct[cmd] = agent.submit
+    channel.start_reader()
+    channel.emit('node_agent', slot=slot, transport=transport.name)
+    return agent
 
 
 def _standalone(backend):
@@ -189,7 +223,7 @@ def _wait_for_assignment(channel, pin, preload_ns, backend, preinit):
     return message
 
 
-def _serve(assignment, backend, channel):
+def _serve(assignment, backend, channel, node_agent=None):
     """Run one assignment to completion: ``(exit code, runtime)``."""
     from .runtime import WorkerConfig, WorkerRuntime, apply_assignment_env
     apply_assignment_env(assignment)
@@ -220,8 +254,10 @@ def _serve(assignment, backend, channel):
         faults = FaultPlan.from_env(redis=redis_factory(),
                                     owner=config.worker_id)
     runtime = WorkerRuntime(config, engine_factory, channel, redis_factory,
-                            fence_factory=_build_fence_factory(config),
-                            event_log=events, faults=faults)
+                            fence_factory=(None if node_agent is not None
+                                           else _build_fence_factory(config)),
+                            event_log=events, faults=faults,
+                            node_agent=node_agent)
     code = runtime.run()
     if events is not None:
         events.emit('worker_exit_self', worker=config.worker_id,

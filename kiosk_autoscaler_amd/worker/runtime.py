@@ -68,7 +68,8 @@ class WorkerConfig(object):
         # forward chunk size (ms) while a fence epoch is in flight (0 = off)
         self.fence_chunk_ms = _env_float(env, 'FENCE_YIELD_CHUNK_MS', 2.0)
         # how long an idle worker blocks in BLMOVE: bounds drain latency
-        self.poll_block = _env_float(env, 'POLL_BLOCK_S', 0.1)
+        # (the drain command waits for it: it bounds scale-down latency)
+        self.poll_block = _env_float(env, 'POLL_BLOCK_S', 0.02)
         self.job_idle_exit = _env_float(env, 'JOB_IDLE_EXIT_S', 1.0)
         self.mock_work_ms = _env_float(env, 'MOCK_WORK_MS', 0.0)
         self.record_events = env.get('WORKER_EVENTS', '1') not in ('0', '')
@@ -126,7 +127,8 @@ class WorkerRuntime(object):
     """Runs one assigned worker to completion.  Returns the exit code."""
 
     def __init__(self, config, engine_factory, channel, redis_factory,
-                 fence_factory=None, event_log=None, faults=None):
+                 fence_factory=None, event_log=None, faults=None,
+                 node_agent=None):
         self.config = config
         self.faults = faults
         self.engine_factory = engine_factory
@@ -136,6 +138,8 @@ class WorkerRuntime(object):
         self.events = event_log
         self.engine = None
         self.fence_agent = None
+        # process-lifetime agent of the node communicator (not ours to close)
+        self.node_agent = node_agent
         self.draining = False
         # back to the standby pool after a clean finish (manager's call:
         # set by the assignment, overridden by the drain command)
@@ -191,7 +195,9 @@ class WorkerRuntime(object):
         self.channel.emit('ready', t=t_ready, stages=self.stages)
         self._emit_event('worker_ready', gpu=cfg.slot, t_ns=t_ready,
                          stages=self.stages)
-        if self.fence_factory is not None:
+        if self.node_agent is not None:
+            self.fence_agent = self.node_agent
+        elif self.fence_factory is not None:
             self.fence_agent = self.fence_factory(self)
             direct = getattr(self.channel, 'direct', None)
             if direct is not None and self.fence_agent is not None:
@@ -243,10 +249,12 @@ class WorkerRuntime(object):
                     self._process(consumer, items)
                 idle_since = time.monotonic()
         finally:
-            for cmd in ('fence', 'fence_abort'):
-                getattr(self.channel, 'direct', {}).pop(cmd, None)
-            if self.fence_agent is not None and not self.fence_agent.close():
-                self.recycle = False    # a collective may still be running
+            if self.node_agent is None:
+                for cmd in ('fence', 'fence_abort'):
+                    getattr(self.channel, 'direct', {}).pop(cmd, None)
+                if self.fence_agent is not None and \
+                        not self.fence_agent.close():
+                    self.recycle = False  # a collective may still be running
             if self.engine is not None:
                 self.engine.close()
         return 0

@@ -164,6 +164,50 @@ def test_fence_agent_rccl_transport(mod):
         agent.close()
 
 
+def test_node_transport_persistent_world_size_one(mod):
+    """The persistent node communicator on RCCL: two-phase connect, then
+    many 72-B fences on the same communicator (no re-init per epoch)."""
+    import time
+    from kiosk_autoscaler_amd.parallel import nodefence
+    t = nodefence.RcclNodeTransport(timeout=30.0, native=mod)
+    uid = t.make_uid(1)
+    t0 = time.perf_counter()
+    t.connect(1, 0, 1, uid, should_abort=lambda: False)
+    init_ms = (time.perf_counter() - t0) * 1e3
+    try:
+        lat = []
+        for epoch in range(1, 201):
+            vec = nodefence.node_vector(epoch, 0, [0] if epoch % 2 else [], 8)
+            out, info = t.allreduce(epoch, vec)
+            assert out == nodefence.node_expected(
+                epoch, 1, [0] if epoch % 2 else [], 8)
+            lat.append(info['allreduce_us'])
+        lat.sort()
+        median = lat[len(lat) // 2]
+        print('node comm init %.1f ms, 72-B all-reduce median %.1f us'
+              % (init_ms, median))
+        assert median < 1000.0          # a fence is sub-millisecond
+        assert not t.comm.abort_requested
+    finally:
+        t.close()
+    assert t.comm is None
+
+
+def test_fence_request_abort_then_destroy(mod):
+    """request_abort() from another thread, then destroy(): the owner
+    aborts instead of finalizing (no use-after-free)."""
+    fence = mod.Fence(1, 0, 30.0)
+    fence.connect(mod.fence_unique_id())
+    out, _ = fence.allreduce([1, 1, 0, 0, 0, 0, 0, 0, 0])
+    assert out[0] == 1
+    fence.request_abort()
+    assert fence.abort_requested
+    fence.destroy()
+    fence.destroy()                      # idempotent
+    with pytest.raises(RuntimeError):
+        fence.allreduce([1])
+
+
 def test_fence_warmup_and_preinit(mod):
     ms = mod.fence_warmup(60.0)
     assert ms > 0

@@ -1,0 +1,362 @@
+"""Persistent node-wide membership communicator (N4, round-2 design).
+
+Unit level: the agent protocol against a fake native module that records
+the order of RCCL calls (connect / allreduce / abort / destroy), the
+generation-aware abort, the vectors.  Integration level (slow, CPU): eight
+mock workers with ``QUEUES=predict,track`` (BASELINE configs 3-4 shape)
+driven through repeated 0 <-> 8 churn and a kill -9, checking the
+reference's multi-queue decisions, the fenced set published in Redis, the
+requeue, GPU-idle accounting and -- the point of the design -- that scale
+events never rebuild the communicator (one generation at boot, one per
+process death)."""
+import json
+import os
+import queue
+import signal
+import threading
+import time
+
+import pytest
+
+from kiosk_autoscaler_amd.parallel import nodefence
+from kiosk_autoscaler_amd.parallel.nodefence import (NodeFenceAgent,
+                                                     node_expected,
+                                                     node_vector)
+
+
+def wait_for(predicate, timeout=30.0, step=0.02):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        value = predicate()
+        if value:
+            return value
+        time.sleep(step)
+    raise AssertionError('condition not met within %.1fs' % timeout)
+
+
+class _Channel(object):
+    def __init__(self):
+        self.out = queue.Queue()
+
+    def emit(self, ev, **fields):
+        fields['ev'] = ev
+        self.out.put(fields)
+
+    def next(self, ev, timeout=10.0):
+        deadline = time.monotonic() + timeout
+        while True:
+            msg = self.out.get(timeout=max(0.01, deadline - time.monotonic()))
+            if msg['ev'] == ev:
+                return msg
+
+
+class _FakeNative(object):
+    """Records the RCCL-facing call order of RcclNodeTransport."""
+
+    def __init__(self, nranks_results=None):
+        self.calls = []
+        self.lock = threading.Lock()
+        self.peers = nranks_results   # list of other ranks' vectors
+
+    def log(self, *what):
+        with self.lock:
+            self.calls.append(what)
+
+    def fence_unique_id(self):
+        self.log('unique_id')
+        return b'\x07' * 128
+
+    def Fence(self, nranks, rank, timeout):
+        native = self
+
+        class Comm(object):
+            def __init__(self):
+                self.abort_requested = False
+                self.block = threading.Event()
+
+            def connect(self, uid):
+                native.log('connect', rank, nranks, len(uid))
+                if self.abort_requested:
+                    raise RuntimeError('ncclCommInitRank aborted on request')
+
+            def allreduce(self, vec):
+                native.log('allreduce', list(vec))
+                if native.peers == 'hang':
+                    while not self.abort_requested:
+                        time.sleep(0.001)
+                    raise RuntimeError('fence all-reduce aborted on request')
+                total = list(vec)
+                for other in native.peers or []:
+                    total = [a + b for a, b in zip(total, other)]
+                return total, 12.5
+
+            def request_abort(self):
+                native.log('request_abort')
+                self.abort_requested = True
+
+            def destroy(self):
+                native.log('destroy', self.abort_requested)
+        native.log('new', nranks, rank)
+        return Comm()
+
+
+def test_node_vectors():
+    assert node_vector(4, 2, [0, 2], 8) == [4, 0, 0, 1, 0, 0, 0, 0, 0]
+    assert node_vector(4, 1, [0, 2], 8) == [4] + [0] * 8   # non-member: 0s
+    assert node_expected(4, 3, [0, 2], 8) == [12, 1, 0, 1, 0, 0, 0, 0, 0]
+    assert len(node_vector(1, 0, [0], 8)) * 8 == 72
+
+
+def test_agent_rank0_publishes_uid_then_fences():
+    native = _FakeNative(nranks_results=[[3, 0, 1] + [0] * 6])
+    chan = _Channel()
+    agent = NodeFenceAgent(0, nodefence.RcclNodeTransport(native=native),
+                           channel=chan)
+    agent.submit({'cmd': 'comm_init', 'gen': 1, 'rank': 0, 'nranks': 2})
+    uid = chan.next('comm_uid')
+    assert uid['gen'] == 1 and bytes.fromhex(uid['uid']) == b'\x07' * 128
+    ready = chan.next('comm_ready')
+    assert ready['ok'] and ready['n'] == 2
+    # members: slots 0 and 1; this is slot 0, the peer contributes slot 1
+    agent.submit({'cmd': 'fence', 'epoch': 3, 'seq': 1, 'gen': 1,
+                  'slots': [0, 1], 'width': 8})
+    fenced = chan.next('fenced')
+    assert fenced['ok'] and fenced['mode'] == 'node' and fenced['n'] == 2
+    assert fenced['allreduce_us'] == 12.5 and fenced['init_ms'] == 0.0
+    names = [c[0] for c in native.calls]
+    assert names == ['unique_id', 'new', 'connect', 'allreduce']
+    # a second epoch reuses the communicator: no new/connect
+    native.peers = [[4, 0, 0] + [0] * 6]
+    agent.submit({'cmd': 'fence', 'epoch': 4, 'seq': 2, 'gen': 1,
+                  'slots': [0], 'width': 8})
+    assert chan.next('fenced')['ok']
+    assert [c[0] for c in native.calls].count('connect') == 1
+    assert agent.close()
+    assert native.calls[-1] == ('destroy', False)
+
+
+def test_agent_non_root_waits_for_uid_and_aborts_cleanly():
+    native = _FakeNative()
+    chan = _Channel()
+    agent = NodeFenceAgent(1, nodefence.RcclNodeTransport(native=native),
+                           channel=chan, uid_timeout=5.0)
+    agent.submit({'cmd': 'comm_init', 'gen': 2, 'rank': 1, 'nranks': 2})
+    time.sleep(0.05)
+    assert not any(c[0] == 'connect' for c in native.calls)
+    agent.submit({'cmd': 'comm_uid', 'gen': 2, 'uid': ('ab' * 128)})
+    assert chan.next('comm_ready')['ok']
+    # a peer dies mid-collective: the blocked all-reduce is aborted from
+    # the reader thread, never destroyed under it
+    native.peers = 'hang'
+    agent.submit({'cmd': 'fence', 'epoch': 1, 'seq': 1, 'gen': 2,
+                  'slots': [1], 'width': 8})
+    wait_for(lambda: any(c[0] == 'allreduce' for c in native.calls))
+    assert not agent.idle.is_set()
+    agent.submit({'cmd': 'comm_abort', 'gen': 2})
+    failed = chan.next('fenced')
+    assert not failed['ok'] and 'aborted' in failed['detail']
+    names = [c[0] for c in native.calls]
+    assert names.index('request_abort') < names.index('destroy')
+    assert ('destroy', True) in native.calls    # abort path, no finalize
+    assert agent.idle.is_set() and agent.rank is None
+    assert agent.close()
+
+
+def test_abort_of_a_generation_cancels_its_pending_init():
+    native = _FakeNative()
+    chan = _Channel()
+    agent = NodeFenceAgent(1, nodefence.RcclNodeTransport(native=native),
+                           channel=chan, uid_timeout=10.0)
+    agent.submit({'cmd': 'comm_init', 'gen': 5, 'rank': 1, 'nranks': 3})
+    agent.submit({'cmd': 'comm_abort', 'gen': 5})   # before the uid came
+    ready = chan.next('comm_ready', timeout=5.0)
+    assert not ready['ok'] and 'aborted' in ready['detail']
+    assert not any(c[0] == 'connect' for c in native.calls)
+    # the next generation is unaffected by the old abort
+    agent.submit({'cmd': 'comm_init', 'gen': 6, 'rank': 1, 'nranks': 3})
+    agent.submit({'cmd': 'comm_uid', 'gen': 6, 'uid': 'cd' * 128})
+    assert chan.next('comm_ready')['ok'] and agent.gen == 6
+    assert agent.close()
+
+
+def test_fence_on_a_stale_generation_fails():
+    native = _FakeNative()
+    chan = _Channel()
+    agent = NodeFenceAgent(0, nodefence.RcclNodeTransport(native=native),
+                           channel=chan)
+    agent.submit({'cmd': 'fence', 'epoch': 1, 'seq': 1, 'gen': 9,
+                  'slots': [0], 'width': 8})
+    report = chan.next('fenced')
+    assert not report['ok'] and 'no communicator' in report['detail']
+    assert agent.close()
+
+
+def test_store_node_transport_three_ranks(redis_client):
+    transports = [nodefence.StoreNodeTransport(redis=redis_client, timeout=5)
+                  for _ in range(3)]
+    for rank, t in enumerate(transports):
+        t.connect(1, rank, 3, 'u1')
+    out = [None] * 3
+
+    def run(rank):
+        vec = node_vector(7, rank, [0, 2], 8)
+        out[rank] = transports[rank].allreduce(1, vec)[0]
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(3)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(10)
+    assert all(o == node_expected(7, 3, [0, 2], 8) for o in out)
+
+
+def _gloo_rank(rank, path, results):
+    t = nodefence.GlooNodeTransport(timeout=20)
+    t.connect(1, rank, 2, path)
+    for epoch in (1, 2, 3):          # one group, many fences
+        vec = node_vector(epoch, rank, [0, 1] if epoch != 2 else [1], 8)
+        results.put((rank, epoch, t.allreduce(epoch, vec)[0]))
+    t.close()
+
+
+@pytest.mark.slow
+def test_gloo_node_transport_two_processes(tmp_path):
+    import multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    results = ctx.Queue()
+    path = str(tmp_path / 'store')
+    procs = [ctx.Process(target=_gloo_rank, args=(r, path, results))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [results.get(timeout=120) for _ in range(6)]
+    for p in procs:
+        p.join(30)
+    for rank, epoch, vec in got:
+        members = [0, 1] if epoch != 2 else [1]
+        assert vec == node_expected(epoch, 2, members, 8)
+
+
+# ---------------------------------------------------------------------------
+# eight mock workers, churn and a death (configs 3-4 shape, CPU)
+# ---------------------------------------------------------------------------
+def _active(client):
+    text = client.get('kiosk:active:default:worker')
+    return json.loads(text) if text else None
+
+
+def _ready_ids(manager):
+    workers = manager.status()['resources'][0]['workers']
+    return sorted((w for w in workers if w['state'] == 'ready'),
+                  key=lambda w: w['gpu'])
+
+
+def _converged(manager, client):
+    ready = [w['id'] for w in _ready_ids(manager)]
+    active = _active(client)
+    return active is not None and active['members'] == ready and \
+        manager.node.inflight is None
+
+
+@pytest.mark.slow
+def test_eight_workers_churn_and_death(resp_server):
+    from kiosk_autoscaler_amd import Autoscaler, gpumgr, policy
+    from kiosk_autoscaler_amd.bench import metrics
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import RedisClient, StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict,track', 'RESOURCE_NAME': 'worker',
+           'MAX_PODS': '8', 'KEYS_PER_POD': '1', 'WORKER_BACKEND': 'cpu',
+           'WARM_POOL': '8', 'FENCE': 'store', 'INTERVAL': '1',
+           'REDIS_INTERVAL': '0', 'EVENT_LOG': 'redis'}
+    s = Settings(Config(environ=env, use_files=False))
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    events = EventLog(source='test')
+    events.keep = True
+    manager = gpumgr.build_manager(s, redis_client=client, events=events,
+                                   extra_env={'MOCK_WORK_MS': '400'}).start()
+    proxy = RedisClient(host=resp_server.host, port=resp_server.port,
+                        backoff=0)
+    scaler = Autoscaler(proxy, s.QUEUES, actuator=manager)
+    counter = [0]
+
+    def enqueue(n_predict, n_track):
+        items = []
+        for queue_name, n in (('predict', n_predict), ('track', n_track)):
+            for _ in range(n):
+                counter[0] += 1
+                item = '%s:job%d' % (queue_name, counter[0])
+                client.hset(item, mapping={'status': 'new', 'rows': 8})
+                client.lpush(queue_name, item)
+                items.append(item)
+        return items
+
+    def tick():
+        return scaler.scale('default', 'deployment', 'worker', 0, 8, 1)
+
+    def all_done(items):
+        return all(client.hget(i, 'status') == 'done' for i in items)
+
+    try:
+        assert manager.node is not None
+        wait_for(lambda: manager.node.ready, timeout=60)
+        assert len(manager.node.members) == 8
+        # {predict:3, track:2} from zero -> 5
+        batch = enqueue(3, 2)
+        assert tick() == 5
+        wait_for(lambda: len(_ready_ids(manager)) == 5)
+        # multi-queue inflation: {predict:1, track:1} at current 5 -> each
+        # queue's clip substitutes current -> 10 -> max clamp 8
+        wait_for(lambda: all_done(batch), timeout=30)
+        batch = enqueue(1, 1)
+        keys = {'predict': 1, 'track': 1}
+        expect = policy.decide(keys, 0, 8, 1, 5, policy='reference')
+        assert expect == 8 and tick() == 8
+        wait_for(lambda: len(_ready_ids(manager)) == 8, timeout=30)
+        wait_for(lambda: _converged(manager, client), timeout=30)
+        wait_for(lambda: all_done(batch), timeout=30)
+        # 8 -> 0 and back, twice
+        for _ in range(2):
+            assert tick() == 0
+            wait_for(lambda: not manager.status()['resources'][0]['workers'],
+                     timeout=30)
+            wait_for(lambda: _active(client)['members'] == [], timeout=30)
+            batch = enqueue(4, 4)
+            assert tick() == 8
+            wait_for(lambda: _converged(manager, client) and
+                     len(_ready_ids(manager)) == 8, timeout=30)
+            wait_for(lambda: all_done(batch), timeout=30)
+        assert manager.node.generations == 1    # churn never re-inits
+        # kill -9 a busy worker: its item is requeued, the slot's new
+        # process joins a second generation, the set converges again
+        batch = enqueue(8, 8)
+        victim = wait_for(lambda: [w for w in _ready_ids(manager)
+                                   if client.exists('processing-%s:%s' % (
+                                       'predict', w['id'])) or
+                                   client.exists('processing-%s:%s' % (
+                                       'track', w['id']))], timeout=10)[0]
+        os.kill(victim['pid'], signal.SIGKILL)
+        wait_for(lambda: any(e['ev'] == 'requeue' for e in events.records),
+                 timeout=20)
+        wait_for(lambda: manager.node.generations == 2, timeout=60)
+        wait_for(lambda: all_done(batch), timeout=60)
+        wait_for(lambda: _converged(manager, client) and
+                 len(_ready_ids(manager)) == 8, timeout=30)
+        assert victim['id'] not in _active(client)['members']
+        assert tick() == 0
+        wait_for(lambda: _active(client)['members'] == [], timeout=30)
+    finally:
+        manager.stop(timeout=15)
+    from kiosk_autoscaler_amd.utils.events import drain_redis
+    records = events.records + drain_redis(client)   # + workers' events
+    done = [e for e in records if e['ev'] == 'fence_done']
+    assert done and all(e['n'] == 8 and e['mode'] == 'node' for e in done)
+    assert sum(1 for e in records if e['ev'] == 'node_comm_ready') == 2
+    breaks = [e for e in records if e['ev'] == 'node_comm_break']
+    assert len(breaks) == 1 and not breaks[0]['failed']
+    idle, alive, busy = metrics.gpu_idle(records, 0, time.monotonic_ns())
+    assert 0 < busy < alive and 0 < idle < 100
+    stats = metrics.fence_stats(records)
+    assert stats['fence_max_ranks'] == 8
+    assert stats['node_comm_generations'] == 2
