@@ -413,25 +413,31 @@ void Server::register_commands() {
     if (d.sorted_version != d.version) {
       d.sorted.clear();
       d.sorted.reserve(d.keys.size());
-      for (auto& kv : d.keys) d.sorted.push_back(kv.first);
+      for (auto& kv : d.keys) d.sorted.emplace_back(scan_hash(kv.first), kv.first);
       std::sort(d.sorted.begin(), d.sorted.end());
       d.sorted_version = d.version;
     }
     // alive() below may expire keys (bumping the version) but only SCAN
     // rebuilds `sorted`, so this reference stays valid for the call
-    const std::vector<std::string>& keys = d.sorted;
+    const auto& keys = d.sorted;
     static const char* names[] = {"string", "list", "hash", "set"};
     std::vector<std::string> out;
-    size_t end = std::min(keys.size(), static_cast<size_t>(cursor + count));
-    for (size_t i = static_cast<size_t>(cursor); i < end; ++i) {
-      const std::string& k = keys[i];
+    size_t i = std::lower_bound(keys.begin(), keys.end(),
+                                std::make_pair(static_cast<uint64_t>(cursor),
+                                               std::string())) - keys.begin();
+    size_t end = std::min(keys.size(), i + static_cast<size_t>(count));
+    // never split keys of one hash value across pages: the next cursor is
+    // a hash, so they would be returned twice
+    while (end < keys.size() && end > i && keys[end].first == keys[end - 1].first) ++end;
+    for (; i < end; ++i) {
+      const std::string& k = keys[i].second;
       if (!alive(d, k)) continue;
       if (!match.empty() && !glob_match(match.data(), match.size(), k.data(), k.size())) continue;
       if (!type.empty() && type != names[d.keys[k].type]) continue;
       out.push_back(k);
     }
     r.array(2);
-    r.bulk(end >= keys.size() ? "0" : std::to_string(end));
+    r.bulk(end >= keys.size() ? "0" : std::to_string(keys[end].first));
     r.array(out.size());
     for (auto& k : out) r.bulk(k);
   };

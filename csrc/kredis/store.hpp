@@ -30,11 +30,14 @@ struct Value {
 struct Db {
   std::unordered_map<std::string, Value> keys;
   std::unordered_map<std::string, int64_t> expires;   // monotonic ms
-  // SCAN walks the keys in sorted order; the sorted copy is rebuilt only
-  // when the key set changed (version bumps on every insert / removal)
+  // SCAN walks the keys in (hash, key) order and its cursor is a position
+  // in *hash space*, not an index: deleting or adding keys between pages
+  // cannot shift a key that was present all along past the cursor (Redis's
+  // guarantee).  The ordered copy is rebuilt only when the key set changed
+  // (version bumps on every insert / removal).
   uint64_t version = 0;
   uint64_t sorted_version = ~0ull;
-  std::vector<std::string> sorted;
+  std::vector<std::pair<uint64_t, std::string>> sorted;
 };
 
 // RESP reply builder.
@@ -60,6 +63,17 @@ class Reply {
 };
 
 bool glob_match(const char* pat, size_t plen, const char* str, size_t slen);
+
+// SCAN position of a key: 64-bit FNV-1a folded into [1, 2^63) (cursor 0
+// is reserved for "start" / "done").
+inline uint64_t scan_hash(const std::string& key) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char ch : key) {
+    h ^= ch;
+    h *= 1099511628211ull;
+  }
+  return (h >> 1) | 1ull;
+}
 
 int64_t now_ms();
 

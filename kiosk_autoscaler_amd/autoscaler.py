@@ -56,6 +56,9 @@ class Autoscaler(object):
                  tally='reference'):
         self.redis_keys = {q: 0 for q in queues.split(queue_delim)}
         self.in_progress = {q: 0 for q in self.redis_keys}
+        # distinct workers holding processing keys (a batched worker holds
+        # one key per slot: processing-q:<id>, processing-q:<id>.1, ...)
+        self.busy_workers = set()
         self.redis_client = redis_client
         self.logger = logging.getLogger(str(self.__class__.__name__))
         self.managed_resource_types = {'deployment', 'job'}
@@ -78,6 +81,7 @@ class Autoscaler(object):
 
         Reference: ``autoscaler/autoscaler.py:60-77``."""
         start = self._clock()
+        busy = set()
         for queue in self.redis_keys:
             self.logger.debug('Tallying items in queue `%s`.', queue)
             pattern = 'processing-{}:*'.format(queue)
@@ -86,12 +90,15 @@ class Autoscaler(object):
                 counted = self._tally_atomic(queue, pattern)
             if counted is None:
                 waiting = self.redis_client.llen(queue)
-                running = sum(1 for _ in self.redis_client.scan_iter(
-                    match=pattern, count=1000))
+                keys = list(self.redis_client.scan_iter(match=pattern,
+                                                        count=1000))
             else:
-                waiting, running = counted
+                waiting, keys = counted
+            running = len(keys)
+            busy.update(k.split(':', 1)[1].split('.', 1)[0] for k in keys)
             self.in_progress[queue] = running
             self.redis_keys[queue] = waiting + running
+        self.busy_workers = busy
         self.logger.debug('Finished tallying redis keys in %s seconds.',
                           self._clock() - start)
         self.logger.info('In-progress or new redis keys: %s', self.redis_keys)
@@ -111,7 +118,7 @@ class Autoscaler(object):
             self.logger.warning('atomic tally of `%s` failed (%s); using '
                                 'LLEN + SCAN', queue, err)
             return None
-        return int(waiting), len(keys)
+        return int(waiting), list(keys)
 
     # -- C7-C9: actuator access ------------------------------------------------
     def get_actuator(self):
@@ -244,7 +251,7 @@ class Autoscaler(object):
                                        current_pods)
         desired = policies.decide(
             self.redis_keys, min_pods, max_pods, keys_per_pod, current_pods,
-            policy=self.policy, busy=sum(self.in_progress.values()))
+            policy=self.policy, busy=len(self.busy_workers))
         if desired < current_pods and self.scale_down_delay > 0:
             now = self._clock()
             if self._lower_since is None:

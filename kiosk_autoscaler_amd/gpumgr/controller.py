@@ -35,6 +35,7 @@ import itertools
 import json
 import logging
 import os
+import re
 import select
 import subprocess
 import sys
@@ -356,14 +357,18 @@ class GpuManager(object):
         if self.redis is None:
             return 0
         moved = 0
-        live = set(resource.workers)
+        # exact id shape <name>-g<slot>-<instance>-<seq>: a prefix match
+        # would also take the live items of a resource named '<name>-g2'
+        # sharing the queue (shared-daemon mode)
+        ours = re.compile(r'^%s-g\d+-[0-9a-f]+-\d+$' % re.escape(resource.name))
+        live = set(wid for r in self.resources.values() for wid in r.workers)
         for queue in resource.template.queues:
             pattern = 'processing-%s:%s-g*' % (queue, resource.name)
             try:
                 for key in list(self.redis.scan_iter(match=pattern,
                                                      count=1000)):
                     wid = key.split(':', 1)[1].split('.', 1)[0]
-                    if wid in live:
+                    if wid in live or not ours.match(wid):
                         continue
                     while self.redis.rpoplpush(key, queue) is not None:
                         moved += 1

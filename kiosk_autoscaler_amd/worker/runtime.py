@@ -39,6 +39,15 @@ def _env_float(env, name, default):
         return default
 
 
+# per-job bounds (a job hash is untrusted input)
+MAX_PASSES = 10000
+MAX_SERVICE_MS = 600000
+
+
+class JobError(ValueError):
+    """A job whose parameters cannot be served; it is marked failed."""
+
+
 class WorkerConfig(object):
     def __init__(self, env, assignment):
         template = assignment.get('template', {})
@@ -259,7 +268,18 @@ class WorkerRuntime(object):
                 self.engine.close()
         return 0
 
+    def max_rows(self):
+        """Rows one forward can take (the engine's preallocated capacity)."""
+        engine = getattr(self.engine, 'engine', None)
+        limit = getattr(engine, 'max_rows', None)
+        if limit is None:
+            limit = max(self.config.rows * self.config.batch, 256)
+        return int(limit)
+
     def _job_params(self, item):
+        """Inference parameters of one job hash.  Raises :class:`JobError`
+        for values no engine call could honour (a poison job must fail on
+        its own, not crash every worker that picks it up)."""
         params = {'rows': self.config.rows, 'passes': self.config.passes,
                   'seed': self.config.seed, 'service_ms': 0}
         try:
@@ -271,18 +291,60 @@ class WorkerRuntime(object):
                 try:
                     params[name] = int(fields[name])
                 except ValueError:
-                    pass
+                    raise JobError('%s=%r is not an integer' % (
+                        name, fields[name]))
+        limit = self.max_rows()
+        if not 1 <= params['rows'] <= limit:
+            raise JobError('rows=%d outside [1, %d]' % (params['rows'], limit))
+        if not 1 <= params['passes'] <= MAX_PASSES:
+            raise JobError('passes=%d outside [1, %d]' % (params['passes'],
+                                                          MAX_PASSES))
+        if not 0 <= params['service_ms'] <= MAX_SERVICE_MS:
+            raise JobError('service_ms=%d outside [0, %d]' % (
+                params['service_ms'], MAX_SERVICE_MS))
         return params, fields
+
+    def _fail(self, consumer, queue, item, pkey, reason, fields=True):
+        """Mark a job failed and release its processing key (no requeue)."""
+        logger.warning('job %s failed: %s', item, reason)
+        try:
+            if fields:
+                self.redis.hset(item, mapping={
+                    'status': 'failed', 'reason': str(reason)[:500],
+                    'worker': self.config.worker_id})
+        except redis_errors.ResponseError:
+            pass   # not a hash key: nothing to annotate
+        consumer.complete(pkey)
+        self._emit_event('key_failed', item=item, queue=queue,
+                         reason=str(reason)[:200])
 
     def _process(self, consumer, items):
         cfg = self.config
         t_start = time.monotonic_ns()
         jobs = []
         for queue, item, pkey in items:
-            params, fields = self._job_params(item)
+            try:
+                params, fields = self._job_params(item)
+            except JobError as err:
+                self._fail(consumer, queue, item, pkey, err)
+                continue
             jobs.append((queue, item, pkey, params, fields))
             self._emit_event('key_start', item=item, queue=queue, t_ns=t_start,
                              gpu=cfg.slot)
+        # a batch whose rows exceed the engine's capacity runs in groups
+        limit = self.max_rows()
+        group, rows = [], 0
+        for job in jobs:
+            if group and rows + job[3]['rows'] > limit:
+                self._run_group(consumer, group, t_start)
+                group, rows, t_start = [], 0, time.monotonic_ns()
+            group.append(job)
+            rows += job[3]['rows']
+        if group:
+            self._run_group(consumer, group, t_start)
+
+    def _run_group(self, consumer, jobs, t_start):
+        cfg = self.config
         if self.faults:
             self.faults.before_key(self.keys_done + 1, self.engine,
                                    self.redis)
@@ -297,10 +359,19 @@ class WorkerRuntime(object):
                                                  cfg.fence_chunk_ms > 0):
                 pause = (self.fence_agent.idle, cfg.fence_yield_ms,
                          cfg.fence_chunk_ms)
-            result = self.engine.forward_for(rows, service_ms,
-                                             jobs[0][3]['seed'], pause=pause)
+            call = lambda: self.engine.forward_for(  # noqa: E731
+                rows, service_ms, jobs[0][3]['seed'], pause=pause)
         else:
-            result = self.engine.forward(rows, passes, jobs[0][3]['seed'])
+            call = lambda: self.engine.forward(  # noqa: E731
+                rows, passes, jobs[0][3]['seed'])
+        try:
+            result = call()
+        except (ValueError, TypeError) as err:
+            # the engine rejected the arguments (std::invalid_argument):
+            # these jobs fail, the worker and its device are fine
+            for queue, item, pkey, _, fields in jobs:
+                self._fail(consumer, queue, item, pkey, err, bool(fields))
+            return
         t_done = time.monotonic_ns()
         with trace_range('kiosk.complete'):
             self._complete(consumer, jobs, result, t_start, t_done)

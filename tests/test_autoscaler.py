@@ -188,6 +188,26 @@ def test_strict_policy_with_hysteresis(redis_client):
     assert scaler.scale('ns', 'deployment', 'w', 0, 8, 1) == 1  # applied
 
 
+@pytest.mark.parametrize('tally', ['reference', 'atomic'])
+def test_strict_busy_floor_counts_workers_not_keys(redis_client, tally):
+    """A batched (job) worker holds one processing key per slot: the strict
+    floor is the number of busy *workers* (ADVICE r1 low), 1 here, not 4."""
+    scaler = make(redis_client, queues='predict,track', policy='strict',
+                  tally=tally)
+    scaler.actuator.list_namespaced_job = lambda ns: ResourceList(
+        items=[ResourceView(kind='job', metadata=Metadata(name='w'),
+                            spec=Spec(parallelism=3),
+                            status=Status(available_replicas=3))])
+    for suffix in ('', '.1', '.2'):
+        redis_client.rpush('processing-predict:w-g0-ab-1' + suffix, 'k')
+    redis_client.rpush('processing-track:w-g0-ab-1.3', 'k')
+    scaler.tally_queues()
+    assert scaler.in_progress == {'predict': 3, 'track': 1}
+    assert scaler.busy_workers == {'w-g0-ab-1'}
+    # 4 keys, kpp 4 -> ceil 1; the floor is one busy worker, not 4 keys
+    assert scaler.scale('ns', 'job', 'w', 0, 8, 4) == 1
+
+
 def test_atomic_tally_matches_and_is_consistent(redis_client):
     """TALLY_MODE=atomic: LLEN + KEYS in one MULTI/EXEC.  A consumer that
     keeps moving items between the queue and processing keys never makes

@@ -182,15 +182,21 @@ def test_state_persist_restore_and_orphans():
     assert state['declared'] == '2' and 0 < redis.ttl(
         'kiosk:gpumgr:ns:deployment:w') <= 3600
     # a dead manager left in-flight items behind
-    redis.rpush('processing-q:w-g0-3', 'job-a')
-    redis.rpush('processing-q:w-g1-4.1', 'job-b')
-    redis.rpush('processing-q:other-g0-1', 'not-ours')
+    redis.rpush('processing-q:w-g0-1f2e3-3', 'job-a')
+    redis.rpush('processing-q:w-g1-1f2e3-4.1', 'job-b')
+    redis.rpush('processing-q:other-g0-1f2e3-1', 'not-ours')
+    # a live worker of resource 'w-g2' sharing the queue:
+    # the 'w-g*' prefix matches it, the exact id shape does not
+    redis.rpush('processing-q:w-g2-g0-abc12-7', 'live-of-w-g2')
     second = gpumgr.GpuManager(slots, redis_client=redis, fence=False)
     second.register('deployment', 'ns', 'w', tpl)
     view = second.list_namespaced_deployment('ns').items[0]
     assert view.spec.replicas == 2 and view.metadata.generation == 5
     assert sorted(redis.lrange('q', 0, -1)) == ['job-a', 'job-b']
-    assert redis.lrange('processing-q:other-g0-1', 0, -1) == ['not-ours']
+    assert redis.lrange('processing-q:other-g0-1f2e3-1', 0, -1) == \
+        ['not-ours']
+    assert redis.lrange('processing-q:w-g2-g0-abc12-7', 0, -1) == \
+        ['live-of-w-g2']
     third = gpumgr.GpuManager(slots, redis_client=redis, fence=False)
     third.register('deployment', 'ns', 'w', tpl, restore=False)
     assert third.list_namespaced_deployment('ns').items[0].spec.replicas == 0

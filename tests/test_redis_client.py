@@ -183,3 +183,30 @@ def test_native_sentinel_personality():
         for p in procs:
             p.terminate()
             p.wait(timeout=5)
+
+
+def test_native_scan_survives_deletes_between_pages(kredis_server):
+    """SCAN guarantee: a key present for the whole scan is
+    returned even when keys already returned are deleted between pages
+    (kredis's cursor is a hash position, not an index)."""
+    client = StrictRedis(host=kredis_server.host, port=kredis_server.port,
+                         decode_responses=True)
+    names = ['processing-q:w-%04d' % i for i in range(3000)]
+    pipe = client.pipeline(transaction=False)
+    for name in names:
+        pipe.rpush(name, 'x')
+    pipe.execute()
+    seen, deleted = set(), set()
+    cursor = 0
+    while True:
+        cursor, page = client.scan(cursor, match='processing-q:*', count=97)
+        seen.update(page)
+        # workers complete items: delete some of what was already returned
+        victims = sorted(seen - deleted)[:13]
+        if victims:
+            client.delete(*victims)
+            deleted.update(victims)
+        if int(cursor) == 0:
+            break
+    assert set(names) - deleted <= seen
+    assert len(seen) == len(names)          # never duplicated either

@@ -1,0 +1,89 @@
+"""Worker runtime: poison jobs fail on their own and
+oversized batches are split to the engine's capacity.  CPU-only, in-proc
+fake Redis, the mock CPU engine."""
+import pytest
+
+from kiosk_autoscaler_amd.models import mlp
+from kiosk_autoscaler_amd.worker import runtime as rt
+
+
+class _Channel(object):
+    def __init__(self):
+        self.events = []
+        self.direct = {}
+
+    def emit(self, ev, **fields):
+        self.events.append((ev, fields))
+
+
+def _runtime(redis_client, batch=1, rows=64, kind='deployment'):
+    env = {'ROWS_PER_KEY': str(rows), 'WORKER_BATCH': str(batch),
+           'MOCK_WORK_MS': '0', 'QUEUES': 'predict'}
+    cfg = rt.WorkerConfig(env, {'worker_id': 'w-g0-x-1', 'kind': kind})
+    run = rt.WorkerRuntime(cfg, None, _Channel(), lambda: redis_client)
+    run.redis = redis_client
+    run.engine = mlp.CpuMlpEngine(cfg)
+    return run
+
+
+def _push(client, name, **fields):
+    client.hset(name, mapping=dict({'status': 'new'}, **fields))
+    client.lpush('predict', name)
+
+
+def test_oversized_job_fails_alone_and_worker_keeps_serving(redis_client):
+    run = _runtime(redis_client)
+    consumer = rt.QueueConsumer(redis_client, 'w-g0-x-1', ['predict'])
+    _push(redis_client, 'predict:bad', rows=10 ** 9)
+    _push(redis_client, 'predict:good', rows=8)
+    for _ in range(2):
+        run._process(consumer, consumer.pull(limit=1, block=False))
+    bad = redis_client.hgetall('predict:bad')
+    assert bad['status'] == 'failed' and 'rows=' in bad['reason']
+    assert redis_client.hget('predict:good', 'status') == 'done'
+    # the poison job is not requeued: no processing key is left behind
+    assert not list(redis_client.scan_iter(match='processing-predict:*'))
+    assert run.keys_done == 1
+
+
+@pytest.mark.parametrize('field,value', [('rows', '0'), ('passes', '-3'),
+                                         ('service_ms', '99999999'),
+                                         ('rows', 'many')])
+def test_invalid_fields_rejected(redis_client, field, value):
+    run = _runtime(redis_client)
+    redis_client.hset('predict:j', mapping={'status': 'new', field: value})
+    with pytest.raises(rt.JobError):
+        run._job_params('predict:j')
+
+
+def test_engine_rejection_marks_batch_failed(redis_client):
+    run = _runtime(redis_client)
+
+    def reject(rows, passes, seed):
+        raise ValueError('rows must be in [1, max_rows]')
+    run.engine.forward = reject
+    consumer = rt.QueueConsumer(redis_client, 'w-g0-x-1', ['predict'])
+    _push(redis_client, 'predict:a', rows=8)
+    run._process(consumer, consumer.pull(limit=1, block=False))
+    assert redis_client.hget('predict:a', 'status') == 'failed'
+    assert not list(redis_client.scan_iter(match='processing-predict:*'))
+
+
+def test_batch_split_to_engine_capacity(redis_client):
+    run = _runtime(redis_client, batch=4, rows=64, kind='job')
+    calls = []
+    real = run.engine.forward
+
+    def forward(rows, passes, seed):
+        calls.append(rows)
+        return real(rows, passes, seed)
+    run.engine.forward = forward
+    limit = run.max_rows()             # max(64 * 4, 256) = 256
+    for i in range(4):
+        _push(redis_client, 'predict:j%d' % i, rows=100)
+    consumer = rt.QueueConsumer(redis_client, 'w-g0-x-1', ['predict'])
+    run._process(consumer, consumer.pull(limit=4, block=False))
+    assert all(r <= limit for r in calls) and sum(calls) == 400
+    assert len(calls) == 2
+    assert all(redis_client.hget('predict:j%d' % i, 'status') == 'done'
+               for i in range(4))
