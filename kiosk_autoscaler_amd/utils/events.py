@@ -32,6 +32,7 @@ class EventLog(object):
         self.redis_key = redis_key
         self.source = source or 'pid%d' % os.getpid()
         self._lock = threading.Lock()
+        self._send_lock = threading.Lock()   # one socket, many threads
         self._fh = None
         self.records = []
         self.keep = False
@@ -53,7 +54,8 @@ class EventLog(object):
                 self._fh.write(line + '\n')
         if self.redis_client is not None:
             try:
-                self.redis_client.rpush(self.redis_key, line)
+                with self._send_lock:
+                    self.redis_client.rpush(self.redis_key, line)
             except Exception:  # pylint: disable=broad-except
                 pass  # observability must never take the control loop down
         for observer in list(self.observers):

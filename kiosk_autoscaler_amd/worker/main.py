@@ -53,6 +53,38 @@ def _preload(backend):
     return time.monotonic_ns() - t0
 
 
+_CLIENTS = {}
+
+
+def _process_redis(role, host=None, port=None):
+    """One sentinel-aware, retrying client per role (``work``: the serving
+    loop; ``events``: the event log, which other threads also write) for the
+    whole process life.  A standby serves many assignments; building fresh
+    clients per assignment re-probed ``SENTINEL MASTERS`` twice on every
+    assign -> READY."""
+    host = host or os.environ.get('REDIS_HOST', '127.0.0.1')
+    port = int(port or os.environ.get('REDIS_PORT', 6379))
+    key = (role, host, port)
+    client = _CLIENTS.get(key)
+    if client is None:
+        from ..redisq import RedisClient
+        client = RedisClient(host=host, port=port,
+                             backoff=float(os.environ.get('REDIS_INTERVAL',
+                                                          1)))
+        _CLIENTS[key] = client
+    return client
+
+
+def _preconnect():
+    """Standby boot: connect before the first assignment (best effort)."""
+    try:
+        _process_redis('work')
+        if os.environ.get('EVENT_LOG'):
+            _process_redis('events')
+    except Exception:  # pylint: disable=broad-except
+        _CLIENTS.clear()   # retried lazily by the first assignment
+
+
 def _build_fence_factory(config):
     if config.fence in ('none', 'off', '0'):
         return None
@@ -113,6 +145,8 @@ def main(argv=None):
             channel.emit('error', message='preinit failed: %s' % err)
             return 4
 
+    if pin is not None and not args.assign:
+        _preconnect()
     node_agent = None
     if node:
         node_agent = _start_node_agent(channel, backend, early.get('slot', 0))
@@ -230,19 +264,20 @@ def _serve(assignment, backend, channel, node_agent=None):
     config = WorkerConfig(os.environ, assignment)
 
     from ..models.mlp import create_engine
-    from ..redisq import RedisClient
     from ..utils.events import EventLog
 
     def redis_factory():
-        # sentinel-aware and retrying, like the autoscaler's own client
-        return RedisClient(host=config.redis_host, port=config.redis_port,
-                           backoff=float(os.environ.get('REDIS_INTERVAL', 1)))
+        # sentinel-aware and retrying, like the autoscaler's own client;
+        # created once per process (see _process_redis)
+        return _process_redis('work', config.redis_host, config.redis_port)
 
     events = None
     if config.record_events:
         path = os.environ.get('EVENT_LOG') or None
         events = EventLog(path=None if path == 'redis' else path,
-                          redis_client=redis_factory(),
+                          redis_client=_process_redis(
+                              'events', config.redis_host,
+                              config.redis_port),
                           source=config.worker_id)
 
     def engine_factory(cfg, stage):
