@@ -206,6 +206,8 @@ PYBIND11_MODULE(_kiosk_hip, m) {
              return d;
            })
       .def("info", &kiosk::Engine::info)
+      .def("copy_output", &kiosk::Engine::copy_output, py::arg("dst"),
+           py::arg("rows"), py::call_guard<py::gil_scoped_release>())
       .def("weight_ptr", &kiosk::Engine::weight_ptr)
       .def("act_ptr", &kiosk::Engine::act_ptr)
       .def_property_readonly("stream", &kiosk::Engine::stream_handle)

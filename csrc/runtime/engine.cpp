@@ -404,6 +404,21 @@ ForwardResult Engine::forward(int rows, int passes, unsigned long long seed) {
   return r;
 }
 
+void Engine::copy_output(unsigned long long dst, int rows) {
+  if (closed_) throw std::runtime_error("engine closed");
+  if (rows < 1 || rows > max_rows_) {
+    throw std::invalid_argument("rows exceeds the engine's max_rows");
+  }
+  // the layers ping-pong x_ <-> y_ starting from x_: an even layer count
+  // ends in x_ (enqueue_forward)
+  const uint16_t* out = (layers_ % 2 == 0) ? x_ : y_;
+  check_hip(hipMemcpyAsync(reinterpret_cast<void*>(dst), out,
+                           size_t(rows) * dim_ * sizeof(uint16_t),
+                           hipMemcpyDeviceToDevice, stream_),
+            "output copy");
+  check_hip(hipStreamSynchronize(stream_), "output sync");
+}
+
 std::map<std::string, double> Engine::info() const {
   std::map<std::string, double> out;
   size_t free_b = 0, total_b = 0;

@@ -64,6 +64,9 @@ class Engine {
   }
   std::map<std::string, double> info() const;
 
+  // copy the last forward's [rows, dim] bf16 output to device memory `dst`
+  // (numerics tests: elementwise comparison against the fp32 reference)
+  void copy_output(unsigned long long dst, int rows);
   // raw pointers for numerics tests
   unsigned long long weight_ptr(int layer, int which) const;
   unsigned long long act_ptr(int which) const;

@@ -150,3 +150,35 @@ def reference_forward_checksum(dim, hidden, layers, rows, model_seed,
     init_uniform_(x, input_seed, -1.0, 1.0)
     y = reference_forward(x, weights)
     return float(y.double().sum().item())
+
+
+def engine_output(engine, rows):
+    """The last ``Engine.forward`` output as a ``[rows, dim]`` bf16 tensor."""
+    import torch
+    out = torch.empty((rows, engine.dim), dtype=torch.bfloat16,
+                      device='cuda')
+    torch.cuda.synchronize()
+    engine.copy_output(out.data_ptr(), rows)
+    return out
+
+
+def compare_engine_forward(engine, rows, model_seed, input_seed):
+    """Run one (graph-replayed) ``Engine.forward`` and compare its whole
+    output elementwise against :func:`reference_forward` (fp32 PyTorch with
+    the kernels' bf16 storage points).  Returns ``(out, ref, stats)``."""
+    import torch
+    engine.prepare(rows)                 # capture: the forward is a replay
+    result = engine.forward(rows, 1, input_seed)
+    out = engine_output(engine, rows).float()
+    weights = model_weights(engine.dim, engine.hidden, engine.layers,
+                            model_seed)
+    x = torch.empty((rows, engine.dim), dtype=torch.bfloat16, device='cuda')
+    init_uniform_(x, input_seed, -1.0, 1.0)
+    ref = reference_forward(x, weights).float()
+    err = (out - ref).abs()
+    stats = {'max_abs_err': float(err.max()),
+             'mean_abs_err': float(err.mean()),
+             'ref_mean_abs': float(ref.abs().mean()),
+             'checksum': result['checksum'], 'graph': result['graph'],
+             'gpu_ms': result['gpu_ms']}
+    return out, ref, stats

@@ -120,6 +120,29 @@ def test_engine_matches_reference(mod):
         engine.close()
 
 
+@pytest.mark.parametrize('dim,hidden,layers,rows', [
+    (4096, 16384, 4, 2048),     # the production worker shape (split-K)
+    (4096, 16384, 3, 1000),     # odd layer count, ragged rows
+    (1024, 4096, 2, 512)])
+def test_engine_forward_elementwise(mod, dim, hidden, layers, rows):
+    """The whole production forward (graph replay, auto GEMM dispatch with
+    the split-K down-projection) elementwise against the fp32 reference --
+    a layout or permutation error cannot hide behind a checksum."""
+    from kiosk_autoscaler_amd.ops import kernels
+    engine = mod.Engine(0, dim, hidden, layers, max(rows, 256), 21)
+    try:
+        out, ref, stats = kernels.compare_engine_forward(engine, rows, 21, 5)
+    finally:
+        engine.close()
+    assert stats['graph']
+    torch.testing.assert_close(out, ref, rtol=3e-2, atol=3e-2)
+    assert stats['mean_abs_err'] < 2e-2 * stats['ref_mean_abs']
+    # rows are not permuted: each output row is closest to its own
+    # reference row
+    d = torch.cdist(out[:64], ref[:64])
+    assert torch.equal(d.argmin(dim=1), torch.arange(64, device=d.device))
+
+
 def test_warmstart_touches_every_cu(mod):
     engine = mod.Engine(0, 256, 512, 1, 64, 1)
     try:
