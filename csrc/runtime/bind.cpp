@@ -153,6 +153,16 @@ PYBIND11_MODULE(_kiosk_hip, m) {
         return d;
       },
       py::arg("device") = 0);
+  // (free, total) HBM bytes of the current device: a device-mode standby
+  // reports it so KEYS_PER_POD is sized against what is actually free
+  m.def("mem_info", [] {
+    size_t free_b = 0, total_b = 0;
+    {
+      py::gil_scoped_release release;
+      check_hip(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
+    }
+    return py::make_tuple(free_b, total_b);
+  });
   m.def("synchronize", [] { check_hip(hipDeviceSynchronize(), "sync"); },
         py::call_guard<py::gil_scoped_release>());
   m.def("roctx_available", &kiosk::roctx_available);

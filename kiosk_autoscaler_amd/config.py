@@ -157,7 +157,8 @@ EXTRA_DEFAULTS = (
     ('MODEL_LAYERS', int, 4),
     ('ROWS_PER_KEY', int, 2048),
     ('HBM_PER_KEY_BYTES', int, 0),          # 0 = derive from the model
-    ('HBM_RESERVE_BYTES', int, 8 << 30),
+    ('HBM_RESERVE_BYTES', int, 8 << 30),    # static sizing (no measurement)
+    ('HBM_FREE_RESERVE_BYTES', int, 1 << 30),  # sizing from measured free HBM
     ('EVENT_LOG', str, ''),                 # JSONL path | 'redis' | '' (off)
     ('TICK_KEY', str, ''),                  # publish tick times to this key
     ('STATE_TTL', int, 3600),

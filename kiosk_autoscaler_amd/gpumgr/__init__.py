@@ -57,6 +57,10 @@ def worker_env(settings, keys_per_pod=None):
     }
     if settings.EVENT_LOG:
         env['EVENT_LOG'] = settings.EVENT_LOG
+    # the manager re-sizes KEYS_PER_POD per assignment from the free HBM a
+    # standby measured (utils.hbm.size_from_free)
+    env['HBM_PER_KEY_BYTES'] = settings.HBM_PER_KEY_BYTES
+    env['HBM_FREE_RESERVE_BYTES'] = settings.HBM_FREE_RESERVE_BYTES
     for passthrough in ('PASSES_PER_KEY', 'MOCK_WORK_MS', 'WORKER_BATCH',
                         'JOB_IDLE_EXIT_S', 'POLL_BLOCK_S', 'MODEL_SEED',
                         'KIOSK_RCCL_LIB', 'WORKER_EVENTS', 'KIOSK_FAULTS',

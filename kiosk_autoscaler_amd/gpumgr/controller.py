@@ -136,6 +136,7 @@ class _Process(object):
         self.eof = False
         self.recycles = 0
         self.node_ok = False    # runs a node-communicator agent
+        self.hbm_free = None    # free HBM bytes the standby measured
 
     @property
     def pid(self):
@@ -628,6 +629,7 @@ class GpuManager(object):
             return
         if message.get('ev') == 'standby':
             proc.booted = True
+            proc.hbm_free = message.get('hbm_free')
             self._publish_pool()
             self.events.emit('standby_ready', pid=proc.pid, slot=proc.slot,
                              boot_s=(time.monotonic_ns() - proc.t_spawn)
@@ -688,6 +690,8 @@ class GpuManager(object):
         }
         proc = self._take_standby(resource.template, slot)
         from_pool = proc is not None
+        if from_pool and proc.hbm_free:
+            self._size_from_free(resource, assign, proc.hbm_free, slot)
         if from_pool:
             if not proc.pipe.send(assign):
                 proc.popen.kill()
@@ -706,6 +710,34 @@ class GpuManager(object):
                     slot.visible_id or slot.index, proc.pid,
                     'warm pool' if from_pool else 'cold spawn')
         return worker
+
+    def _size_from_free(self, resource, assign, free, slot):
+        """N5: clamp this assignment's KEYS_PER_POD (the job worker's batch)
+        to what fits in the HBM the standby measured free."""
+        from ..utils import hbm
+        tpl = resource.template
+        env = tpl.env
+
+        def num(name, default):
+            try:
+                return int(env.get(name, default))
+            except (TypeError, ValueError):
+                return default
+        kpp, limit = hbm.size_from_free(
+            tpl.keys_per_pod, free, num('MODEL_DIM', 4096),
+            num('MODEL_HIDDEN', 16384), num('MODEL_LAYERS', 4),
+            num('ROWS_PER_KEY', 2048),
+            reserve=num('HBM_FREE_RESERVE_BYTES', 1 << 30),
+            per_key=num('HBM_PER_KEY_BYTES', 0))
+        if kpp != tpl.keys_per_pod:
+            logger.warning('KEYS_PER_POD=%d does not fit the %.1f GB free on '
+                           'GPU %s (max %d); this worker batches %d',
+                           tpl.keys_per_pod, free / 1e9, slot.index, limit,
+                           kpp)
+        assign['template'] = dict(assign['template'], keys_per_pod=kpp)
+        self.events.emit('hbm_sizing', gpu=slot.index, hbm_free=free,
+                         max_keys_per_pod=limit, keys_per_pod=kpp,
+                         requested=tpl.keys_per_pod)
 
     def _drain(self, worker, reason):
         if worker.state in (DRAINING, EXITED):

@@ -78,6 +78,25 @@ def size_keys_per_pod(keys_per_pod, dim, hidden, layers, rows,
     return int(keys_per_pod)
 
 
+def size_from_free(keys_per_pod, free_bytes, dim, hidden, layers, rows,
+                   reserve=1 << 30, per_key=0):
+    """``KEYS_PER_POD`` against the HBM a standby *measured* free
+    (``hipMemGetInfo`` after its HIP context, code objects and communicator
+    exist, so their overhead is already excluded):
+
+        max_kpp = floor((HBM_free - weights - reserve) / per_key_bytes)
+
+    ``reserve`` covers what the engine allocates beyond weights and per-key
+    activations (split-K workspace, graph exec, allocator slack).  Returns
+    ``(usable kpp, max_kpp)``; usable is at least 1 (a worker always takes
+    one key)."""
+    weights = model_bytes(dim, hidden, layers)
+    footprint = per_key or per_key_bytes(rows, dim, hidden)
+    limit = int(max_keys_per_pod(int(free_bytes), weights, footprint,
+                                 reserve))
+    return int(max(1, min(int(keys_per_pod), limit))), limit
+
+
 def report(dim, hidden, layers, rows, hbm_bytes=None, reserve=8 << 30):
     hbm = hbm_bytes or device_hbm_bytes()
     weights = model_bytes(dim, hidden, layers)

@@ -240,10 +240,26 @@ def _standalone(backend):
     return code
 
 
+def _hbm_free(backend, preinit):
+    """Free HBM bytes as this standby sees it, or None (not measurable:
+    no HIP context yet).  ``MOCK_HBM_FREE_BYTES`` stands in on CPU."""
+    mock = os.environ.get('MOCK_HBM_FREE_BYTES')
+    if mock:
+        return int(mock)
+    if backend != 'hip' or not preinit:
+        return None
+    try:
+        from ..ops import native
+        free, _total = native.load().mem_info()
+        return int(free)
+    except Exception:  # pylint: disable=broad-except
+        return None
+
+
 def _wait_for_assignment(channel, pin, preload_ns, backend, preinit):
     """Standby: report, then block until ``assign`` (or ``exit``/EOF)."""
     channel.emit('standby', preload_ns=preload_ns, backend=backend,
-                 preinit=preinit)
+                 preinit=preinit, hbm_free=_hbm_free(backend, preinit))
     while True:
         message = channel.read_command()
         if message is None or message.get('cmd') in ('exit', 'eof'):

@@ -1,0 +1,90 @@
+"""N5 / BASELINE config 5: ``RESOURCE_TYPE=job KEYS_PER_POD=4`` sized against
+the HBM a standby measured free (``hipMemGetInfo`` after its context, code
+objects and communicator exist), per assignment.  CPU: the mock standby
+reports ``MOCK_HBM_FREE_BYTES``; GPU: the real measurement on MI355X."""
+import pytest
+
+from kiosk_autoscaler_amd.utils import hbm
+from test_integration_cpu import enqueue, stack, tick, wait_for  # noqa: F401
+
+
+def test_size_from_free_formula():
+    weights = hbm.model_bytes(64, 256, 1)
+    kpp, limit = hbm.size_from_free(4, weights + 2.5e9, 64, 256, 1, 8,
+                                    reserve=0, per_key=10 ** 9)
+    assert (kpp, limit) == (2, 2)
+    kpp, limit = hbm.size_from_free(4, 10 ** 12, 4096, 16384, 4, 2048)
+    assert kpp == 4 and limit > 1000          # 288 GB: thousands of keys
+    assert hbm.size_from_free(4, 1, 64, 256, 1, 8)[0] == 1   # never below 1
+
+
+def _sizing(events):
+    return [e for e in events.records if e['ev'] == 'hbm_sizing']
+
+
+@pytest.mark.slow
+def test_job_kpp4_clamped_to_measured_free(stack):
+    weights = hbm.model_bytes(64, 256, 1)
+    s, client, manager, scaler, events = stack(
+        RESOURCE_TYPE='job', KEYS_PER_POD='4', MAX_PODS='1',
+        MODEL_DIM='64', MODEL_HIDDEN='256', MODEL_LAYERS='1',
+        HBM_PER_KEY_BYTES=str(10 ** 9), HBM_FREE_RESERVE_BYTES='0',
+        extra_env={'MOCK_HBM_FREE_BYTES': str(int(weights + 2.5e9)),
+                   'JOB_IDLE_EXIT_S': '0.3', 'MOCK_WORK_MS': '50'})
+    wait_for(lambda: manager.standbys and all(
+        p.booted for p in manager.standbys.values()))
+    enqueue(client, 4)
+    assert tick(scaler, s) == 1                 # 4 keys // 4 per pod
+    wait_for(lambda: _sizing(events))
+    sizing = _sizing(events)[0]
+    assert sizing['requested'] == 4 and sizing['max_keys_per_pod'] == 2
+    assert sizing['keys_per_pod'] == 2
+    wait_for(lambda: all(client.hget('predict:job%d' % i, 'status') == 'done'
+                         for i in range(4)), timeout=30)
+    # two batches of two: both jobs of a batch report the same start stamp
+    starts = sorted(client.hget('predict:job%d' % i, 'started_ns')
+                    for i in range(4))
+    assert len(set(starts)) == 2
+
+
+@pytest.mark.gpu
+def test_gpu_job_kpp4_sized_from_hip_free(stack):
+    """Real MI355X: the standby measures free HBM after preinit; at the
+    production model (1 GiB of bf16 weights, 2048-row keys) KEYS_PER_POD=4
+    fits and is kept; with a per-key footprint of a third of the free HBM it
+    is clamped to 2 -- and 4 keys are served in two batches of two."""
+    s, client, manager, scaler, events = stack(
+        RESOURCE_TYPE='job', KEYS_PER_POD='4', MAX_PODS='1', WARM_POOL='1',
+        WORKER_BACKEND='hip', FENCE='none', ROWS_PER_KEY='256',
+        extra_env={'JOB_IDLE_EXIT_S': '0.3'})
+    wait_for(lambda: manager.standbys and all(
+        p.booted for p in manager.standbys.values()), timeout=180)
+    free = manager.standbys[0].hbm_free
+    assert free and 200e9 < free < 320e9          # 288 GB HBM3E, measured
+    enqueue(client, 4)
+    assert tick(scaler, s) == 1
+    wait_for(lambda: _sizing(events), timeout=60)
+    first = _sizing(events)[0]
+    assert first['hbm_free'] == free and first['keys_per_pod'] == 4
+    wait_for(lambda: all(client.hget('predict:job%d' % i, 'status') == 'done'
+                         for i in range(4)), timeout=120)
+    wait_for(lambda: manager.list_namespaced_job('default').items[0]
+             .spec.parallelism == 0, timeout=60)
+    wait_for(lambda: manager.standbys and manager.standbys[0].booted,
+             timeout=60)
+    # clamp: a per-key footprint of free/3 leaves room for 2 keys
+    free = manager.standbys[0].hbm_free
+    manager.resources[('job', 'default', 'worker')].template.env[
+        'HBM_PER_KEY_BYTES'] = str(free // 3)
+    for i in range(4):
+        client.delete('predict:job%d' % i)
+    enqueue(client, 4)
+    assert tick(scaler, s) == 1
+    wait_for(lambda: len(_sizing(events)) == 2, timeout=60)
+    second = _sizing(events)[1]
+    assert second['keys_per_pod'] == 2 and second['max_keys_per_pod'] == 2
+    wait_for(lambda: all(client.hget('predict:job%d' % i, 'status') == 'done'
+                         for i in range(4)), timeout=120)
+    starts = {client.hget('predict:job%d' % i, 'started_ns')
+              for i in range(4)}
+    assert len(starts) == 2
