@@ -360,3 +360,52 @@ def test_eight_workers_churn_and_death(resp_server):
     stats = metrics.fence_stats(records)
     assert stats['fence_max_ranks'] == 8
     assert stats['node_comm_generations'] == 2
+
+
+@pytest.mark.gpu
+def test_gpu_node_comm_through_the_manager(resp_server):
+    """MI355X, world size 1: the manager builds the RCCL node communicator
+    once at pool boot; two scale 0 -> 1 -> 0 cycles are fenced by the
+    72-B all-reduce alone (no further generation)."""
+    from kiosk_autoscaler_amd import Autoscaler, gpumgr
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import RedisClient, StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict', 'RESOURCE_NAME': 'worker', 'MAX_PODS': '1',
+           'WORKER_BACKEND': 'hip', 'WARM_POOL': '1', 'FENCE': 'auto',
+           'INTERVAL': '1', 'REDIS_INTERVAL': '0', 'GPU_IDS': '0',
+           'MODEL_DIM': '1024', 'MODEL_HIDDEN': '4096', 'MODEL_LAYERS': '2',
+           'ROWS_PER_KEY': '256'}
+    s = Settings(Config(environ=env, use_files=False))
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    events = EventLog(source='test')
+    events.keep = True
+    manager = gpumgr.build_manager(s, redis_client=client,
+                                   events=events).start()
+    scaler = Autoscaler(RedisClient(host=resp_server.host,
+                                    port=resp_server.port, backoff=0),
+                        'predict', actuator=manager)
+    try:
+        wait_for(lambda: manager.node.ready, timeout=180)
+        for cycle in range(2):
+            item = 'predict:g%d' % cycle
+            client.hset(item, mapping={'status': 'new', 'rows': 256})
+            client.lpush('predict', item)
+            assert scaler.scale('default', 'deployment', 'worker',
+                                0, 1, 1) == 1
+            wait_for(lambda: client.hget(item, 'status') == 'done',
+                     timeout=120)
+            wait_for(lambda: _converged(manager, client) and
+                     len(_active(client)['members']) == 1, timeout=60)
+            assert scaler.scale('default', 'deployment', 'worker',
+                                0, 1, 1) == 0
+            wait_for(lambda: _active(client)['members'] == [], timeout=60)
+        assert manager.node.generations == 1
+    finally:
+        manager.stop(timeout=20)
+    done = [e for e in events.records if e['ev'] == 'fence_done']
+    assert done and all(e['transport'] == 'rccl' and e['mode'] == 'node'
+                        for e in done)
+    assert max(e['wall_s'] for e in done) < 0.05
