@@ -31,6 +31,10 @@
 
 namespace kredis {
 
+// SIGTERM/SIGINT end the event loop normally (destructors and, in the
+// sanitizer build, LeakSanitizer's exit check run)
+volatile sig_atomic_t g_terminate = 0;
+
 int64_t now_ms() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -1166,7 +1170,7 @@ int Server::run(const std::string& bind_addr, int port) {
          ntohs(addr.sin_port));
   fflush(stdout);
   std::vector<epoll_event> events(256);
-  while (!shutdown_) {
+  while (!shutdown_ && !g_terminate) {
     int timeout = blocked_order_.empty() ? 1000 : 10;
     int n = epoll_wait(epfd_, events.data(), static_cast<int>(events.size()),
                        timeout);
@@ -1211,6 +1215,8 @@ int Server::run(const std::string& bind_addr, int port) {
 
 int main(int argc, char** argv) {
   signal(SIGPIPE, SIG_IGN);
+  signal(SIGTERM, [](int) { kredis::g_terminate = 1; });
+  signal(SIGINT, [](int) { kredis::g_terminate = 1; });
   std::string bind_addr = "127.0.0.1";
   int port = 6379;
   kredis::SentinelConfig sentinel;

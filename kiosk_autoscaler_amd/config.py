@@ -162,9 +162,12 @@ EXTRA_DEFAULTS = (
     ('EVENT_LOG', str, ''),                 # JSONL path | 'redis' | '' (off)
     ('TICK_KEY', str, ''),                  # publish tick times to this key
     ('STATE_TTL', int, 3600),
-    ('WORKER_TIMEOUT', float, 0.0),         # s without progress while busy -> kill (0 = off)
-    ('START_TIMEOUT', float, 0.0),          # s from assignment to READY -> kill (0 = off)
-    ('WORKER_RECYCLE', bool, True),         # drained worker -> back to the warm pool
+    # s without progress while busy -> kill (0 = off)
+    ('WORKER_TIMEOUT', float, 0.0),
+    # s from assignment to READY -> kill (0 = off)
+    ('START_TIMEOUT', float, 0.0),
+    ('WORKER_RECYCLE', bool, True),         # drained worker -> warm pool
+    ('FENCE_COMM', str, 'node'),            # node (persistent) | epoch
     ('METRICS_PORT', int, 0),               # Prometheus /metrics port (0 = off)
     ('METRICS_ADDR', str, '0.0.0.0'),
     ('DEBUG', bool, True),

@@ -112,7 +112,8 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
                          state_ttl=settings.STATE_TTL,
                          worker_timeout=settings.WORKER_TIMEOUT,
                          start_timeout=settings.START_TIMEOUT,
-                         recycle=settings.WORKER_RECYCLE)
+                         recycle=settings.WORKER_RECYCLE,
+                         fence_comm=settings.FENCE_COMM)
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

@@ -36,7 +36,10 @@ def resp_server():
 
 
 def kredis_binary():
-    path = os.path.join(ROOT, 'build', 'kredis-server')
+    """``build/kredis-server``; ``KIOSK_KREDIS_BIN`` selects another build
+    (CI runs the RESP suites against ``build/kredis-server-asan``)."""
+    path = os.environ.get('KIOSK_KREDIS_BIN') or os.path.join(
+        ROOT, 'build', 'kredis-server')
     return path if os.path.exists(path) else None
 
 

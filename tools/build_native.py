@@ -111,7 +111,17 @@ def check_no_undefined_own_symbols(path):
             path, '\n  '.join(missing)))
 
 
-def build_kredis(verbose=False):
+KREDIS_ASAN = os.path.join(BUILD, 'kredis-server-asan')
+SANITIZE_FLAGS = ['-O1', '-g', '-fno-omit-frame-pointer',
+                  '-fsanitize=address,undefined',
+                  '-fno-sanitize-recover=undefined']
+
+
+def build_kredis(verbose=False, sanitize=False):
+    """``build/kredis-server`` (-O2), or with ``sanitize`` the ASan+UBSan
+    build ``build/kredis-server-asan`` (the parser and network
+    code is where memory bugs hide; tests/test_kredis_sanitized.py drives it
+    with valid and malformed traffic)."""
     src_dir = os.path.join(ROOT, 'csrc', 'kredis')
     if not os.path.isdir(src_dir):
         return None
@@ -120,17 +130,21 @@ def build_kredis(verbose=False):
     if not sources:
         return None
     os.makedirs(BUILD, exist_ok=True)
-    if _stale(KREDIS, sources + _headers(src_dir)):
+    target = KREDIS_ASAN if sanitize else KREDIS
+    flags = SANITIZE_FLAGS if sanitize else ['-O2']
+    if _stale(target, sources + _headers(src_dir)):
         cxx = shutil.which('g++') or 'c++'
-        _run([cxx, '-O2', '-std=c++17', '-Wall', '-pthread'] + sources +
-             ['-o', KREDIS], verbose)
-    return KREDIS
+        _run([cxx] + flags + ['-std=c++17', '-Wall', '-pthread'] + sources +
+             ['-o', target], verbose)
+    return target
 
 
-def build(verbose=False, clean=False, jobs=4, kernels=True):
+def build(verbose=False, clean=False, jobs=4, kernels=True, sanitize=False):
     if clean and os.path.isdir(BUILD):
         shutil.rmtree(BUILD)
     out = {'kredis': build_kredis(verbose)}
+    if sanitize:
+        out['kredis_asan'] = build_kredis(verbose, sanitize=True)
     if kernels:
         objects = compile_units(verbose, jobs)
         out['extension'] = link_extension(objects, verbose)
@@ -143,8 +157,11 @@ def main():
     parser.add_argument('--clean', action='store_true')
     parser.add_argument('-j', '--jobs', type=int, default=4)
     parser.add_argument('--no-kernels', action='store_true')
+    parser.add_argument('--sanitize', action='store_true',
+                        help='also build the ASan+UBSan kredis-server')
     args = parser.parse_args()
-    out = build(args.verbose, args.clean, args.jobs, not args.no_kernels)
+    out = build(args.verbose, args.clean, args.jobs, not args.no_kernels,
+                args.sanitize)
     for key, value in out.items():
         print('%s: %s' % (key, value))
 
