@@ -10,11 +10,15 @@ this module plays API server + controller + kubelet:
 * **Workers** are OS processes, one per GPU, pinned with
   ``HIP_VISIBLE_DEVICES`` and CPU affinity to the GPU's NUMA-local cores.
   The lowest free GPU index is allocated first.
-* **Warm pool**: ``pool_size`` standby processes have already imported
-  PyTorch-ROCm and the native kernel module but have *not* initialised HIP
-  (so they hold no GPU).  A scale-up hands a standby its GPU over a pipe,
-  taking the ~1.6 s interpreter/torch import off the critical path
-  (SURVEY §7.4 item 4).  Standbys do not count as replicas.
+* **Warm pool**: ``pool_size`` standby processes, each pinned to its GPU
+  at spawn, have imported PyTorch-ROCm and the native kernel module.  With
+  ``WARM_POOL_MODE=device`` (the default) they have also created the HIP
+  context and loaded every code object, so **a standby holds its GPU**
+  (context and code objects, no weights; the benchmark reports this as
+  ``standby_gpu_s``); with ``import`` they stop before HIP and hold none.
+  A scale-up hands a standby its assignment over a pipe, taking the ~1.6 s
+  interpreter/torch import and the HIP init off the critical path (SURVEY
+  §7.4 item 4).  Standbys do not count as replicas.
 * **READY** (``status.available_replicas``) means the worker has its
   weights in HBM and has run the warm-start kernel.
 * **Scale-down** drains: the worker finishes its in-flight key and exits.
@@ -26,9 +30,12 @@ this module plays API server + controller + kubelet:
   the reference's stranded-keys case (a completed Job that is never
   restarted) cannot occur.
 * **Membership fence**: whenever the READY set changes the manager starts a
-  fence epoch (coalesced: one in flight at a time); workers agree on the set
-  with an RCCL all-reduce over xGMI and rank 0 acknowledges.  The fenced
-  set is published to Redis (``kiosk:active:<ns>:<name>``).
+  fence epoch (coalesced: one in flight at a time); the set is agreed with
+  a 72-B RCCL all-reduce over xGMI and rank 0 acknowledges.  With a standby
+  per GPU the communicator is persistent (:mod:`.nodecomm`: built once over
+  every slot's process, rebuilt only when one dies); otherwise each epoch
+  bootstraps its own over the READY workers.  The fenced set is published
+  to Redis (``kiosk:active:<ns>:<name>``).
 """
 import collections
 import itertools
