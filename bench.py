@@ -363,7 +363,7 @@ def reference_sim(episodes, events, args, same_grid=True):
     return {'latency_mean_s': sum(lat) / len(lat) if lat else None,
             'gpu_idle_pct': sum(idle) / len(idle) if idle else None,
             'grid': 'live tick instants' if same_grid else 'ideal',
-            'ready_delay_s': 0.0}
+            'ready_delay_s': 0.0, 'episodes': results}
 
 
 def cold_spawn_cycle(svc, gen, args, budget):
@@ -443,9 +443,18 @@ def main():
         if world > 1:
             import datetime
             import torch.distributed as dist
-            dist.init_process_group(
-                'gloo', rank=rank, world_size=world,
-                timeout=datetime.timedelta(seconds=args.budget_s + 300))
+            # gloo prints its connection summary on fd 1: keep stdout for
+            # the one JSON line the driver parses
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group(
+                    'gloo', rank=rank, world_size=world,
+                    timeout=datetime.timedelta(seconds=args.budget_s + 300))
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
         use_cuda = torch.cuda.is_available() and args.backend == 'hip'
         if use_cuda:
             torch.cuda.set_device(local_rank)

@@ -101,6 +101,8 @@ def episode_metrics(events, episode):
                            if first_item in done else None),
         'all_ready_s': (ready[-1] - t0) / 1e9 if ready else None,
         'workers_ready': len(ready),
+        'workers_assigned': sum(1 for e in in_window
+                                if e['ev'] == 'worker_assigned'),
         'keys': len(episode['keys']),
         'keys_done': sum(1 for item, _, _ in episode['keys'] if item in done),
         'queue_wait_mean_s': _mean(waits),
