@@ -1,0 +1,27 @@
+# Round-2 MI355X bench set: the driver's default command, then labelled
+# variants (each its own bounded run; stop at the first failure).
+#   bash tools/gpu_round2_variants.sh A   -> default + strict + 2 queues + idle-interval
+#   bash tools/gpu_round2_variants.sh B   -> job KEYS_PER_POD=4 + 60 s-burst long form
+set -o pipefail
+OUT=gpurun_out/r2_variants
+mkdir -p $OUT
+run() {
+  tag=$1; limit=$2; shift 2
+  echo "== $tag: bench.py $*"
+  timeout -k 10 $limit python bench.py "$@" > $OUT/$tag.json 2> $OUT/$tag.err
+  rc=$?
+  cp gpurun_out/bench_detail_n1.json $OUT/${tag}_detail.json 2>/dev/null
+  tail -1 $OUT/$tag.err
+  head -c 400 $OUT/$tag.json; echo
+  return $rc
+}
+if [ "$1" = "A" ]; then
+  run default 560 --gpus 1 --steps 20 --warmup 5 && \
+  run strict 200 --gpus 1 --steps 10 --warmup 1 --policy strict --budget-s 180 && \
+  run two_queues 200 --gpus 1 --steps 10 --warmup 1 --queues predict,track --budget-s 180 && \
+  run idle_interval_0.1 200 --gpus 1 --steps 10 --warmup 1 --idle-interval 0.1 --budget-s 180
+else
+  run job_kpp4_strict 260 --gpus 1 --steps 6 --warmup 1 --resource-type job --kpp 4 --on 8 --lam-per-gpu 1.0 --policy strict --budget-s 240 && \
+  run job_kpp4_reference 260 --gpus 1 --steps 6 --warmup 1 --resource-type job --kpp 4 --on 8 --lam-per-gpu 1.0 --budget-s 240 --drain-timeout 20 && \
+  run longform_60s_bursts 400 --gpus 1 --steps 2 --warmup 0 --on 60 --budget-s 380
+fi
