@@ -62,9 +62,11 @@ PYBIND11_MODULE(_kiosk_hip, m) {
   m.attr("gemm_lds_bytes") = kiosk::kGemmLdsBytes;
   m.attr("gemm_ring_lds_bytes") = kiosk::kGemmRingLdsBytes;
   m.def("gemm_set_splitk_fused", &kiosk::gemm_set_splitk_fused,
-        py::arg("on"),
-        "4-wave split-K: combine in-launch (True) or via the reduce kernel "
-        "(False, the default)");
+        py::arg("mode"),
+        "4-wave split-K combine: 0 = partial planes + reduce kernel, "
+        "1 = in-launch by the last slice (both planes), 2 = in-launch, "
+        "ticket first (one plane, accumulators kept)");
+  m.def("gemm_splitk_fused", &kiosk::gemm_splitk_fused);
   m.attr("sum_blocks") = kiosk::kSumBlocks;
 
   m.def("gemm_shape_ok", &kiosk::gemm_shape_ok);

@@ -56,10 +56,22 @@ def main():
         def ours_splitk():
             kernels.gemm(a, b, out=out, variant='256splitk')
 
+        default_mode = mod.gemm_splitk_fused()
+
         def ours_splitk_fused():
-            mod.gemm_set_splitk_fused(True)
+            mod.gemm_set_splitk_fused(1)
             kernels.gemm(a, b, out=out, variant='256splitk')
-            mod.gemm_set_splitk_fused(False)
+            mod.gemm_set_splitk_fused(default_mode)
+
+        def ours_splitk_ticket():
+            mod.gemm_set_splitk_fused(2)
+            kernels.gemm(a, b, out=out, variant='256splitk')
+            mod.gemm_set_splitk_fused(default_mode)
+
+        def ours_splitk_reduce():
+            mod.gemm_set_splitk_fused(0)
+            kernels.gemm(a, b, out=out, variant='256splitk')
+            mod.gemm_set_splitk_fused(default_mode)
 
         def theirs():
             torch.nn.functional.gelu(torch.addmm(bias.to(torch.bfloat16), a,
@@ -79,6 +91,8 @@ def main():
         if mod.gemm_workspace_bytes(M, N, K):
             fns['native256splitk'] = ours_splitk
             fns['native256splitk_fused'] = ours_splitk_fused
+            fns['native256splitk_ticket'] = ours_splitk_ticket
+            fns['native256splitk_reduce'] = ours_splitk_reduce
 
         results = {k: [] for k in fns}
         for fn in fns.values():
