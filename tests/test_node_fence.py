@@ -258,7 +258,8 @@ def _converged(manager, client):
 
 
 @pytest.mark.slow
-def test_eight_workers_churn_and_death(resp_server):
+@pytest.mark.parametrize('transport', ['store', 'gloo'])
+def test_eight_workers_churn_and_death(resp_server, transport):
     from kiosk_autoscaler_amd import Autoscaler, gpumgr, policy
     from kiosk_autoscaler_amd.bench import metrics
     from kiosk_autoscaler_amd.config import Config, Settings
@@ -267,7 +268,7 @@ def test_eight_workers_churn_and_death(resp_server):
     env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
            'QUEUES': 'predict,track', 'RESOURCE_NAME': 'worker',
            'MAX_PODS': '8', 'KEYS_PER_POD': '1', 'WORKER_BACKEND': 'cpu',
-           'WARM_POOL': '8', 'FENCE': 'store', 'INTERVAL': '1',
+           'WARM_POOL': '8', 'FENCE': transport, 'INTERVAL': '1',
            'REDIS_INTERVAL': '0', 'EVENT_LOG': 'redis'}
     s = Settings(Config(environ=env, use_files=False))
     client = StrictRedis(host=resp_server.host, port=resp_server.port,
@@ -300,7 +301,8 @@ def test_eight_workers_churn_and_death(resp_server):
 
     try:
         assert manager.node is not None
-        wait_for(lambda: manager.node.ready, timeout=60)
+        # gloo: every rank imports torch.distributed for its first group
+        wait_for(lambda: manager.node.ready, timeout=120)
         assert len(manager.node.members) == 8
         # {predict:3, track:2} from zero -> 5
         batch = enqueue(3, 2)
@@ -351,7 +353,8 @@ def test_eight_workers_churn_and_death(resp_server):
     from kiosk_autoscaler_amd.utils.events import drain_redis
     records = events.records + drain_redis(client)   # + workers' events
     done = [e for e in records if e['ev'] == 'fence_done']
-    assert done and all(e['n'] == 8 and e['mode'] == 'node' for e in done)
+    assert done and all(e['n'] == 8 and e['mode'] == 'node' and
+                        e['transport'] == transport for e in done)
     assert sum(1 for e in records if e['ev'] == 'node_comm_ready') == 2
     breaks = [e for e in records if e['ev'] == 'node_comm_break']
     assert len(breaks) == 1 and not breaks[0]['failed']
@@ -409,3 +412,62 @@ def test_gpu_node_comm_through_the_manager(resp_server):
     assert done and all(e['transport'] == 'rccl' and e['mode'] == 'node'
                         for e in done)
     assert max(e['wall_s'] for e in done) < 0.05
+
+
+_RANK_SCRIPT = r'''
+import json, os, sys, time
+sys.path.insert(0, os.environ['KIOSK_ROOT'])
+from kiosk_autoscaler_amd.ops import native
+mod = native.load()
+rank, path = int(sys.argv[1]), sys.argv[2]
+fence = mod.Fence(2, rank, 20.0)
+if rank == 0:
+    with open(path + '.tmp', 'w') as f:
+        f.write(mod.fence_unique_id().hex())
+    os.rename(path + '.tmp', path)
+else:
+    while not os.path.exists(path):
+        time.sleep(0.01)
+uid = bytes.fromhex(open(path).read())
+t0 = time.time()
+try:
+    fence.connect(uid)
+    out, _ = fence.allreduce([1, rank + 1])
+    fence.destroy()
+    print(json.dumps({'rank': rank, 'ok': True, 'out': out}))
+except RuntimeError as err:
+    fence.destroy()          # after a failed init: frees, never double-aborts
+    print(json.dumps({'rank': rank, 'ok': False, 'error': str(err),
+                      's': time.time() - t0}))
+'''
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_init_failure_is_contained(tmp_path):
+    """Two ranks on ONE MI355X: RCCL refuses the communicator (duplicate
+    GPU).  The failure must come back as an exception from the two-phase
+    connect -- no hang, no crash, no double abort (ADVICE r1 high) -- the
+    same path a generation whose peer died mid-init takes.  Should this RCCL
+    accept the pair instead, the all-reduce must be right."""
+    import json as _json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / 'rank.py'
+    script.write_text(_RANK_SCRIPT)
+    env = dict(os.environ, KIOSK_ROOT=root)
+    uid = str(tmp_path / 'uid')
+    procs = [subprocess.Popen([sys.executable, str(script), str(r), uid],
+                              env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True)
+             for r in range(2)]
+    results = []
+    for proc in procs:
+        out, err = proc.communicate(timeout=100)
+        assert proc.returncode == 0, err[-2000:]
+        results.append(_json.loads(out.strip().splitlines()[-1]))
+    if all(r['ok'] for r in results):
+        assert all(r['out'] == [2, 3] for r in results)
+    else:
+        assert not any(r['ok'] for r in results), results
+        assert all(r['s'] < 30.0 for r in results), results
