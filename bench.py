@@ -159,6 +159,8 @@ class Services(object):
             'IDLE_INTERVAL': str(args.idle_interval),
             'GPU_IDS': ','.join(str(i) for i in range(n_gpus)),
             'WORKER_BACKEND': args.backend, 'WARM_POOL': str(pool),
+            'WARM_POOL_MODE': args.pool_mode,
+            'WORKER_RECYCLE': '0' if args.no_recycle else '1',
             'FENCE': args.fence, 'MODEL_DIM': str(args.dim),
             'MODEL_HIDDEN': str(args.hidden), 'MODEL_LAYERS': str(args.layers),
             'ROWS_PER_KEY': str(args.rows), 'EVENT_LOG': 'redis',
@@ -405,6 +407,13 @@ def parse_args():
                    help='opt-in fast poll while at zero workers (changes the '
                         "reference's INTERVAL semantics; reported separately)")
     p.add_argument('--resource-type', default='deployment')
+    p.add_argument('--pool-mode', default='device',
+                   help="standby preinit: 'device' (HIP context + code "
+                        "objects: fastest READY, holds the GPU) or 'import' "
+                        "(imports only: holds nothing)")
+    p.add_argument('--no-recycle', action='store_true',
+                   help='drained workers exit (a fresh standby replaces '
+                        'them) instead of returning to the pool')
     p.add_argument('--backend', default='hip')
     p.add_argument('--fence', default='auto')
     p.add_argument('--dim', type=int, default=4096)
@@ -556,6 +565,8 @@ def base_line(args, episodes, elapsed):
             'max_pods': args.gpus, 'keys_per_pod': args.kpp,
             'policy': args.policy, 'resource_type': args.resource_type,
             'idle_interval_s': args.idle_interval,
+            'warm_pool_mode': args.pool_mode,
+            'worker_recycle': not args.no_recycle,
         },
         'steps_requested': args.steps,
     }

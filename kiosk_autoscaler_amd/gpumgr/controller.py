@@ -285,9 +285,12 @@ class GpuManager(object):
         # every epoch bootstraps its own communicator (round-1 mode)
         self.fence_comm = fence_comm
         self.node = None
+        # (an import-mode standby must not create a HIP context: a
+        # communicator in it would, so that mode fences per epoch)
         if (fence and fence_comm == 'node' and self.recycle and
                 pool_template is not None and self.slots and
-                self.pool_size >= len(self.slots)):
+                self.pool_size >= len(self.slots) and
+                (pool_mode == 'device' or pool_template.backend == 'cpu')):
             self.node = NodeComm(self, fence_timeout=min(fence_timeout, 30.0))
 
     # ------------------------------------------------------------------

@@ -114,6 +114,7 @@ class HipMlpEngine(object):
         if stage:
             stage('native_loaded')
         self.cfg = cfg
+        self.reused = False     # served an earlier assignment (engine cache)
         self.engine = mod.Engine(0, cfg.dim, cfg.hidden, cfg.layers,
                                  max(cfg.rows * cfg.batch, 256), cfg.seed)
         self.pass_ms = {}
@@ -126,10 +127,14 @@ class HipMlpEngine(object):
         info = dict(self.engine.warmstart())
         # capture the default-shape forward and run it once: every code
         # object is loaded and the graph instantiated, so the first key
-        # after READY is a single graph launch per pass
-        self.engine.prepare(self.cfg.rows)
-        self.measure(self.cfg.rows)
+        # after READY is a single graph launch per pass.  A reused engine
+        # (weights, graph and pass time from its last assignment) only
+        # re-runs the warm-start kernel.
+        if not (self.reused and self.cfg.rows in self.pass_ms):
+            self.engine.prepare(self.cfg.rows)
+            self.measure(self.cfg.rows, passes=1)
         info['pass_ms'] = self.pass_ms[self.cfg.rows]
+        info['reused'] = self.reused
         return info
 
     def measure(self, rows, passes=2):

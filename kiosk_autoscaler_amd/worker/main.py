@@ -54,6 +54,45 @@ def _preload(backend):
 
 
 _CLIENTS = {}
+# HIP engines kept across recycles (WORKER_KEEP_ENGINE=1): the recycled
+# standby's next assignment with the same model finds its weights, graph
+# and pass time resident and only re-runs the warm-start kernel
+_ENGINES = {}
+
+
+def _engine_key(backend, cfg):
+    if backend != 'hip':
+        return None
+    return ('hip', cfg.dim, cfg.hidden, cfg.layers,
+            max(cfg.rows * cfg.batch, 256), cfg.seed)
+
+
+def _cached_engine(backend, cfg, stage):
+    """An engine for this assignment: the cached one when the model and its
+    capacity match (anything else cached is freed first), else a new one."""
+    from ..models.mlp import create_engine
+    key = _engine_key(backend, cfg)
+    keep = os.environ.get('WORKER_KEEP_ENGINE', '1') not in ('0', '')
+    if key is not None and keep and key in _ENGINES and \
+            getattr(_ENGINES[key], 'engine', None) is not None:
+        engine = _ENGINES[key]
+        engine.reused = True
+        engine.cfg = cfg
+        return engine
+    for old in list(_ENGINES.values()):
+        old.close()
+    _ENGINES.clear()
+    engine = create_engine(backend, cfg, stage)
+    if key is not None and keep:
+        _ENGINES[key] = engine
+    return engine
+
+
+def _release_engine(engine):
+    """End of an assignment: a cached engine stays resident (freed when the
+    process exits or a different model needs the HBM)."""
+    if engine is not None and engine not in _ENGINES.values():
+        engine.close()
 
 
 def _process_redis(role, host=None, port=None):
@@ -279,7 +318,6 @@ def _serve(assignment, backend, channel, node_agent=None):
     apply_assignment_env(assignment)
     config = WorkerConfig(os.environ, assignment)
 
-    from ..models.mlp import create_engine
     from ..utils.events import EventLog
 
     def redis_factory():
@@ -297,7 +335,7 @@ def _serve(assignment, backend, channel, node_agent=None):
                           source=config.worker_id)
 
     def engine_factory(cfg, stage):
-        return create_engine(backend, cfg, stage)
+        return _cached_engine(backend, cfg, stage)
 
     faults = None
     if os.environ.get('KIOSK_FAULTS'):
@@ -308,7 +346,8 @@ def _serve(assignment, backend, channel, node_agent=None):
                             fence_factory=(None if node_agent is not None
                                            else _build_fence_factory(config)),
                             event_log=events, faults=faults,
-                            node_agent=node_agent)
+                            node_agent=node_agent,
+                            engine_release=_release_engine)
     code = runtime.run()
     if events is not None:
         events.emit('worker_exit_self', worker=config.worker_id,

@@ -137,7 +137,7 @@ class WorkerRuntime(object):
 
     def __init__(self, config, engine_factory, channel, redis_factory,
                  fence_factory=None, event_log=None, faults=None,
-                 node_agent=None):
+                 node_agent=None, engine_release=None):
         self.config = config
         self.faults = faults
         self.engine_factory = engine_factory
@@ -149,6 +149,9 @@ class WorkerRuntime(object):
         self.fence_agent = None
         # process-lifetime agent of the node communicator (not ours to close)
         self.node_agent = node_agent
+        # how an assignment gives its engine back (default: close it; the
+        # worker process may keep it resident for its next assignment)
+        self.engine_release = engine_release or (lambda e: e.close())
         self.draining = False
         # back to the standby pool after a clean finish (manager's call:
         # set by the assignment, overridden by the drain command)
@@ -223,7 +226,7 @@ class WorkerRuntime(object):
             self.channel.emit('error', message='%s: %s' % (
                 type(err).__name__, err))
             if self.engine is not None:
-                self.engine.close()
+                self.engine.close()   # never cache a failed start
             return 3
         consumer = QueueConsumer(self.redis, cfg.worker_id, cfg.queues,
                                  cfg.poll_block)
@@ -265,7 +268,7 @@ class WorkerRuntime(object):
                         not self.fence_agent.close():
                     self.recycle = False  # a collective may still be running
             if self.engine is not None:
-                self.engine.close()
+                self.engine_release(self.engine)
         return 0
 
     def max_rows(self):

@@ -357,3 +357,39 @@ def test_splitk_dispatch(mod):
     # two fp32 partial planes + one ticket counter per 256x256 tile
     assert mod.gemm_workspace_bytes(2048, 4096, 16384) == \
         2 * 2048 * 4096 * 4 + 512
+
+
+def test_engine_cache_across_assignments(mod):
+    """A recycled worker keeps its engine (weights, captured graph, pass
+    time): the next assignment with the same model reuses it and re-runs
+    only the warm-start kernel; a different model frees it first."""
+    import time
+    from kiosk_autoscaler_amd.worker import main as wmain
+    from kiosk_autoscaler_amd.worker.runtime import WorkerConfig
+    env = {'MODEL_DIM': '1024', 'MODEL_HIDDEN': '4096', 'MODEL_LAYERS': '2',
+           'ROWS_PER_KEY': '256'}
+    cfg = WorkerConfig(env, {'worker_id': 'w-g0-a-1'})
+    wmain._ENGINES.clear()
+    first = wmain._cached_engine('hip', cfg, None)
+    try:
+        info = first.warmstart()
+        assert info['reused'] is False
+        wmain._release_engine(first)               # kept, not closed
+        assert first.engine is not None
+        t0 = time.perf_counter()
+        again = wmain._cached_engine('hip', WorkerConfig(
+            env, {'worker_id': 'w-g0-a-2'}), None)
+        info = again.warmstart()
+        reuse_ms = (time.perf_counter() - t0) * 1e3
+        assert again is first and info['reused'] is True
+        assert info['cus_touched'] > 0 and reuse_ms < 50.0
+        out = again.forward(256, 1, 3)
+        assert out['gpu_ms'] > 0
+        other = wmain._cached_engine('hip', WorkerConfig(
+            dict(env, MODEL_LAYERS='1'), {'worker_id': 'w-g0-a-3'}), None)
+        assert other is not first and first.engine is None   # evicted
+        wmain._release_engine(other)
+    finally:
+        for eng in list(wmain._ENGINES.values()):
+            eng.close()
+        wmain._ENGINES.clear()
