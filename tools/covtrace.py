@@ -118,6 +118,30 @@ def executable_lines(path):
     return lines - excluded
 
 
+def _package_files(package=PACKAGE):
+    for base, dirs, files in os.walk(package):
+        dirs[:] = [d for d in dirs if d != '__pycache__']
+        for name in files:
+            if name.endswith('.py'):
+                yield os.path.join(base, name)
+
+
+def _ranges(numbers):
+    out, start, prev = [], None, None
+    for n in numbers:
+        if start is None:
+            start = prev = n
+        elif n == prev + 1:
+            prev = n
+        else:
+            out.append(str(start) if start == prev else '%d-%d' % (start,
+                                                                    prev))
+            start = prev = n
+    if start is not None:
+        out.append(str(start) if start == prev else '%d-%d' % (start, prev))
+    return ','.join(out)
+
+
 def report(tracer, package=PACKAGE):
     rows = []
     total_exec = total_hit = 0
@@ -148,6 +172,9 @@ def main(argv=None):
     parser.add_argument('--fail-under', type=float, default=80.0)
     parser.add_argument('--output', default=None,
                         help='also write the table to this file')
+    parser.add_argument('--missing', default='',
+                        help='comma-separated file name fragments: list '
+                             'their never-executed lines')
     args = parser.parse_args(argv)
     sys.path.insert(0, ROOT)
     import tempfile
@@ -170,6 +197,12 @@ def main(argv=None):
     for path, n, hit, pct in rows:
         lines.append('%-52s %6d %6d %5.1f%%' % (path, n, hit, pct))
     lines.append('%-52s %6s %6s %5.1f%%' % ('TOTAL', '', '', total))
+    for frag in filter(None, args.missing.split(',')):
+        for path in sorted(p for p in _package_files() if frag in p):
+            missed = sorted(executable_lines(path) -
+                            tracer.hits.get(path, set()))
+            lines.append('missing %s: %s' % (os.path.relpath(path, ROOT),
+                                             _ranges(missed)))
     text = '\n'.join(lines)
     print(text)
     if args.output:
