@@ -471,3 +471,58 @@ def test_gpu_rccl_init_failure_is_contained(tmp_path):
     else:
         assert not any(r['ok'] for r in results), results
         assert all(r['s'] < 30.0 for r in results), results
+
+
+@pytest.mark.slow
+def test_two_resources_share_the_node_communicator(resp_server):
+    """Two resources (one queue each) on one manager with a standby per
+    slot: both get a worker, both READY sets are fenced over the one node
+    communicator (epochs serialized node-wide, other slots contribute
+    zeros) and published under their own keys; no second generation."""
+    from kiosk_autoscaler_amd import gpumgr
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'qa', 'RESOURCE_NAME': 'a', 'MAX_PODS': '2',
+           'WORKER_BACKEND': 'cpu', 'WARM_POOL': '2', 'FENCE': 'store',
+           'REDIS_INTERVAL': '0'}
+    s = Settings(Config(environ=env, use_files=False))
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    events = EventLog(source='test')
+    events.keep = True
+    manager = gpumgr.build_manager(s, redis_client=client, events=events)
+    other = Settings(Config(environ=dict(env, QUEUES='qb', RESOURCE_NAME='b'),
+                            use_files=False))
+    manager.register('deployment', 'default', 'b',
+                     gpumgr.template_for(other, 'cpu'))
+    manager.start()
+    try:
+        wait_for(lambda: manager.node.ready, timeout=60)
+        for name in ('a', 'b'):
+            manager.patch_namespaced_deployment(name, 'default',
+                                                {'spec': {'replicas': 1}})
+        for name in ('a', 'b'):
+            wait_for(lambda: (client.get('kiosk:active:default:%s' % name)
+                              and len(json.loads(client.get(
+                                  'kiosk:active:default:%s' % name))
+                                  ['members']) == 1), timeout=30)
+        members = [json.loads(client.get('kiosk:active:default:%s' % n))
+                   ['members'][0] for n in ('a', 'b')]
+        assert members[0].startswith('a-g') and members[1].startswith('b-g')
+        assert {m.split('-g')[1][0] for m in members} == {'0', '1'}
+        for name in ('a', 'b'):
+            manager.patch_namespaced_deployment(name, 'default',
+                                                {'spec': {'replicas': 0}})
+        for name in ('a', 'b'):
+            wait_for(lambda: json.loads(client.get(
+                'kiosk:active:default:%s' % name))['members'] == [],
+                timeout=30)
+        assert manager.node.generations == 1
+    finally:
+        manager.stop(timeout=15)
+    done = [e for e in events.records if e['ev'] == 'fence_done']
+    assert len(done) >= 2 and all(e['n'] == 2 for e in done)
+    seqs = [e['seq'] for e in events.records if e['ev'] == 'fence_start']
+    assert seqs == sorted(seqs) and len(set(seqs)) == len(seqs)
