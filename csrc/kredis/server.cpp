@@ -1171,7 +1171,19 @@ int Server::run(const std::string& bind_addr, int port) {
   fflush(stdout);
   std::vector<epoll_event> events(256);
   while (!shutdown_ && !g_terminate) {
-    int timeout = blocked_order_.empty() ? 1000 : 10;
+    // sleep until the nearest blocked client's deadline (1 ms resolution),
+    // so a BLMOVE with a 5 ms bound returns after 5 ms, not the next 10 ms
+    int timeout = 1000;
+    if (!blocked_order_.empty()) {
+      const int64_t now = now_ms();
+      for (int bfd : blocked_order_) {
+        auto bit = clients_.find(bfd);
+        if (bit == clients_.end() || !bit->second->deadline) continue;
+        const int64_t left = bit->second->deadline - now;
+        timeout = static_cast<int>(std::max<int64_t>(
+            0, std::min<int64_t>(timeout, left)));
+      }
+    }
     int n = epoll_wait(epfd_, events.data(), static_cast<int>(events.size()),
                        timeout);
     if (n < 0 && errno != EINTR) break;

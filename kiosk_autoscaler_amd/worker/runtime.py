@@ -77,8 +77,9 @@ class WorkerConfig(object):
         # forward chunk size (ms) while a fence epoch is in flight (0 = off)
         self.fence_chunk_ms = _env_float(env, 'FENCE_YIELD_CHUNK_MS', 2.0)
         # how long an idle worker blocks in BLMOVE: bounds drain latency
-        # (the drain command waits for it: it bounds scale-down latency)
-        self.poll_block = _env_float(env, 'POLL_BLOCK_S', 0.02)
+        # (the drain command waits for it: it bounds scale-down latency;
+        # kredis honours it to the millisecond)
+        self.poll_block = _env_float(env, 'POLL_BLOCK_S', 0.005)
         self.job_idle_exit = _env_float(env, 'JOB_IDLE_EXIT_S', 1.0)
         self.mock_work_ms = _env_float(env, 'MOCK_WORK_MS', 0.0)
         self.record_events = env.get('WORKER_EVENTS', '1') not in ('0', '')
