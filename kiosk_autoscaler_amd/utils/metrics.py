@@ -7,7 +7,8 @@ the manager daemon can serve ``/metrics``:
 * from the event stream (an :class:`~.events.EventLog` observer): queue
   depth and in-flight keys per queue, desired / current workers, tick
   duration, scale events, assignment -> READY latency, worker exits by
-  outcome, requeued items, watchdog kills, fence epochs and their duration;
+  outcome, requeued items, watchdog kills, fence epochs and their duration,
+  node-communicator generations / breaks / init time, free-HBM sizing;
 * at scrape time from the GPU manager: workers per state, standbys
   (booted / booting), GPU slots.
 
@@ -57,6 +58,21 @@ class PrometheusExporter(object):
         self.fence_seconds = Histogram('kiosk_fence_seconds', 'fence epoch '
                                        'start -> rank-0 ack', registry=r,
                                        buckets=LATENCY_BUCKETS)
+        self.comm_builds = Counter('kiosk_node_comm_generations',
+                                   'node communicators built (pool boot, '
+                                   'then one per slot-process death)',
+                                   registry=r)
+        self.comm_breaks = Counter('kiosk_node_comm_breaks', 'node '
+                                   'communicator generations dropped',
+                                   ['failed'], registry=r)
+        self.comm_init_seconds = Histogram(
+            'kiosk_node_comm_init_seconds', 'slowest rank of a generation',
+            registry=r, buckets=LATENCY_BUCKETS)
+        self.hbm_free = Gauge('kiosk_hbm_free_bytes', 'free HBM a standby '
+                              'measured at its last assignment', ['gpu'],
+                              registry=r)
+        self.kpp = Gauge('kiosk_keys_per_pod_effective', 'KEYS_PER_POD '
+                         'after free-HBM sizing', ['gpu'], registry=r)
         if manager is not None:
             r.register(_ManagerCollector(manager))
         self.port = None
@@ -106,6 +122,17 @@ class PrometheusExporter(object):
             self.fences.labels(str(record.get('transport'))).inc()
             if record.get('wall_s') is not None:
                 self.fence_seconds.observe(record['wall_s'])
+        elif ev == 'node_comm_ready':
+            self.comm_builds.inc()
+            self.comm_init_seconds.observe(
+                float(record.get('init_ms') or 0.0) / 1e3)
+        elif ev == 'node_comm_break':
+            self.comm_breaks.labels(
+                str(bool(record.get('failed'))).lower()).inc()
+        elif ev == 'hbm_sizing':
+            gpu = str(record.get('gpu'))
+            self.hbm_free.labels(gpu).set(record.get('hbm_free') or 0)
+            self.kpp.labels(gpu).set(record.get('keys_per_pod') or 0)
 
 
 class _ManagerCollector(object):

@@ -31,7 +31,16 @@ def test_exporter_counts_events_and_serves_http():
     events.emit('worker_exit', code=-9, killed='no progress')
     events.emit('requeue', items=2)
     events.emit('fence_done', transport='rccl', wall_s=0.05)
+    events.emit('node_comm_ready', gen=1, n=8, init_ms=1900.0)
+    events.emit('node_comm_break', gen=1, failed=False)
+    events.emit('hbm_sizing', gpu=0, hbm_free=2.8e11, keys_per_pod=4)
     text = generate_latest(exporter.registry).decode()
+    for line in ('kiosk_node_comm_generations_total 1.0',
+                 'kiosk_node_comm_breaks_total{failed="false"} 1.0',
+                 'kiosk_node_comm_init_seconds_count 1.0',
+                 'kiosk_hbm_free_bytes{gpu="0"} 2.8e+11',
+                 'kiosk_keys_per_pod_effective{gpu="0"} 4.0'):
+        assert line in text, line
     for line in ('kiosk_queue_keys{queue="q"} 4.0',
                  'kiosk_in_progress_keys{queue="q"} 1.0',
                  'kiosk_desired_workers 3.0',
