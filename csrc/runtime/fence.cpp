@@ -313,17 +313,18 @@ void Fence::destroy() {
       abort();   // a peer is gone: finalize would wait on it
     }
   }
+  // teardown: nothing useful to do with an error here
   if (stream_) {
-    hipStreamSynchronize(stream_);
-    hipStreamDestroy(stream_);
+    (void)hipStreamSynchronize(stream_);
+    (void)hipStreamDestroy(stream_);
     stream_ = nullptr;
   }
   if (dev_) {
-    hipFree(dev_);
+    (void)hipFree(dev_);
     dev_ = nullptr;
   }
   if (host_) {
-    hipHostFree(host_);
+    (void)hipHostFree(host_);
     host_ = nullptr;
   }
 }

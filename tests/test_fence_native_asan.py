@@ -1,0 +1,47 @@
+"""csrc/runtime/fence.cpp under AddressSanitizer + UBSan on the host (CPU):
+the fence's failure paths -- async init error, init timeout, abort
+requested before connect or during a blocked all-reduce, all-reduce
+timeout, stuck finalize -- against a fake HIP + RCCL library whose
+communicators are heap objects, so any double abort or use after abort
+ is an ASan report.  GPU code is not involved: the pool has
+no GPU sanitizer; this is the host half of SURVEY §5.2."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+
+def test_fence_failure_paths_under_asan(tmp_path):
+    cxx = shutil.which('g++')
+    if cxx is None or not os.path.exists('/opt/rocm/include/rccl/rccl.h'):
+        pytest.skip('needs g++ and the ROCm headers')
+    san = ['-fsanitize=address,undefined', '-fno-sanitize-recover=undefined',
+           '-fno-omit-frame-pointer', '-g', '-O1']
+    inc = ['-std=c++17', '-D__HIP_PLATFORM_AMD__', '-I/opt/rocm/include',
+           '-I' + os.path.join(ROOT, 'csrc', 'runtime')]
+    fake = str(tmp_path / 'libkiosk_fake_hip_rccl.so')
+    native = os.path.join(ROOT, 'tests', 'native')
+    subprocess.run([cxx] + san + inc + ['-shared', '-fPIC',
+                   os.path.join(native, 'fake_hip_rccl.cpp'), '-o', fake],
+                   check=True, timeout=300)
+    exe = str(tmp_path / 'fence_asan')
+    subprocess.run([cxx] + san + inc + [
+        os.path.join(native, 'fence_asan_main.cpp'),
+        os.path.join(ROOT, 'csrc', 'runtime', 'fence.cpp'),
+        os.path.join(ROOT, 'csrc', 'runtime', 'trace.cpp'),
+        fake, '-Wl,-rpath,' + str(tmp_path), '-ldl', '-pthread', '-o', exe],
+        check=True, timeout=300)
+    env = dict(os.environ, KIOSK_RCCL_LIB=fake, KIOSK_ROCTX='0',
+               ASAN_OPTIONS='detect_leaks=1:abort_on_error=0',
+               UBSAN_OPTIONS='print_stacktrace=1:halt_on_error=1')
+    proc = subprocess.run([exe], env=env, stdout=subprocess.PIPE,
+                          stderr=subprocess.PIPE, text=True, timeout=120)
+    text = proc.stdout + proc.stderr
+    assert proc.returncode == 0, text[-4000:]
+    assert 'PASSED: 0 failure(s)' in proc.stdout, text[-4000:]
+    assert 'AddressSanitizer' not in text and 'runtime error' not in text
+    assert proc.stdout.count('ok ') >= 14
