@@ -215,7 +215,14 @@ def main(argv=None):
     from . import build_manager
     parser = argparse.ArgumentParser(description=__doc__)
     parser.add_argument('--socket', default='/tmp/kiosk-gpumgr.sock')
+    parser.add_argument('--status', action='store_true',
+                        help='print the running daemon\'s status (slots, '
+                             'standbys, resources, workers) as JSON and exit')
     args = parser.parse_args(argv)
+    if args.status:
+        print(json.dumps(GpuManagerClient(args.socket).status(), indent=1,
+                         default=str))
+        return 0
     settings = Settings(require_resource_name=False)
     initialize_logger(settings.DEBUG, log_file='')
     # the manager needs Redis for requeue, persisted state, orphan recovery

@@ -109,6 +109,17 @@ def test_daemon_transport(tmp_path):
         assert client.status()['slots'][0]['kind'] == 'cpu'
         assert gpumgr.connect('unix:' + path).list_namespaced_deployment(
             'ns').items == []
+        # operator view: `python -m kiosk_autoscaler_amd.gpumgr.daemon
+        # --status --socket PATH`
+        import contextlib
+        import io
+        import json
+        from kiosk_autoscaler_amd.gpumgr import daemon
+        out = io.StringIO()
+        with contextlib.redirect_stdout(out):
+            assert daemon.main(['--status', '--socket', path]) == 0
+        status = json.loads(out.getvalue())
+        assert status['resources'][0]['metadata']['name'] == 'w'
     finally:
         server.stop()
     with pytest.raises(ActuatorError) as info:
