@@ -443,6 +443,7 @@ def main():
     error = None
     episodes = []
     elapsed = 0.0
+    warmups_done = [0]
     try:
         if rank == 0:
             # everything that forks runs before this process touches the GPU
@@ -485,11 +486,15 @@ def main():
                                 service_ms=args.service_ms, rows=args.rows,
                                 seed=args.seed)
             for w in range(args.warmup):
-                if w and not budget.fits(budget.cycle_max + 3 * args.interval):
+                # on a slow boot the timed steps keep priority: a warmup
+                # beyond the first runs only if it leaves room for them
+                cycle = max(budget.cycle_max, 2 * args.interval + args.on)
+                if w and not budget.fits(cycle * (1 + min(args.steps, 10))):
                     log('budget: skipping warmup %d..' % w)
                     break
                 run_cycle(svc, gen, args, 0.5 * args.interval, 0.0,
                           'warmup %d' % w, budget)
+                warmups_done[0] += 1
         sampler = start_util_sampler(args.gpus) if rank == 0 else None
         barrier()
         sync()
@@ -529,6 +534,7 @@ def main():
     if rank == 0:
         if line is None:
             line = base_line(args, episodes, elapsed)
+        line['warmup_done'] = warmups_done[0]
         if error:
             line['error'] = error
         print(json.dumps(line), flush=True)
