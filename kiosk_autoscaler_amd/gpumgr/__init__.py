@@ -64,7 +64,8 @@ def worker_env(settings, keys_per_pod=None):
     for passthrough in ('PASSES_PER_KEY', 'MOCK_WORK_MS', 'WORKER_BATCH',
                         'JOB_IDLE_EXIT_S', 'POLL_BLOCK_S', 'MODEL_SEED',
                         'KIOSK_RCCL_LIB', 'WORKER_EVENTS', 'KIOSK_FAULTS',
-                        'KIOSK_ROCTX', 'WORKER_KEEP_ENGINE'):
+                        'KIOSK_ROCTX', 'WORKER_KEEP_ENGINE',
+                        'WORKER_IMPORT_TORCH'):
         if passthrough in os.environ:
             env[passthrough] = os.environ[passthrough]
     return env

@@ -1,12 +1,16 @@
 """Loader for the in-tree native module ``_kiosk_hip`` (HIP/gfx950 + RCCL).
 
 Load order matters: PyTorch-ROCm bundles its own ``libamdhip64.so`` (SONAME
-``libamdhip64.so.7``).  Importing torch first makes the extension's
-``libamdhip64.so.7`` dependency resolve to that already-loaded runtime, so
-one HIP runtime serves both (two runtimes in one process would each own the
-device).  RCCL is *not* a link-time dependency: the fence code ``dlopen``s a
-full RCCL (``KIOSK_RCCL_LIB``, default ROCm's, which has
-``ncclCommShrink``) with ``RTLD_LOCAL``.
+``libamdhip64.so.7``).  In a process that uses torch, importing torch first
+makes the extension's ``libamdhip64.so.7`` dependency resolve to that
+already-loaded runtime, so one HIP runtime serves both (two runtimes in one
+process would each own the device).  The worker never uses torch: it loads
+the extension with ``torch_first=False`` and runs on ROCm's own runtime (the
+one the extension was compiled against), which takes the ~1.5 s torch
+import -- minutes on a fresh node -- off standby boot and cold spawns.
+RCCL is *not* a link-time dependency: the fence code ``dlopen``s a full RCCL
+(``KIOSK_RCCL_LIB``, default ROCm's, which has ``ncclCommShrink``) with
+``RTLD_LOCAL``.
 
 There is no silent fallback: on a machine with a GPU a missing or stale
 extension raises :class:`NativeUnavailable` with the build command.
@@ -30,18 +34,21 @@ def extension_candidates():
     return sorted(glob.glob(os.path.join(HERE, '_kiosk_hip*.so')))
 
 
-def load():
-    """Import and return the native module (cached)."""
+def load(torch_first=True):
+    """Import and return the native module (cached; the first call decides
+    the load order).  ``torch_first=False`` is for processes that never
+    import torch (the worker)."""
     global _MOD
     if _MOD is not None:
         return _MOD
     if not extension_candidates():
         raise NativeUnavailable('native module _kiosk_hip is not built; '
                                 + BUILD_HINT)
-    try:
-        import torch  # noqa: F401  -- must precede the extension (see above)
-    except ImportError:
-        pass
+    if torch_first:
+        try:
+            import torch  # noqa: F401  -- must precede the extension
+        except ImportError:
+            pass
     try:
         _MOD = importlib.import_module('kiosk_autoscaler_amd.ops._kiosk_hip')
     except ImportError as err:

@@ -42,12 +42,15 @@ def _die_with_parent():
 
 
 def _preload(backend):
-    """Import everything heavy *without* touching the GPU."""
+    """Import everything heavy *without* touching the GPU.  The HIP worker
+    needs only the native module (engine, fence): no torch import unless
+    ``WORKER_IMPORT_TORCH=1`` (then torch's bundled HIP runtime is shared)."""
     t0 = time.monotonic_ns()
     if backend == 'hip':
-        import torch  # noqa: F401  -- shares libamdhip64 with the extension
         from ..ops import native
-        native.load()
+        with_torch = os.environ.get('WORKER_IMPORT_TORCH', '0') not in (
+            '0', '')
+        native.load(torch_first=with_torch)
     else:
         import numpy  # noqa: F401
     return time.monotonic_ns() - t0
