@@ -11,14 +11,14 @@ this module plays API server + controller + kubelet:
   ``HIP_VISIBLE_DEVICES`` and CPU affinity to the GPU's NUMA-local cores.
   The lowest free GPU index is allocated first.
 * **Warm pool**: ``pool_size`` standby processes, each pinned to its GPU
-  at spawn, have imported PyTorch-ROCm and the native kernel module.  With
+  at spawn, have imported the native kernel module (not PyTorch).  With
   ``WARM_POOL_MODE=device`` (the default) they have also created the HIP
   context and loaded every code object, so **a standby holds its GPU**
   (context and code objects, no weights; the benchmark reports this as
   ``standby_gpu_s``); with ``import`` they stop before HIP and hold none.
-  A scale-up hands a standby its assignment over a pipe, taking the ~1.6 s
-  interpreter/torch import and the HIP init off the critical path (SURVEY
-  §7.4 item 4).  Standbys do not count as replicas.
+  A scale-up hands a standby its assignment over a pipe, taking process
+  start, imports and the HIP init (0.27 s together) off the critical path
+  (SURVEY §7.4 item 4).  Standbys do not count as replicas.
 * **READY** (``status.available_replicas``) means the worker has its
   weights in HBM and has run the warm-start kernel.
 * **Scale-down** drains: the worker finishes its in-flight key and exits.

@@ -3,7 +3,7 @@
 Two start modes (both spawned by :mod:`kiosk_autoscaler_amd.gpumgr`):
 
 * **standby** (``--pin JSON``, no ``--assign``): pinned to its GPU before
-  anything loads, import PyTorch-ROCm and the native kernel module and --
+  anything loads, import the native kernel module (not PyTorch) and --
   with ``WARM_POOL_MODE=device``, the default -- create the HIP context,
   load every code object and size the LDS ring (``preinit_device``).  Such a
   standby **holds its GPU** (context + code objects, no weights); the
