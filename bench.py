@@ -359,11 +359,18 @@ def reference_sim(episodes, events, args, same_grid=True):
             ready_delay=0.0, max_pods=args.gpus, keys_per_pod=args.kpp,
             queues=args.queues.split(','), policy='reference',
             tick_s=0.0, dt=0.001, **kwargs))
-    lat = [r['cold_start_mean_s'] for r in results
-           if r['cold_start_mean_s'] is not None]
-    idle = [r['gpu_idle_pct'] for r in results if r['gpu_idle_pct'] is not None]
-    return {'latency_mean_s': sum(lat) / len(lat) if lat else None,
-            'gpu_idle_pct': sum(idle) / len(idle) if idle else None,
+    # aggregate exactly like the live metrics: latency over all cold starts,
+    # idle = (sum alive - sum busy) / sum alive (a mean of per-episode
+    # percentages would weight a 1-worker cycle like an 8-worker one)
+    n_cold = sum(r['cold_starts'] for r in results
+                 if r['cold_start_mean_s'] is not None)
+    lat_sum = sum(r['cold_start_mean_s'] * r['cold_starts'] for r in results
+                  if r['cold_start_mean_s'] is not None)
+    alive = sum(r['alive_s'] for r in results)
+    busy = sum(r['busy_s'] for r in results)
+    return {'latency_mean_s': lat_sum / n_cold if n_cold else None,
+            'gpu_idle_pct': 100.0 * (alive - busy) / alive if alive else None,
+            'alive_s': alive, 'busy_s': busy,
             'grid': 'live tick instants' if same_grid else 'ideal',
             'ready_delay_s': 0.0, 'episodes': results}
 

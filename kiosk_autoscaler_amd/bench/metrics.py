@@ -91,7 +91,11 @@ def episode_metrics(events, episode):
     waits = [(start[item] - t) / 1e9 for item, _, t in episode['keys']
              if item in start]
     colds = cold_starts(events, episode['keys'], t0, t_end)
+    _, ep_alive, ep_busy = gpu_idle(events, t0 - int(episode.get(
+        'lead_ns', 0)), t_end)
     out = {
+        't_first': t0, 't_end': t_end,
+        'alive_s': ep_alive, 'busy_s': ep_busy,
         'latency_s': (ready[0] - t0) / 1e9 if ready else None,
         'cold_starts_s': [(b - a) / 1e9 for a, b in colds],
         'decision_s': (scale[0] - t0) / 1e9 if scale else None,

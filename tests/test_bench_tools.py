@@ -151,6 +151,15 @@ def test_bench_cpu_smoke(tmp_path):
     assert line['keys_done'] == line['keys'] > 0
     assert line['value'] is not None and line['value'] < 1.0
     assert (tmp_path / 'bench_detail_n1.json').exists()
+    # the reference simulation is aggregated like the live metrics
+    detail = json.loads((tmp_path / 'bench_detail_n1.json').read_text())
+    ref = detail['reference_sim']
+    assert ref['gpu_idle_pct'] == pytest.approx(
+        100.0 * (ref['alive_s'] - ref['busy_s']) / ref['alive_s'])
+    assert line['baseline_gpu_idle_pct'] == pytest.approx(
+        ref['gpu_idle_pct'], abs=1e-3)
+    ep = detail['summary']['episodes'][0]
+    assert ep['alive_s'] > 0 and ep['t_end'] > ep['t_first']
 
 
 @pytest.mark.slow
