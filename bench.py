@@ -183,6 +183,14 @@ class Services(object):
         if pool:
             wait_for(self.pool_ready, timeout, step=0.2,
                      what='standby pool boot')
+            # the node communicator's first generation pays RCCL's one-time
+            # init (~2 s; its code-object load slows an engine built
+            # meanwhile): let it finish, bounded -- a broken communicator
+            # only costs fences, never the run
+            deadline = time.time() + 30.0
+            while time.time() < deadline and self.node_state() not in (
+                    'ready', 'off', None):
+                time.sleep(0.1)
 
     def stop_scaler(self):
         proc = self.scaler_proc
@@ -217,8 +225,13 @@ class Services(object):
         value = self.redis.get('kiosk:pool')
         if not value:
             return False
-        booted, _total = (int(v) for v in value.split())
+        booted, _total = (int(v) for v in value.split()[:2])
         return booted >= self.pool
+
+    def node_state(self):
+        value = self.redis.get('kiosk:pool')
+        fields = value.split() if value else []
+        return fields[2] if len(fields) > 2 else None
 
     def idle(self):
         if any(True for _ in self.redis.scan_iter(match='kiosk:worker:*')):

@@ -160,17 +160,12 @@ constexpr int waitcnt_vm(int vm) {
   return (vm & 0xF) | (((vm >> 4) & 3) << 14) | 0x0070;
 }
 
-// kFused (4-wave split-K, two K slices), two in-launch combines:
-//  1: every K-slice block writes its fp32 partial tile to P[blockIdx.y];
-//     the block that arrives last at its tile's counter re-reads both
-//     partials and runs the epilogue.
-//  2: ticket first.  A block that finishes its K slice draws a ticket; the
-//     first of a tile's two blocks writes its partial (one plane, P[0]),
-//     releases it and leaves; the second keeps its accumulators in AGPRs,
-//     waits -- only if the first has not published yet, and only for that
-//     first block, which already holds its ticket and is running, so the
-//     wait cannot deadlock -- then adds the partial and runs the epilogue.
-//     Half the partial traffic of 1, none of the reduce kernel's.
+// kFused (4-wave split-K, two K slices): in-launch combine.  Every K-slice
+// block writes its fp32 partial tile to P[blockIdx.y]; the block that
+// arrives last at its tile's counter re-reads both partials and runs the
+// epilogue.  (A "ticket first" variant -- the first block publishes one
+// plane, the second keeps its accumulators and waits for it -- measured
+// slower than the reduce kernel and spilled: removed, profiles/r2_splitk_ab.)
 template <int EPI, int BN, int kWaves, int kFused = 0>
 __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
@@ -498,8 +493,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   auto finish = [&](int m, int nb, int j, const f32x4& a, float (&v)[4]) {
     v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
     if constexpr (kFused) {
-      // mode 1: the other slice's plane; mode 2: the first block's plane
-      const size_t plane = kFused == 1 ? static_cast<size_t>(split ^ 1) : 0;
+      // the other slice's plane
+      const size_t plane = static_cast<size_t>(split ^ 1);
       const float4 q = *reinterpret_cast<const float4*>(
           P + plane * M * N + static_cast<size_t>(m) * N + nb);
       v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
@@ -526,55 +521,6 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   };
   const int g = lane >> 4;
   const bool odd = (g & 1) != 0;
-  if constexpr (kFused == 2) {
-    // counter: +1 per ticket, +4 when the first block's partial is
-    // published (cdna_hip_programming.md §6 Guideline 16: plain stores ->
-    // vmcnt(0) -> barrier -> one lane: agent release fence, vmcnt(0),
-    // relaxed agent atomic; reader: relaxed polls, one acquire fence)
-    int* shared_ticket = reinterpret_cast<int*>(smem);   // the one LDS array
-    __syncthreads();            // every wave is done with the LDS ring
-    if (threadIdx.x == 0)
-      *shared_ticket = __hip_atomic_fetch_add(
-          cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int ticket = *shared_ticket;
-    if (ticket == 0) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int m = m0 + wm * (TM * 16) + i * 16 + (lane & 15);
-        if (m >= M) continue;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int nb = n0 + wn * (TN * 16) + j * 16 + g * 4;
-          *reinterpret_cast<float4*>(P + static_cast<size_t>(m) * N + nb) =
-              float4{acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(cnt + blockIdx.x, 4, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return;
-    }
-    if (threadIdx.x == 0) {
-      // bounded: every wave reaches the epilogue even if the partner never
-      // published (a wrong tile, never a hung grid)
-      int value = ticket;
-      for (int spin = 0; value < 4 && spin < (1 << 22); ++spin) {
-        __builtin_amdgcn_s_sleep(1);
-        value = __hip_atomic_load(cnt + blockIdx.x, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-  }
   if constexpr (kFused == 1) {
     // In-launch split-K combine (cdna_hip_programming.md §5, projection
     // GEMM item 2): plain 16-B partial stores -> every wave vmcnt(0) ->
@@ -732,12 +678,8 @@ hipError_t launch_fused4(const uint16_t* A, const uint16_t* B, uint16_t* C,
 
 template <int EPI>
 hipError_t configure_fused4() {
-  hipError_t err = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&gemm256_kernel<EPI, 256, 4, 1>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256, 4>::kLdsBytes);
-  if (err != hipSuccess) return err;
   return hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&gemm256_kernel<EPI, 256, 4, 2>),
+      reinterpret_cast<const void*>(&gemm256_kernel<EPI, 256, 4, 1>),
       hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256, 4>::kLdsBytes);
 }
 
@@ -900,11 +842,10 @@ int gemm256_splits(int M, int N, int K) {
 
 // Split-K combine: 0 = partial planes + the reduce kernel; 1 = in-launch,
 // last arriver re-reads both planes (6 % slower than 0 at 2048x4096x16384,
-// profiles/r1_gemm/gemm_w4_splitk_fused_ab.jsonl); 2 = in-launch, ticket
-// first (one plane, accumulators kept, see the kernel).
+// profiles/r1_gemm/gemm_w4_splitk_fused_ab.jsonl).
 int g_splitk_fused = 0;
 
-void gemm_set_splitk_fused(int mode) { g_splitk_fused = mode; }
+void gemm_set_splitk_fused(int mode) { g_splitk_fused = mode ? 1 : 0; }
 int gemm_splitk_fused() { return g_splitk_fused; }
 
 // the fused 4-wave split-K path: two 64-deep-aligned slices, 32-bit
@@ -952,9 +893,6 @@ hipError_t launch_gemm256_splitk(const uint16_t* A, const uint16_t* B,
     int* cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + off);
     hipError_t err = hipMemsetAsync(cnt, 0, tiles * 4, stream);
     if (err != hipSuccess) return err;
-    if (g_splitk_fused == 2)
-      return launch_fused4_epi<2>(A, B, C, bias, R, M, N, K / splits, K,
-                                  splits, workspace, cnt, epilogue, stream);
     return launch_fused4_epi<1>(A, B, C, bias, R, M, N, K / splits, K, splits,
                                 workspace, cnt, epilogue, stream);
   }

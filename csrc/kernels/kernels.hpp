@@ -65,7 +65,7 @@ int gemm256_splits(int M, int N, int K);
 size_t gemm256_splitk_workspace(int M, int N, int K);
 // split-K on the 4-wave kernel: combine in-launch by each tile's last
 // slice, or (default, faster here) partial planes + the reduce kernel
-void gemm_set_splitk_fused(int mode);   // 0 reduce kernel, 1, 2: in-launch
+void gemm_set_splitk_fused(int mode);   // 0 reduce kernel, 1 in-launch
 int gemm_splitk_fused();
 hipError_t launch_gemm256_splitk(const uint16_t* A, const uint16_t* B,
                                  uint16_t* C, const float* bias,

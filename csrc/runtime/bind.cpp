@@ -64,8 +64,7 @@ PYBIND11_MODULE(_kiosk_hip, m) {
   m.def("gemm_set_splitk_fused", &kiosk::gemm_set_splitk_fused,
         py::arg("mode"),
         "4-wave split-K combine: 0 = partial planes + reduce kernel, "
-        "1 = in-launch by the last slice (both planes), 2 = in-launch, "
-        "ticket first (one plane, accumulators kept)");
+        "1 = in-launch by the last slice (both planes)");
   m.def("gemm_splitk_fused", &kiosk::gemm_splitk_fused);
   m.attr("sum_blocks") = kiosk::kSumBlocks;
 

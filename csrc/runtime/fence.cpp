@@ -202,6 +202,9 @@ void Fence::init(const std::string& unique_id) {
   std::memcpy(id.internal, unique_id.data(), sizeof(id.internal));
   ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
   config.blocking = 0;   // init must be abortable on timeout
+  // (channel count: NCCL_MAX_NCHANNELS, set by the worker -- the config's
+  // maxCTAs leaves RCCL's 128 channels and their ~670 MB allocated)
+  config.commName = "kiosk-fence";
   ncclComm_t comm = nullptr;
   check_nccl(api.CommInitRankConfig(&comm, nranks, id, rank, &config),
              "ncclCommInitRankConfig");

@@ -13,9 +13,25 @@ runtime), ``models`` (worker model), ``ops`` (native HIP kernels),
 ``parallel`` (membership fence), ``utils`` (events, logging, HBM sizing),
 ``bench`` (load generator, simulator, metrics).
 """
-from .redisq import failover as redis
-from .autoscaler import Autoscaler
+import importlib
 
 __version__ = '0.1.0'
 
 __all__ = ['redis', 'Autoscaler', '__version__']
+
+# resolved on first use (PEP 562): a GPU worker imports this package for
+# its runtime only and should not pay for the autoscaler and the manager
+_LAZY = {'redis': ('.redisq.failover', None),
+         'Autoscaler': ('.autoscaler', 'Autoscaler')}
+
+
+def __getattr__(name):
+    if name not in _LAZY:
+        raise AttributeError('module %r has no attribute %r'
+                             % (__name__, name))
+    module, attr = _LAZY[name]
+    value = importlib.import_module(module, __name__)
+    if attr is not None:
+        value = getattr(value, attr)
+    globals()[name] = value
+    return value

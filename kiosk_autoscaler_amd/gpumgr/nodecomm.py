@@ -113,6 +113,7 @@ class NodeComm(object):
                            slots=[index for index, _ in members],
                            pids=[proc.pid for _, proc in members])
         logger.info('Node communicator generation %d: %d ranks.', self.gen, n)
+        self.m._publish_pool()
 
     def break_(self, reason, failed=False):
         """Drop the current generation (survivors abort; a fence in flight
@@ -138,6 +139,7 @@ class NodeComm(object):
                            failed=failed)
         logger.warning('Node communicator generation %d dropped: %s.',
                        self.gen, reason)
+        self.m._publish_pool()
 
     # ------------------------------------------------------------------
     def on_message(self, proc, message):
@@ -171,6 +173,7 @@ class NodeComm(object):
                                    transport=self.transport)
                 logger.info('Node communicator generation %d ready (%d ranks,'
                             ' %.0f ms).', self.gen, len(self.members), init_ms)
+                self.m._publish_pool()
         elif kind == 'fenced':
             inflight = self.inflight
             if inflight is None or message.get('seq') != inflight['seq']:

@@ -20,18 +20,21 @@ Engines:
 * :func:`torch_reference` -- fp32 PyTorch reference used by the numerics
   tests.
 """
+import math
 import time
-
-import numpy as np
 
 GELU_C = 0.7978845608028654  # sqrt(2/pi)
 
+# numpy is imported by the CPU engine only: the HIP worker never needs it
+# and its ~80 ms import sat on the cold-spawn critical path
+
 
 def init_bound(fan_in):
-    return 1.0 / np.sqrt(fan_in)
+    return 1.0 / math.sqrt(fan_in)
 
 
 def gelu_tanh_np(x):
+    import numpy as np
     return 0.5 * x * (1.0 + np.tanh(GELU_C * (x + 0.044715 * x ** 3)))
 
 
@@ -54,6 +57,7 @@ class CpuMlpEngine(object):
     name = 'cpu'
 
     def __init__(self, cfg, stage=None, dim=64, hidden=256):
+        import numpy as np
         self.cfg = cfg
         rng = np.random.default_rng(cfg.seed)
         self.layers = []
@@ -75,6 +79,7 @@ class CpuMlpEngine(object):
         return {'backend': 'cpu', 'cus_touched': 0}
 
     def forward(self, rows, passes, seed):
+        import numpy as np
         t0 = time.perf_counter()
         rng = np.random.default_rng(seed)
         x = rng.standard_normal((min(rows, 256), self.dim)).astype(np.float32)
@@ -141,7 +146,6 @@ class HipMlpEngine(object):
         out = self.engine.forward(int(rows), passes, 0)
         self.pass_ms[rows] = max(out['gpu_ms'] / passes, 1e-3)
         return self.pass_ms[rows]
-
 
     def forward(self, rows, passes, seed):
         return dict(self.engine.forward(int(rows), int(max(1, passes)),

@@ -10,7 +10,10 @@ Two start modes (both spawned by :mod:`kiosk_autoscaler_amd.gpumgr`):
   benchmark reports that time as ``standby_gpu_s``.  With
   ``WARM_POOL_MODE=import`` it stops after the imports and holds no GPU.
   Report ``standby`` and block on the command pipe.
-* **cold** (``--assign JSON``): the same, but start immediately.
+* **cold** (``--assign JSON``): start immediately.  The HIP context and
+  the code objects are created on a helper thread (``preinit_device``
+  releases the GIL) while the main thread imports the runtime and connects
+  to Redis; the engine joins it.
 
 With the node communicator (``node_fence`` in the pin/assignment) the
 process also runs a :class:`~..parallel.nodefence.NodeFenceAgent` for its
@@ -27,6 +30,7 @@ import gc
 import logging
 import os
 import sys
+import threading
 import time
 
 
@@ -56,6 +60,45 @@ def _preload(backend):
     return time.monotonic_ns() - t0
 
 
+def _preimport(backend):
+    """Standby: import what an assignment needs, off the critical path."""
+    from . import runtime  # noqa: F401
+    from ..utils import events  # noqa: F401
+    if backend == 'hip':
+        from ..models import mlp  # noqa: F401
+
+
+# cold spawn: the helper thread opening the device (see the module doc)
+_DEVICE_OPEN = {}
+
+
+def _open_device_async():
+    from ..ops import native
+    mod = native.load()
+
+    def run():
+        try:
+            _DEVICE_OPEN['stages'] = dict(mod.preinit_device(0))
+        except Exception as err:  # pylint: disable=broad-except
+            # the engine's own init reports the failure
+            _DEVICE_OPEN['error'] = str(err)
+    thread = threading.Thread(target=run, name='device-open', daemon=True)
+    _DEVICE_OPEN['thread'] = thread
+    thread.start()
+
+
+def _join_device_open(stage=None):
+    thread = _DEVICE_OPEN.pop('thread', None)
+    if thread is None:
+        return
+    thread.join()
+    if stage:
+        for name, t in sorted(_DEVICE_OPEN.get('stages', {}).items(),
+                              key=lambda kv: kv[1]):
+            stage(name, t)
+        stage('device_open_joined')
+
+
 _CLIENTS = {}
 # HIP engines kept across recycles (WORKER_KEEP_ENGINE=1): the recycled
 # standby's next assignment with the same model finds its weights, graph
@@ -82,6 +125,7 @@ def _cached_engine(backend, cfg, stage):
         engine.reused = True
         engine.cfg = cfg
         return engine
+    _join_device_open(stage)
     for old in list(_ENGINES.values()):
         old.close()
     _ENGINES.clear()
@@ -164,12 +208,20 @@ def main(argv=None):
     if backend == 'auto':
         backend = 'hip' if early and early.get('gpu') not in (None, '') \
             else 'cpu'
+    if backend == 'hip':
+        # the fence is this process's only RCCL user and moves 72 bytes: one
+        # channel instead of RCCL's gfx950 default of 128 holds 166 MB of
+        # HBM per communicator instead of 670 MB (profiles/r2_rccl_init)
+        os.environ.setdefault('NCCL_MIN_NCHANNELS', '1')
+        os.environ.setdefault('NCCL_MAX_NCHANNELS', '1')
     if early is not None:
         # pin before anything can initialise HIP (HIP_VISIBLE_DEVICES is
         # read once, at runtime init) and before the heavy imports
         apply_assignment_env({'gpu': early.get('gpu'),
                               'cpus': early.get('cpus')})
     preload_ns = _preload(backend)
+    if args.assign and backend == 'hip':
+        _open_device_async()
     preinit = {}
     node = bool((early or {}).get('node_fence')) and os.environ.get(
         'FENCE', 'auto') not in ('none', 'off', '0')
@@ -188,6 +240,7 @@ def main(argv=None):
             return 4
 
     if pin is not None and not args.assign:
+        _preimport(backend)
         _preconnect()
     node_agent = None
     if node:
@@ -222,6 +275,7 @@ def main(argv=None):
         pin = {'gpu': assignment.get('gpu'), 'slot': assignment.get('slot'),
                'cpus': assignment.get('cpus')}
         assignment = None
+    _join_device_open()     # never exit under a running device open
     # The engine (HBM, streams, graphs) and the fence are released by now;
     # skip interpreter teardown (torch/HIP static destructors take ~0.5 s)
     # so the GPU slot frees promptly.

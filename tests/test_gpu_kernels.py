@@ -312,13 +312,12 @@ def test_spin_kernel_and_roctx(mod):
 @pytest.mark.parametrize('M,N,K', [(2048, 1024, 4096), (512, 512, 16384),
                                    (300, 512, 8192), (777, 1024, 4096)])
 @pytest.mark.parametrize('epilogue', ['none', 'gelu', 'residual'])
-@pytest.mark.parametrize('fused', [0, 1, 2])
+@pytest.mark.parametrize('fused', [0, 1])
 def test_gemm_splitk(mod, M, N, K, epilogue, fused):
     """Split-K 256x256: two 64-deep-aligned slices run the 4-wave kernel,
     combined through fp32 partial planes + the reduce/epilogue kernel
-    (mode 0), in-launch by each tile's last slice (1), or ticket-first (2:
-    the first slice publishes one plane, the second combines from its
-    registers); more slices use the 8-wave kernel + reduce."""
+    (mode 0) or in-launch by each tile's last slice (1); more slices use
+    the 8-wave kernel + reduce."""
     from kiosk_autoscaler_amd.ops import kernels
     assert mod.gemm_workspace_bytes(M, N, K) > 0
     default = mod.gemm_splitk_fused()

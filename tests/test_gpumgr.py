@@ -226,3 +226,37 @@ def test_worker_ids_unique_across_instances_and_fence_backoff():
     a._fence_failed(res)
     assert res.fence_failures == 2 and res.fence_retry_at > first
     assert res.fence_wanted and res.fence_fresh
+
+
+def test_hip_worker_spawns_without_site_packages(monkeypatch):
+    """The torch-free HIP worker starts with ``python -S`` (no .pth scan on
+    the cold-spawn path); torch-importing, custom-module and CPU workers
+    keep site-packages."""
+    from kiosk_autoscaler_amd.gpumgr.controller import _bare_worker
+    monkeypatch.delenv('WORKER_IMPORT_TORCH', raising=False)
+    monkeypatch.delenv('WORKER_PYTHON_SITE', raising=False)
+    assert _bare_worker(gpumgr.WorkerTemplate(queues=['q'], backend='hip'))
+    assert not _bare_worker(gpumgr.WorkerTemplate(queues=['q'],
+                                                  backend='cpu'))
+    assert not _bare_worker(gpumgr.WorkerTemplate(
+        queues=['q'], backend='hip', env={'WORKER_IMPORT_TORCH': '1'}))
+    assert not _bare_worker(gpumgr.WorkerTemplate(
+        queues=['q'], backend='hip', module='my.worker'))
+    monkeypatch.setenv('WORKER_PYTHON_SITE', '1')
+    assert not _bare_worker(gpumgr.WorkerTemplate(queues=['q'],
+                                                  backend='hip'))
+    # and the worker's whole import graph resolves without site-packages
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ('import sys; '
+            'import kiosk_autoscaler_amd.worker.main, '
+            'kiosk_autoscaler_amd.worker.runtime, '
+            'kiosk_autoscaler_amd.models.mlp, '
+            'kiosk_autoscaler_amd.parallel.nodefence, '
+            'kiosk_autoscaler_amd.ops.native; '
+            'bad = [m for m in sys.modules if m.split(".")[0] in '
+            '("numpy", "torch")]; assert not bad, bad')
+    env = dict(os.environ, PYTHONPATH=root)
+    subprocess.run([sys.executable, '-S', '-c', code], env=env, check=True,
+                   timeout=60)

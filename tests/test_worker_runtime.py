@@ -87,3 +87,37 @@ def test_batch_split_to_engine_capacity(redis_client):
     assert len(calls) == 2
     assert all(redis_client.hget('predict:j%d' % i, 'status') == 'done'
                for i in range(4))
+
+
+def test_cold_spawn_opens_the_device_on_a_helper_thread(monkeypatch):
+    """Cold spawn: ``preinit_device`` runs on a helper thread while the main
+    thread imports and connects; the engine joins it and records its
+    stamps.  A failing open is left to the engine's own init to report."""
+    import threading
+    from kiosk_autoscaler_amd.ops import native
+    from kiosk_autoscaler_amd.worker import main as worker_main
+    release = threading.Event()
+
+    class FakeMod(object):
+        fail = False
+
+        def preinit_device(self, device):
+            release.wait(10)
+            if self.fail:
+                raise RuntimeError('no device')
+            return {'preinit_enter': 1, 'preinit_done': 2}
+    mod = FakeMod()
+    monkeypatch.setattr(native, 'load', lambda **kw: mod)
+    worker_main._open_device_async()
+    assert worker_main._DEVICE_OPEN['thread'].is_alive()   # not joined yet
+    release.set()
+    stages = []
+    worker_main._join_device_open(lambda name, t=None: stages.append(name))
+    assert stages == ['preinit_enter', 'preinit_done', 'device_open_joined']
+    worker_main._join_device_open()          # idempotent
+    mod.fail = True
+    worker_main._DEVICE_OPEN.clear()
+    worker_main._open_device_async()
+    worker_main._join_device_open()
+    assert 'no device' in worker_main._DEVICE_OPEN['error']
+    worker_main._DEVICE_OPEN.clear()

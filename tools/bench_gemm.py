@@ -63,11 +63,6 @@ def main():
             kernels.gemm(a, b, out=out, variant='256splitk')
             mod.gemm_set_splitk_fused(default_mode)
 
-        def ours_splitk_ticket():
-            mod.gemm_set_splitk_fused(2)
-            kernels.gemm(a, b, out=out, variant='256splitk')
-            mod.gemm_set_splitk_fused(default_mode)
-
         def ours_splitk_reduce():
             mod.gemm_set_splitk_fused(0)
             kernels.gemm(a, b, out=out, variant='256splitk')
@@ -91,7 +86,6 @@ def main():
         if mod.gemm_workspace_bytes(M, N, K):
             fns['native256splitk'] = ours_splitk
             fns['native256splitk_fused'] = ours_splitk_fused
-            fns['native256splitk_ticket'] = ours_splitk_ticket
             fns['native256splitk_reduce'] = ours_splitk_reduce
 
         results = {k: [] for k in fns}

@@ -18,7 +18,7 @@ def main():
     parser.add_argument('--dim', type=int, default=4096)
     parser.add_argument('--hidden', type=int, default=16384)
     parser.add_argument('--layers', type=int, default=4)
-    parser.add_argument('--modes', default='0,2,1')
+    parser.add_argument('--modes', default='0,1')
     parser.add_argument('--rounds', type=int, default=9)
     parser.add_argument('--passes', type=int, default=20)
     args = parser.parse_args()

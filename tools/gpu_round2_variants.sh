@@ -3,7 +3,7 @@
 #   bash tools/gpu_round2_variants.sh A   -> default + strict + 2 queues + idle-interval
 #   bash tools/gpu_round2_variants.sh B   -> job KEYS_PER_POD=4 + 60 s-burst long form
 set -o pipefail
-OUT=gpurun_out/r2_variants
+OUT=${OUT:-gpurun_out/r2_variants}
 mkdir -p $OUT
 run() {
   tag=$1; limit=$2; shift 2
@@ -23,5 +23,6 @@ if [ "$1" = "A" ]; then
 else
   run job_kpp4_strict 260 --gpus 1 --steps 6 --warmup 1 --resource-type job --kpp 4 --on 8 --lam-per-gpu 1.0 --policy strict --budget-s 240 && \
   run job_kpp4_reference 260 --gpus 1 --steps 6 --warmup 1 --resource-type job --kpp 4 --on 8 --lam-per-gpu 1.0 --budget-s 240 --drain-timeout 20 && \
-  run longform_60s_bursts 400 --gpus 1 --steps 2 --warmup 0 --on 60 --budget-s 380
+  run longform_60s_bursts 400 --gpus 1 --steps 2 --warmup 0 --on 60 --budget-s 380 && \
+  run import_norecycle 200 --gpus 1 --steps 8 --warmup 2 --budget-s 180 --pool-mode import --no-recycle --cold-cycles 0
 fi
