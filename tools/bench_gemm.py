@@ -75,8 +75,15 @@ def main():
         def theirs_plain():
             torch.matmul(a, b.t(), out=out)
 
+        bias_bf16 = bias.to(torch.bfloat16)
+
+        def theirs_fused_gelu():
+            # hipBLASLt with its own GELU_BIAS epilogue (tanh GELU)
+            torch._addmm_activation(bias_bf16, a, b.t(), use_gelu=True)
+
         fns = {'native_gelu_auto': ours, 'native128': ours_plain,
-               'torch_gelu': theirs, 'torch': theirs_plain}
+               'torch_gelu': theirs, 'torch': theirs_plain,
+               'hipblaslt_epilogue_gelu': theirs_fused_gelu}
         if N % 256 == 0:
             fns['native256'] = ours_256
             fns['native256w4'] = ours_256w4
