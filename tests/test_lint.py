@@ -40,6 +40,7 @@ def test_covtrace_counts_lines(tmp_path):
                    '    return 2  # pragma: no cover\n')
     tracer = covtrace.LineTracer(str(pkg))
     sys.path.insert(0, str(tmp_path))
+    outer = sys.gettrace()      # covtrace's own tracer when run under it
     try:
         tracer.start()
         import pkg.m as m  # noqa: F401
@@ -47,6 +48,9 @@ def test_covtrace_counts_lines(tmp_path):
         tracer.stop()
     finally:
         sys.path.remove(str(tmp_path))
+    # a nested tracer hands the process back to the outer one: stopping it
+    # used to switch the gate's tracing off for the rest of the session
+    assert sys.gettrace() is outer
     rows, total = covtrace.report(tracer, str(pkg))
     assert rows and total == 100.0   # line 4 excluded by the pragma
 

@@ -45,12 +45,16 @@ class LineTracer(object):
         return local
 
     def start(self):
+        # nested tracers (tests of this tool) restore the outer one on stop
+        gettrace = getattr(threading, 'gettrace', lambda: None)
+        self._saved = (sys.gettrace(), gettrace())
         threading.settrace(self._global)
         sys.settrace(self._global)
 
     def stop(self):
-        sys.settrace(None)
-        threading.settrace(None)
+        outer, outer_threads = getattr(self, '_saved', (None, None))
+        sys.settrace(outer)
+        threading.settrace(outer_threads)
 
 
 def _dump(tracer, directory):
