@@ -260,3 +260,65 @@ def test_hip_worker_spawns_without_site_packages(monkeypatch):
     env = dict(os.environ, PYTHONPATH=root)
     subprocess.run([sys.executable, '-S', '-c', code], env=env, check=True,
                    timeout=60)
+
+
+@pytest.mark.gpu
+def test_gpu_cold_spawn_opens_the_device_in_parallel(resp_server):
+    """MI355X, no standby (``WARM_POOL=0``): the worker starts as
+    ``python -S`` (no torch, no numpy), opens the device on a helper thread
+    while it imports and connects, serves a key and drains."""
+    import sys
+    import time
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict', 'RESOURCE_NAME': 'cold', 'MAX_PODS': '1',
+           'WORKER_BACKEND': 'hip', 'WARM_POOL': '0', 'FENCE': 'none',
+           'REDIS_INTERVAL': '0', 'GPU_IDS': '0', 'MODEL_DIM': '1024',
+           'MODEL_HIDDEN': '4096', 'MODEL_LAYERS': '2',
+           'ROWS_PER_KEY': '256'}
+    s = Settings(Config(environ=env, use_files=False))
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    events = EventLog(source='test')
+    manager = gpumgr.build_manager(s, redis_client=client,
+                                   events=events).start()
+
+    def until(predicate, timeout):
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            value = predicate()
+            if value:
+                return value
+            time.sleep(0.02)
+        raise AssertionError('timed out')
+
+    def ready_worker():
+        for resource in manager.resources.values():
+            for worker in resource.workers.values():
+                if worker.state == 'ready':
+                    return worker
+        return None
+    try:
+        client.hset('predict:c0', mapping={'status': 'new', 'rows': 256})
+        client.lpush('predict', 'predict:c0')
+        manager.patch_namespaced_deployment(
+            'cold', 'default', {'spec': {'replicas': 1}})
+        worker = until(ready_worker, 120)
+        argv = list(worker.proc.popen.args)
+        assert argv[:2] == [sys.executable, '-S'], argv
+        stages = worker.stages
+        for name in ('preinit_context', 'preinit_done', 'device_open_joined',
+                     'warmstart_done', 'ready'):
+            assert name in stages, sorted(stages)
+        # the device opened while the main thread was still importing: the
+        # context exists before the engine asked for it
+        assert stages['preinit_context'] <= stages['device_open_joined']
+        assert (stages['ready'] - worker.t_assigned) / 1e9 < 10.0
+        until(lambda: client.hget('predict:c0', 'status') == 'done', 120)
+        manager.patch_namespaced_deployment(
+            'cold', 'default', {'spec': {'replicas': 0}})
+        until(lambda: ready_worker() is None, 60)
+    finally:
+        manager.stop()
