@@ -73,3 +73,33 @@ def test_lint_cli_exit_status():
                                                         'lint.py')],
                           stdout=subprocess.PIPE, text=True, timeout=120)
     assert proc.returncode == 0, proc.stdout
+
+
+def test_covtrace_config_exclusions_and_lcov(tmp_path):
+    """``.coveragerc`` drives the gate (fail_under, exclude_lines with
+    coverage.py's block semantics, omit) and ``--lcov`` output is a valid
+    tracefile."""
+    rc = tmp_path / 'rc'
+    rc.write_text('[run]\nomit =\n    pkg/skip.py\n[report]\nfail_under = 91\n'
+                  'exclude_lines =\n    pragma: no cover\n'
+                  '    except ImportError\n')
+    config = covtrace.load_config(str(rc))
+    assert config['fail_under'] == 91.0
+    assert config['omit'] == ['pkg/skip.py']
+    text = ['try:', '    import x', 'except ImportError:', '    x = None',
+            '    y = 1', 'z = 2  # pragma: no cover', 'w = 3']
+    assert covtrace._excluded(text, config['exclude_lines']) == {3, 4, 5, 6}
+    # the repository's own file parses and keeps the reference's gate
+    assert covtrace.load_config()['fail_under'] == 80.0
+
+    tracer = covtrace.LineTracer('/nonexistent')
+    pkg = os.path.join(ROOT, 'kiosk_autoscaler_amd')
+    policy = os.path.join(pkg, 'policy.py')
+    tracer.hits[policy] = {1, 2, 3}
+    out = tmp_path / 'lcov.info'
+    covtrace.write_lcov(tracer, str(out), package=pkg,
+                        omit=['kiosk_autoscaler_amd/[!p]*',
+                              'kiosk_autoscaler_amd/p[!o]*'])
+    records = out.read_text().strip().split('end_of_record')
+    assert records[0].startswith('TN:\nSF:kiosk_autoscaler_amd/policy.py')
+    assert 'LF:' in records[0] and 'LH:' in records[0]

@@ -15,7 +15,9 @@ goes on ``PYTHONPATH`` and its ``sitecustomize`` dumps each child's lines
     python tools/covtrace.py --fail-under 80 -- tests -m "not gpu" -q
 
 prints a per-file table and the total and exits 1 below the gate (or with
-pytest's own failure status).
+pytest's own failure status).  Settings (``fail_under``, ``exclude_lines``,
+``omit``) come from ``.coveragerc``, the file coverage.py reads too;
+``--lcov`` writes an LCOV tracefile for Coveralls.
 """
 import argparse
 import os
@@ -103,7 +105,53 @@ def merge_children(tracer, directory):
             tracer.hits.setdefault(path, set()).update(lines)
 
 
-def executable_lines(path):
+DEFAULT_EXCLUDE = ('pragma: no cover',)
+
+
+def load_config(path=os.path.join(ROOT, '.coveragerc')):
+    """``fail_under``, ``exclude_lines`` and ``omit`` from a coverage.py
+    style ``.coveragerc`` (the same file serves coverage.py users)."""
+    import configparser
+    parser = configparser.ConfigParser()
+    parser.read(path)
+
+    def listed(section, key):
+        raw = parser.get(section, key, fallback='')
+        return [v.strip() for v in raw.splitlines() if v.strip()]
+    return {
+        'fail_under': parser.getfloat('report', 'fail_under', fallback=80.0),
+        'exclude_lines': listed('report', 'exclude_lines') or list(
+            DEFAULT_EXCLUDE),
+        'omit': listed('run', 'omit') + listed('report', 'omit'),
+    }
+
+
+def _excluded(text, patterns):
+    """Lines matching an ``exclude_lines`` regex; a matching block opener
+    (``except ImportError:``) excludes the whole block, as coverage.py
+    does."""
+    import re
+    regexes = [re.compile(p) for p in patterns]
+    out = set()
+    i = 0
+    while i < len(text):
+        line = text[i]
+        if any(r.search(line) for r in regexes):
+            out.add(i + 1)
+            if line.rstrip().endswith(':'):
+                indent = len(line) - len(line.lstrip())
+                j = i + 1
+                while j < len(text) and (not text[j].strip() or len(
+                        text[j]) - len(text[j].lstrip()) > indent):
+                    out.add(j + 1)
+                    j += 1
+                i = j
+                continue
+        i += 1
+    return out
+
+
+def executable_lines(path, exclude=DEFAULT_EXCLUDE):
     with open(path, encoding='utf-8') as handle:
         source = handle.read()
     code = compile(source, path, 'exec')
@@ -115,11 +163,8 @@ def executable_lines(path):
             if line is not None:
                 lines.add(line)
         stack.extend(c for c in co.co_consts if hasattr(c, 'co_lines'))
-    text = source.split('\n')
-    excluded = {i + 1 for i, line in enumerate(text)
-                if 'pragma: no cover' in line}
     # a module docstring / first line counts as executed on import only
-    return lines - excluded
+    return lines - _excluded(source.split('\n'), exclude)
 
 
 def _package_files(package=PACKAGE):
@@ -146,7 +191,8 @@ def _ranges(numbers):
     return ','.join(out)
 
 
-def report(tracer, package=PACKAGE):
+def report(tracer, package=PACKAGE, exclude=DEFAULT_EXCLUDE, omit=()):
+    import fnmatch
     rows = []
     total_exec = total_hit = 0
     for base, dirs, files in os.walk(package):
@@ -155,7 +201,10 @@ def report(tracer, package=PACKAGE):
             if not name.endswith('.py'):
                 continue
             path = os.path.join(base, name)
-            lines = executable_lines(path)
+            rel = os.path.relpath(path, ROOT)
+            if any(fnmatch.fnmatch(rel, pat) for pat in omit):
+                continue
+            lines = executable_lines(path, exclude)
             hit = tracer.hits.get(path, set()) & lines
             total_exec += len(lines)
             total_hit += len(hit)
@@ -166,6 +215,27 @@ def report(tracer, package=PACKAGE):
     return rows, total
 
 
+def write_lcov(tracer, out_path, package=PACKAGE, exclude=DEFAULT_EXCLUDE,
+               omit=()):
+    """LCOV tracefile (Coveralls / genhtml input) of the same data."""
+    import fnmatch
+    records = []
+    for path in sorted(_package_files(package)):
+        rel = os.path.relpath(path, ROOT)
+        if any(fnmatch.fnmatch(rel, pat) for pat in omit):
+            continue
+        lines = sorted(executable_lines(path, exclude))
+        hits = tracer.hits.get(path, set())
+        body = ['TN:', 'SF:%s' % rel]
+        body += ['DA:%d,%d' % (n, 1 if n in hits else 0) for n in lines]
+        body += ['LF:%d' % len(lines),
+                 'LH:%d' % sum(1 for n in lines if n in hits),
+                 'end_of_record']
+        records.append('\n'.join(body))
+    with open(out_path, 'w') as handle:
+        handle.write('\n'.join(records) + '\n')
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     pytest_args = []
@@ -173,13 +243,20 @@ def main(argv=None):
         split = argv.index('--')
         argv, pytest_args = argv[:split], argv[split + 1:]
     parser = argparse.ArgumentParser(description=__doc__.split('\n')[0])
-    parser.add_argument('--fail-under', type=float, default=80.0)
+    parser.add_argument('--fail-under', type=float, default=None,
+                        help='default: .coveragerc [report] fail_under')
+    parser.add_argument('--rcfile', default=os.path.join(ROOT, '.coveragerc'))
+    parser.add_argument('--lcov', default=None,
+                        help='also write an LCOV tracefile (Coveralls)')
     parser.add_argument('--output', default=None,
                         help='also write the table to this file')
     parser.add_argument('--missing', default='',
                         help='comma-separated file name fragments: list '
                              'their never-executed lines')
     args = parser.parse_args(argv)
+    config = load_config(args.rcfile)
+    if args.fail_under is None:
+        args.fail_under = config['fail_under']
     sys.path.insert(0, ROOT)
     import tempfile
     import pytest
@@ -196,15 +273,19 @@ def main(argv=None):
     finally:
         tracer.stop()
     merge_children(tracer, child_dir)
-    rows, total = report(tracer)
+    rows, total = report(tracer, exclude=config['exclude_lines'],
+                         omit=config['omit'])
+    if args.lcov:
+        write_lcov(tracer, args.lcov, exclude=config['exclude_lines'],
+                   omit=config['omit'])
     lines = ['%-52s %6s %6s %6s' % ('file', 'stmts', 'hit', 'cover')]
     for path, n, hit, pct in rows:
         lines.append('%-52s %6d %6d %5.1f%%' % (path, n, hit, pct))
     lines.append('%-52s %6s %6s %5.1f%%' % ('TOTAL', '', '', total))
     for frag in filter(None, args.missing.split(',')):
         for path in sorted(p for p in _package_files() if frag in p):
-            missed = sorted(executable_lines(path) -
-                            tracer.hits.get(path, set()))
+            missed = sorted(executable_lines(path, config['exclude_lines'])
+                            - tracer.hits.get(path, set()))
             lines.append('missing %s: %s' % (os.path.relpath(path, ROOT),
                                              _ranges(missed)))
     text = '\n'.join(lines)
