@@ -25,11 +25,13 @@ def main():
     parser.add_argument('--keys', type=int, default=3)
     parser.add_argument('--passes', type=int, default=20)
     parser.add_argument('--no-preinit', action='store_true')
+    parser.add_argument('--with-torch', action='store_true',
+                        help='import torch first (round-1 worker)')
     args = parser.parse_args()
     t0 = time.monotonic_ns()
-    import torch  # noqa: F401
     from kiosk_autoscaler_amd.ops import native
-    mod = native.load()
+    # like the worker: the native module on ROCm's HIP runtime, no torch
+    mod = native.load(torch_first=bool(args.with_torch))
     t_import = time.monotonic_ns()
     pre = {} if args.no_preinit else dict(mod.preinit_device(0))
     t_assign = time.monotonic_ns()
