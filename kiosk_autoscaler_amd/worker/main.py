@@ -27,7 +27,6 @@ context, becomes its GPU's standby again.
 """
 import argparse
 import gc
-import logging
 import os
 import sys
 import threading
@@ -193,15 +192,10 @@ def main(argv=None):
     if args.standalone:
         return _standalone(args.backend)
     _die_with_parent()
-
-    logging.basicConfig(
-        level=logging.INFO, stream=sys.stderr,
-        format='[%(asctime)s]:[%(levelname)s]:[%(name)s]: %(message)s')
-
-    from .channel import Channel
-    from .runtime import apply_assignment_env, parse_assignment
-    channel = Channel(args.cmd_fd, args.ev_fd)
-
+    # ordered for the cold spawn: pin, load the native module and start
+    # opening the device first; logging, the channel and the runtime
+    # modules load while the helper thread creates the HIP context
+    from .pinning import apply_assignment_env, parse_assignment
     backend = args.backend
     pin = parse_assignment(args.pin) if args.pin else None
     early = parse_assignment(args.assign) if args.assign else pin
@@ -222,6 +216,13 @@ def main(argv=None):
     preload_ns = _preload(backend)
     if args.assign and backend == 'hip':
         _open_device_async()
+
+    import logging
+    logging.basicConfig(
+        level=logging.INFO, stream=sys.stderr,
+        format='[%(asctime)s]:[%(levelname)s]:[%(name)s]: %(message)s')
+    from .channel import Channel
+    channel = Channel(args.cmd_fd, args.ev_fd)
     preinit = {}
     node = bool((early or {}).get('node_fence')) and os.environ.get(
         'FENCE', 'auto') not in ('none', 'off', '0')
@@ -308,6 +309,7 @@ def _standalone(backend):
     ``job`` worker exits when the queue is empty."""
     import signal
     import socket
+    import logging
     logging.basicConfig(
         level=logging.INFO, stream=sys.stderr,
         format='[%(asctime)s]:[%(levelname)s]:[%(name)s]: %(message)s')
