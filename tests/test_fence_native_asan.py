@@ -1,4 +1,5 @@
-"""csrc/runtime/fence.cpp under AddressSanitizer + UBSan on the host (CPU):
+"""csrc/runtime/fence.cpp under AddressSanitizer + UBSan, and under
+ThreadSanitizer, on the host (CPU):
 the fence's failure paths -- async init error, init timeout, abort
 requested before connect or during a blocked all-reduce, all-reduce
 timeout, stuck finalize -- against a fake HIP + RCCL library whose
@@ -15,12 +16,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.slow
 
 
-def test_fence_failure_paths_under_asan(tmp_path):
+SANITIZERS = {
+    'asan': ['-fsanitize=address,undefined',
+             '-fno-sanitize-recover=undefined'],
+    # the abort flag is set from another thread while connect / all-reduce
+    # poll it (scenarios 4-5): ThreadSanitizer checks that hand-off
+    'tsan': ['-fsanitize=thread'],
+}
+
+
+@pytest.mark.parametrize('sanitizer', sorted(SANITIZERS))
+def test_fence_failure_paths_under_sanitizers(tmp_path, sanitizer):
     cxx = shutil.which('g++')
     if cxx is None or not os.path.exists('/opt/rocm/include/rccl/rccl.h'):
         pytest.skip('needs g++ and the ROCm headers')
-    san = ['-fsanitize=address,undefined', '-fno-sanitize-recover=undefined',
-           '-fno-omit-frame-pointer', '-g', '-O1']
+    san = SANITIZERS[sanitizer] + ['-fno-omit-frame-pointer', '-g', '-O1']
     inc = ['-std=c++17', '-D__HIP_PLATFORM_AMD__', '-I/opt/rocm/include',
            '-I' + os.path.join(ROOT, 'csrc', 'runtime')]
     fake = str(tmp_path / 'libkiosk_fake_hip_rccl.so')
@@ -37,11 +47,13 @@ def test_fence_failure_paths_under_asan(tmp_path):
         check=True, timeout=300)
     env = dict(os.environ, KIOSK_RCCL_LIB=fake, KIOSK_ROCTX='0',
                ASAN_OPTIONS='detect_leaks=1:abort_on_error=0',
-               UBSAN_OPTIONS='print_stacktrace=1:halt_on_error=1')
+               UBSAN_OPTIONS='print_stacktrace=1:halt_on_error=1',
+               TSAN_OPTIONS='halt_on_error=1:second_deadlock_stack=1')
     proc = subprocess.run([exe], env=env, stdout=subprocess.PIPE,
                           stderr=subprocess.PIPE, text=True, timeout=120)
     text = proc.stdout + proc.stderr
     assert proc.returncode == 0, text[-4000:]
     assert 'PASSED: 0 failure(s)' in proc.stdout, text[-4000:]
     assert 'AddressSanitizer' not in text and 'runtime error' not in text
+    assert 'ThreadSanitizer' not in text, text[-4000:]
     assert proc.stdout.count('ok ') >= 14
