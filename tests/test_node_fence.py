@@ -414,6 +414,60 @@ def test_gpu_node_comm_through_the_manager(resp_server):
     assert max(e['wall_s'] for e in done) < 0.05
 
 
+@pytest.mark.gpu
+def test_gpu_failing_node_comm_never_blocks_serving(resp_server):
+    """MI355X: two slots on the SAME GPU, so every node-communicator
+    generation fails (RCCL refuses a duplicate GPU) and is retried with
+    backoff -- the multi-GPU failure this pool cannot stage otherwise.
+    Scale-up, READY and serving must not wait on it: the fence is off the
+    critical path."""
+    from kiosk_autoscaler_amd import Autoscaler, gpumgr
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import RedisClient, StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict', 'RESOURCE_NAME': 'dup', 'MAX_PODS': '1',
+           'WORKER_BACKEND': 'hip', 'WARM_POOL': '2', 'FENCE': 'auto',
+           'INTERVAL': '1', 'REDIS_INTERVAL': '0', 'GPU_IDS': '0,0',
+           'MODEL_DIM': '1024', 'MODEL_HIDDEN': '4096', 'MODEL_LAYERS': '2',
+           'ROWS_PER_KEY': '256'}
+    s = Settings(Config(environ=env, use_files=False))
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    events = EventLog(source='test')
+    events.keep = True
+    manager = gpumgr.build_manager(s, redis_client=client,
+                                   events=events).start()
+    scaler = Autoscaler(RedisClient(host=resp_server.host,
+                                    port=resp_server.port, backoff=0),
+                        'predict', actuator=manager)
+    try:
+        assert manager.node is not None and len(manager.slots) == 2
+        # the first generation has been tried (and, normally, refused)
+        wait_for(lambda: any(e['ev'] in ('node_comm_break', 'node_comm_ready')
+                             for e in events.records), timeout=120)
+        for cycle in range(2):
+            item = 'predict:dup%d' % cycle
+            client.hset(item, mapping={'status': 'new', 'rows': 256})
+            client.lpush('predict', item)
+            t0 = time.monotonic()
+            assert scaler.scale('default', 'deployment', 'dup', 0, 1, 1) == 1
+            wait_for(lambda: client.hget(item, 'status') == 'done',
+                     timeout=60)
+            assert time.monotonic() - t0 < 30.0
+            assert scaler.scale('default', 'deployment', 'dup', 0, 1, 1) == 0
+            wait_for(lambda: not [w for r in manager.resources.values()
+                                  for w in r.workers.values()
+                                  if w.state == 'ready'], timeout=60)
+    finally:
+        manager.stop(timeout=20)
+    breaks = [e for e in events.records if e['ev'] == 'node_comm_break']
+    ready = [e for e in events.records if e['ev'] == 'node_comm_ready']
+    # either RCCL refused the pair (failed generations, retried) or it
+    # accepted it; serving never depended on which
+    assert (breaks and all(b['failed'] for b in breaks)) or ready
+
+
 _RANK_SCRIPT = r'''
 import json, os, sys, time
 sys.path.insert(0, os.environ['KIOSK_ROOT'])
