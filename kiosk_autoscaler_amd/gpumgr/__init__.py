@@ -65,7 +65,8 @@ def worker_env(settings, keys_per_pod=None):
                         'JOB_IDLE_EXIT_S', 'POLL_BLOCK_S', 'MODEL_SEED',
                         'KIOSK_RCCL_LIB', 'WORKER_EVENTS', 'KIOSK_FAULTS',
                         'KIOSK_ROCTX', 'WORKER_KEEP_ENGINE',
-                        'WORKER_IMPORT_TORCH'):
+                        'WORKER_IMPORT_TORCH', 'WORKER_ENGINE',
+                        'WORKER_PYTHON_SITE'):
         if passthrough in os.environ:
             env[passthrough] = os.environ[passthrough]
     return env

@@ -51,12 +51,18 @@ def _preload(backend):
     t0 = time.monotonic_ns()
     if backend == 'hip':
         from ..ops import native
-        with_torch = os.environ.get('WORKER_IMPORT_TORCH', '0') not in (
-            '0', '')
-        native.load(torch_first=with_torch)
+        native.load(torch_first=_imports_torch())
     else:
         import numpy  # noqa: F401
     return time.monotonic_ns() - t0
+
+
+def _imports_torch():
+    """Torch before the native module (one HIP runtime per process):
+    ``WORKER_IMPORT_TORCH``, default on for a ``WORKER_ENGINE`` plug-in
+    (which may well be a PyTorch model), off for the built-in engine."""
+    default = '1' if os.environ.get('WORKER_ENGINE') else '0'
+    return os.environ.get('WORKER_IMPORT_TORCH', default) not in ('0', '')
 
 
 def _preimport(backend):
@@ -65,6 +71,13 @@ def _preimport(backend):
     from ..utils import events  # noqa: F401
     if backend == 'hip':
         from ..models import mlp  # noqa: F401
+    spec = os.environ.get('WORKER_ENGINE')
+    if spec:
+        from ..models.plugin import load_factory
+        try:
+            load_factory(spec)
+        except Exception:  # pylint: disable=broad-except
+            pass   # the assignment reports it, as a failed start
 
 
 # cold spawn: the helper thread opening the device (see the module doc)
@@ -106,6 +119,10 @@ _ENGINES = {}
 
 
 def _engine_key(backend, cfg):
+    spec = os.environ.get('WORKER_ENGINE', '')
+    if spec:
+        return ('plugin', spec, backend, cfg.dim, cfg.hidden, cfg.layers,
+                max(cfg.rows * cfg.batch, 256), cfg.seed)
     if backend != 'hip':
         return None
     return ('hip', cfg.dim, cfg.hidden, cfg.layers,
@@ -128,7 +145,12 @@ def _cached_engine(backend, cfg, stage):
     for old in list(_ENGINES.values()):
         old.close()
     _ENGINES.clear()
-    engine = create_engine(backend, cfg, stage)
+    spec = os.environ.get('WORKER_ENGINE', '')
+    if spec:
+        from ..models.plugin import PluginEngine
+        engine = PluginEngine(spec, cfg, stage)
+    else:
+        engine = create_engine(backend, cfg, stage)
     if key is not None and keep:
         _ENGINES[key] = engine
     return engine

@@ -351,6 +351,9 @@ class WorkerRuntime(object):
         if self.faults:
             self.faults.before_key(self.keys_done + 1, self.engine,
                                    self.redis)
+        if callable(getattr(self.engine, 'infer', None)):
+            self._run_plugin(consumer, jobs, t_start)
+            return
         rows = sum(p['rows'] for _, _, _, p, _ in jobs)
         passes = max(p['passes'] for _, _, _, p, _ in jobs)
         service_ms = max(p['service_ms'] for _, _, _, p, _ in jobs)
@@ -381,15 +384,41 @@ class WorkerRuntime(object):
         # liveness for the manager's watchdog (WORKER_TIMEOUT)
         self.channel.emit('beat', keys=self.keys_done)
 
-    def _complete(self, consumer, jobs, result, t_start, t_done):
+    def _run_plugin(self, consumer, jobs, t_start):
+        """A ``WORKER_ENGINE`` batch: the engine maps the job hashes to
+        result fields (models/plugin.py)."""
+        batch = [{'item': item, 'queue': queue, 'rows': p['rows'],
+                  'seed': p['seed'], 'passes': p['passes'],
+                  'service_ms': p['service_ms'], 'fields': dict(fields)}
+                 for queue, item, _, p, fields in jobs]
+        try:
+            outputs, ms = self.engine.infer(batch)
+        except (ValueError, TypeError) as err:
+            for queue, item, pkey, _, fields in jobs:
+                self._fail(consumer, queue, item, pkey, err, bool(fields))
+            return
+        t_done = time.monotonic_ns()
+        with trace_range('kiosk.complete'):
+            self._complete(consumer, jobs, {'ms': ms}, t_start, t_done,
+                           outputs=outputs)
+        self.channel.emit('beat', keys=self.keys_done)
+
+    def _complete(self, consumer, jobs, result, t_start, t_done,
+                  outputs=None):
         cfg = self.config
-        for queue, item, pkey, params, fields in jobs:
-            if fields:
-                self.redis.hset(item, mapping={
+        for index, (queue, item, pkey, params, fields) in enumerate(jobs):
+            if fields:      # results go into the job hash (kiosk convention)
+                mapping = {
                     'status': 'done', 'worker': cfg.worker_id,
                     'gpu': cfg.slot, 'compute_ms': '%.3f' % result['ms'],
-                    'checksum': '%.6e' % result.get('checksum', 0.0),
-                    'started_ns': t_start, 'finished_ns': t_done})
+                    'started_ns': t_start, 'finished_ns': t_done}
+                if outputs is None:
+                    mapping['checksum'] = '%.6e' % result.get('checksum',
+                                                              0.0)
+                else:
+                    mapping.update({str(k): str(v) for k, v in
+                                    outputs[index].items()})
+                self.redis.hset(item, mapping=mapping)
             consumer.complete(pkey)
             self.keys_done += 1
             self._emit_event('key_done', item=item, queue=queue, t_ns=t_done,
