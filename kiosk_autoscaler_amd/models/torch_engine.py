@@ -23,18 +23,22 @@ class TorchMlpEngine(object):
         self.dtype = torch.bfloat16
         self.dim, self.hidden = cfg.dim, cfg.hidden
         self.max_rows = max(cfg.rows * cfg.batch, 1)
-        gen = torch.Generator(device='cpu').manual_seed(cfg.seed)
+        # weights are created and randomised on the device: a GB of
+        # parameters initialised on the host would dominate the first
+        # scale-up (the built-in engine does the same with its init kernel)
+        gen = torch.Generator(device=self.device).manual_seed(cfg.seed)
+        factory = {'device': self.device, 'dtype': self.dtype}
         layers = []
         for _ in range(cfg.layers):
-            up = torch.nn.Linear(cfg.dim, cfg.hidden)
-            down = torch.nn.Linear(cfg.hidden, cfg.dim)
+            up = torch.nn.Linear(cfg.dim, cfg.hidden, **factory)
+            down = torch.nn.Linear(cfg.hidden, cfg.dim, **factory)
             for lin in (up, down):
                 bound = 1.0 / math.sqrt(lin.in_features)
                 with torch.no_grad():
                     lin.weight.uniform_(-bound, bound, generator=gen)
                     lin.bias.uniform_(-bound, bound, generator=gen)
             layers.append(torch.nn.ModuleList([up, down]))
-        self.layers = torch.nn.ModuleList(layers).to(self.device, self.dtype)
+        self.layers = torch.nn.ModuleList(layers)
         self.layers.eval()
         if stage:
             stage('weights_on_device')
