@@ -2,6 +2,7 @@
 # variants (each its own bounded run; stop at the first failure).
 #   bash tools/gpu_round2_variants.sh A   -> default + strict + 2 queues + idle-interval
 #   bash tools/gpu_round2_variants.sh B   -> job KEYS_PER_POD=4 + 60 s-burst long form
+#   bash tools/gpu_round2_variants.sh C   -> PyTorch plug-in engine (WORKER_ENGINE)
 set -o pipefail
 OUT=${OUT:-gpurun_out/r2_variants}
 mkdir -p $OUT
@@ -20,6 +21,11 @@ if [ "$1" = "A" ]; then
   run strict 200 --gpus 1 --steps 10 --warmup 1 --policy strict --budget-s 180 && \
   run two_queues 200 --gpus 1 --steps 10 --warmup 1 --queues predict,track --budget-s 180 && \
   run idle_interval_0.1 200 --gpus 1 --steps 10 --warmup 1 --idle-interval 0.1 --budget-s 180
+elif [ "$1" = "C" ]; then
+  # a user's PyTorch model as the engine (WORKER_ENGINE plug-in): the same
+  # standby / recycle / cache path, torch imported by the standby at boot
+  WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine \
+    run torch_plugin 260 --gpus 1 --steps 8 --warmup 1 --budget-s 240
 else
   run job_kpp4_strict 260 --gpus 1 --steps 6 --warmup 1 --resource-type job --kpp 4 --on 8 --lam-per-gpu 1.0 --policy strict --budget-s 240 && \
   run job_kpp4_reference 260 --gpus 1 --steps 6 --warmup 1 --resource-type job --kpp 4 --on 8 --lam-per-gpu 1.0 --budget-s 240 --drain-timeout 20 && \
