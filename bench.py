@@ -341,9 +341,11 @@ def tick_instants(events):
     return sorted(out)
 
 
-def reference_sim(episodes, events, args, same_grid=True):
+def reference_sim(episodes, events, args, same_grid=True, ready_delay=0.0):
     """The reference policy + ideal actuator on each episode's trace, at the
-    live loop's tick instants (``same_grid``) or on an ideal grid."""
+    live loop's tick instants (``same_grid``) or on an ideal grid.  With
+    ``ready_delay`` > 0 the actuator instead takes that long per scale-up
+    (a Kubernetes pod start: BASELINE.md's D)."""
     from kiosk_autoscaler_amd.bench import sim
     ticks = tick_instants(events)
     results = []
@@ -362,14 +364,15 @@ def reference_sim(episodes, events, args, same_grid=True):
         arrivals = [((t - base) / 1e9 + shift + offset, q)
                     for _, q, t in ep['keys']]
         kwargs = {'horizon': (ep['t_end'] - base) / 1e9 + shift +
-                  3 * args.interval}
+                  3 * args.interval + 2 * ready_delay}
         if grid:
             kwargs['tick_times'] = [t + shift for t in grid]
         else:
             kwargs['first_tick'] = shift if same_grid else 0.0
         results.append(sim.simulate(
             arrivals, interval=args.interval, service_s=args.service_ms / 1e3,
-            ready_delay=0.0, max_pods=args.gpus, keys_per_pod=args.kpp,
+            ready_delay=ready_delay, max_pods=args.gpus,
+            keys_per_pod=args.kpp,
             queues=args.queues.split(','), policy='reference',
             tick_s=0.0, dt=0.001, **kwargs))
     # aggregate exactly like the live metrics: latency over all cold starts,
@@ -385,13 +388,13 @@ def reference_sim(episodes, events, args, same_grid=True):
             'gpu_idle_pct': 100.0 * (alive - busy) / alive if alive else None,
             'alive_s': alive, 'busy_s': busy,
             'grid': 'live tick instants' if same_grid else 'ideal',
-            'ready_delay_s': 0.0, 'episodes': results}
+            'ready_delay_s': ready_delay, 'episodes': results}
 
 
 def cold_spawn_cycle(svc, gen, args, budget):
     """One ``WARM_POOL=0`` cycle on GPU 0 after the timed region: the worker
-    process is spawned by the scale-up (no standby), so READY includes
-    interpreter + torch import, HIP context, weights and warm-start."""
+    process is spawned by the scale-up (no standby), so READY includes the
+    interpreter, the native module, HIP context, weights and warm-start."""
     from kiosk_autoscaler_amd.bench import metrics
     from kiosk_autoscaler_amd.utils.events import drain_redis
     svc.stop_scaler()
@@ -445,6 +448,10 @@ def parse_args():
                    help='wall-clock budget of the whole run (s)')
     p.add_argument('--cold-cycles', type=int, default=1,
                    help='WARM_POOL=0 cycles after the timed region (0 = off)')
+    p.add_argument('--pod-start-s', type=float, default=10.0,
+                   help='context figure: the reference policy on the same '
+                        'trace with a Kubernetes pod start of this many '
+                        'seconds (BASELINE.md D=10 row; 0 = off)')
     p.add_argument('--pool-timeout', type=float, default=300.0)
     p.add_argument('--idle-timeout', type=float, default=60.0)
     p.add_argument('--drain-timeout', type=float, default=120.0)
@@ -605,6 +612,11 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
     summary = metrics.summarize(events, episodes) if episodes else None
     ref = reference_sim(episodes, events, args, same_grid=True)
     ref_ideal = reference_sim(episodes, events, args, same_grid=False)
+    # context only (never vs_baseline): the same trace and ticks with the
+    # reference's real actuator, a pod start of --pod-start-s
+    ref_pod = (reference_sim(episodes, events, args, same_grid=True,
+                             ready_delay=args.pod_start_s)
+               if args.pod_start_s > 0 else None)
     cold = None
     if args.cold_cycles and args.backend in ('hip', 'cpu') and \
             budget.fits(2 * args.interval + 20.0):
@@ -623,6 +635,7 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
     value = summary['latency_mean_s']
     detail = {'summary': summary, 'reference_sim': ref,
               'reference_sim_ideal_grid': ref_ideal,
+              'reference_sim_pod_start': ref_pod,
               'derived_baseline': derived, 'cold_spawn': cold,
               'args': vars(args), 'amdsmi': util,
               'amdsmi_error': getattr(sampler, 'error', None),
@@ -671,6 +684,11 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         'fence': {k: _r(v) for k, v in fence.items()
                   if k not in ('fence_transport', 'fence_max_ranks')},
         'reference_sim_ideal_grid_latency_s': _r(ref_ideal['latency_mean_s']),
+        'reference_pod_start_s': args.pod_start_s,
+        'reference_sim_pod_start_latency_s': _r((ref_pod or {}).get(
+            'latency_mean_s')),
+        'reference_sim_pod_start_gpu_idle_pct': _r((ref_pod or {}).get(
+            'gpu_idle_pct')),
         'derived_baseline_latency_s': _r((derived or {}).get(
             'latency_mean_s')),
         'derived_baseline_gpu_idle_pct': _r((derived or {}).get(

@@ -3,6 +3,7 @@
 #   bash tools/gpu_round2_variants.sh A   -> default + strict + 2 queues + idle-interval
 #   bash tools/gpu_round2_variants.sh B   -> job KEYS_PER_POD=4 + 60 s-burst long form
 #   bash tools/gpu_round2_variants.sh C   -> PyTorch plug-in engine (WORKER_ENGINE)
+#   bash tools/gpu_round2_variants.sh D   -> INTERVAL=0.1 (reference loop, fast cadence)
 set -o pipefail
 OUT=${OUT:-gpurun_out/r2_variants}
 mkdir -p $OUT
@@ -21,6 +22,11 @@ if [ "$1" = "A" ]; then
   run strict 200 --gpus 1 --steps 10 --warmup 1 --policy strict --budget-s 180 && \
   run two_queues 200 --gpus 1 --steps 10 --warmup 1 --queues predict,track --budget-s 180 && \
   run idle_interval_0.1 200 --gpus 1 --steps 10 --warmup 1 --idle-interval 0.1 --budget-s 180
+elif [ "$1" = "D" ]; then
+  # the reference's own loop at INTERVAL=0.1: only viable with a ~1 ms
+  # actuator (with a pod start the same policy thrashes: see the
+  # reference_sim_pod_start_* context fields)
+  run interval_0.1 200 --gpus 1 --steps 20 --warmup 2 --interval 0.1 --budget-s 180
 elif [ "$1" = "C" ]; then
   # a user's PyTorch model as the engine (WORKER_ENGINE plug-in): the same
   # standby / recycle / cache path, torch imported by the standby at boot
