@@ -160,6 +160,12 @@ def test_bench_cpu_smoke(tmp_path):
         ref['gpu_idle_pct'], abs=1e-3)
     ep = detail['summary']['episodes'][0]
     assert ep['alive_s'] > 0 and ep['t_end'] > ep['t_first']
+    # context: the same policy, trace and ticks with a 10 s pod start
+    pod = detail['reference_sim_pod_start']
+    assert pod['ready_delay_s'] == 10.0 and line['reference_pod_start_s'] == 10
+    assert line['reference_sim_pod_start_latency_s'] == pytest.approx(
+        pod['latency_mean_s'], abs=1e-3)
+    assert pod['latency_mean_s'] >= ref['latency_mean_s'] + 9.9
 
 
 @pytest.mark.slow
