@@ -224,10 +224,11 @@ def main(argv=None):
     if backend == 'auto':
         backend = 'hip' if early and early.get('gpu') not in (None, '') \
             else 'cpu'
-    if backend == 'hip':
+    if backend == 'hip' and not os.environ.get('WORKER_ENGINE'):
         # the fence is this process's only RCCL user and moves 72 bytes: one
         # channel instead of RCCL's gfx950 default of 128 holds 166 MB of
-        # HBM per communicator instead of 670 MB (profiles/r2_rccl_init)
+        # HBM per communicator instead of 670 MB (profiles/r2_rccl_init);
+        # a plug-in engine may run collectives of its own: left alone
         os.environ.setdefault('NCCL_MIN_NCHANNELS', '1')
         os.environ.setdefault('NCCL_MAX_NCHANNELS', '1')
     if early is not None:
