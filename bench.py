@@ -8,7 +8,7 @@ the ``INTERVAL`` tick grid, Poisson arrivals at the config's rate continue
 for ``--on`` seconds, the queue drains and the autoscaler scales back to
 zero.  The whole product runs for real: ``scale.py`` (the
 reference-compatible CLI, embedded GPU manager) hands the work to
-PyTorch-ROCm workers pinned to MI355X GPUs; each builds its random-init
+worker processes pinned to MI355X GPUs; each builds its random-init
 model in HBM, runs the gfx950 warm-start kernel, publishes READY and serves
 keys with the MFMA MLP (1 s of GPU work per key, S of BASELINE.md §3), and
 READY-set changes are fenced with RCCL.  Warmup cycles carry one key each.
@@ -24,7 +24,9 @@ zero-delay actuator is simulated on the *identical* arrival trace and the
 the same-N, same-lambda figure: the measured value can only exceed it by
 the real actuation time (tick -> PATCH -> standby -> READY).  BASELINE.md's
 N=8 row (3.13 s) comes from a different trace and N and is reported for
-context only (``derived_baseline_*``).
+context only (``derived_baseline_*``), as is the reference policy on the
+same trace with its real actuator, a Kubernetes pod start of
+``--pod-start-s`` (BASELINE.md's D = 10 s; ``reference_sim_pod_start_*``).
 
 Accounting that the headline does not hide: ``standby_gpu_s`` (GPU-seconds
 held by standbys that own a HIP context) and ``cold_spawn_*`` (one
