@@ -150,6 +150,9 @@ EXTRA_DEFAULTS = (
     ('WORKER_BACKEND', str, 'auto'),        # auto | hip | cpu
     ('WARM_POOL', int, -1),                 # standby processes (-1 = MAX_PODS)
     ('WARM_POOL_MODE', str, 'device'),      # device (HIP ctx preinit) | import
+    # s with no demand after which the standbys exit (0 = keep them): the
+    # node then holds no GPU, the next scale-up is a cold spawn (~0.13 s)
+    ('POOL_IDLE_RELEASE_S', float, 0.0),
     ('WARM_START', bool, True),             # run the N1 warm-start kernel
     ('FENCE', str, 'auto'),                 # auto | rccl | store | none
     ('MODEL_DIM', int, 4096),

@@ -115,7 +115,8 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
                          worker_timeout=settings.WORKER_TIMEOUT,
                          start_timeout=settings.START_TIMEOUT,
                          recycle=settings.WORKER_RECYCLE,
-                         fence_comm=settings.FENCE_COMM)
+                         fence_comm=settings.FENCE_COMM,
+                         pool_idle_release_s=settings.POOL_IDLE_RELEASE_S)
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

@@ -265,7 +265,7 @@ class GpuManager(object):
                  pool_mode='device', state_ttl=3600,
                  fence_timeout=60.0, max_restart_backoff=10.0,
                  worker_timeout=0.0, start_timeout=0.0, recycle=True,
-                 fence_comm='node'):
+                 fence_comm='node', pool_idle_release_s=0.0):
         self.slots = list(slots)
         self.redis = redis_client
         self.pool_size = max(0, int(pool_size))
@@ -280,6 +280,11 @@ class GpuManager(object):
         self.start_timeout = float(start_timeout or 0.0)
         self.recycle = bool(recycle)
         self.retiring = []   # recycled processes told to exit
+        # deep idle: after this long without demand the standbys exit and
+        # the pool stays empty until the next scale-up (0 = never)
+        self.pool_idle_release_s = float(pool_idle_release_s or 0.0)
+        self.pool_parked = False
+        self._last_demand = time.monotonic()
         self.resources = collections.OrderedDict()
         self.standbys = collections.OrderedDict()   # slot index -> _Process
         self.lock = threading.RLock()
@@ -614,6 +619,12 @@ class GpuManager(object):
                 proc.pipe.close()
                 self.retiring.remove(proc)
                 changed = True
+        if self._park_pool():
+            changed = True
+        if self.pool_parked:
+            if changed:
+                self._publish_pool()
+            return
         for slot in self._free_slots()[:self.pool_size]:
             if slot.index not in self.standbys:
                 self.standbys[slot.index] = self._spawn(
@@ -621,6 +632,41 @@ class GpuManager(object):
                 changed = True
         if changed:
             self._publish_pool()
+
+    def _park_pool(self):
+        """Deep idle (``POOL_IDLE_RELEASE_S``): with no declared or live
+        worker for that long, retire every standby -- the node then holds
+        no GPU, like the reference at zero replicas -- and keep the pool
+        empty until demand returns; the first scale-up after it is a cold
+        spawn and the pool refills behind it.  True if standbys were
+        retired."""
+        now = time.monotonic()
+        demand = any(r.declared > 0 or any(w.state != EXITED
+                                           for w in r.workers.values())
+                     for r in self.resources.values())
+        if demand:
+            self._last_demand = now
+            if self.pool_parked:
+                self.pool_parked = False
+                self.events.emit('pool_resumed')
+                logger.info('Demand returned: refilling the warm pool.')
+            return False
+        if (self.pool_idle_release_s <= 0 or self.pool_parked or
+                now - self._last_demand < self.pool_idle_release_s):
+            return False
+        self.pool_parked = True
+        released = 0
+        for index, proc in list(self.standbys.items()):
+            if proc.popen.poll() is None:
+                proc.pipe.send({'cmd': 'exit'})
+                self.retiring.append(proc)
+                released += 1
+            del self.standbys[index]
+        self.events.emit('pool_parked', standbys=released,
+                         idle_s=round(now - self._last_demand, 3))
+        logger.info('No demand for %.0f s: released %d standby process(es).',
+                    now - self._last_demand, released)
+        return True
 
     def _take_standby(self, template, slot):
         """The standby pinned to ``slot`` (booted or still booting: it

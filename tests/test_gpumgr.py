@@ -322,3 +322,57 @@ def test_gpu_cold_spawn_opens_the_device_in_parallel(resp_server):
         until(lambda: ready_worker() is None, 60)
     finally:
         manager.stop()
+
+
+def test_pool_parks_after_idle_and_refills_on_demand(resp_server):
+    """``POOL_IDLE_RELEASE_S``: after that long without demand the standbys
+    exit (the node holds no GPU, like the reference at zero replicas); the
+    next scale-up is a cold spawn, served normally, and the pool refills
+    behind it."""
+    import time
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict', 'RESOURCE_NAME': 'park', 'MAX_PODS': '1',
+           'WORKER_BACKEND': 'cpu', 'WARM_POOL': '1', 'FENCE': 'none',
+           'REDIS_INTERVAL': '0', 'POOL_IDLE_RELEASE_S': '0.3'}
+    s = Settings(Config(environ=env, use_files=False))
+    assert s.POOL_IDLE_RELEASE_S == 0.3
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    events = EventLog(source='test')
+    events.keep = True
+    manager = gpumgr.build_manager(s, redis_client=client,
+                                   events=events).start()
+
+    def until(predicate, timeout=30):
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            if predicate():
+                return
+            time.sleep(0.02)
+        raise AssertionError('timed out')
+
+    def kinds():
+        return [e['ev'] for e in events.records]
+    try:
+        until(lambda: 'pool_parked' in kinds())
+        until(lambda: not manager.standbys and not manager.retiring)
+        assert client.get('kiosk:pool').split()[:2] == ['0', '0']
+        client.hset('predict:k', mapping={'status': 'new'})
+        client.lpush('predict', 'predict:k')
+        manager.patch_namespaced_deployment('park', 'default',
+                                            {'spec': {'replicas': 1}})
+        until(lambda: client.hget('predict:k', 'status') == 'done')
+        assert 'pool_resumed' in kinds()
+        spawned = [e for e in events.records if e['ev'] == 'worker_assigned']
+        assert spawned and spawned[-1]['from_pool'] is False   # cold spawn
+        manager.patch_namespaced_deployment('park', 'default',
+                                            {'spec': {'replicas': 0}})
+        # the drained worker is recycled into the pool ...
+        until(lambda: len(manager.standbys) == 1)
+        # ... and parked again after the next idle period
+        until(lambda: kinds().count('pool_parked') == 2)
+    finally:
+        manager.stop()
