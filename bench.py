@@ -29,7 +29,9 @@ same trace with its real actuator, a Kubernetes pod start of
 ``--pod-start-s`` (BASELINE.md's D = 10 s; ``reference_sim_pod_start_*``).
 
 Accounting that the headline does not hide: ``standby_gpu_s`` (GPU-seconds
-held by standbys that own a HIP context) and ``cold_spawn_*`` (one
+held by standbys that own a HIP context; what they hold is HBM only,
+``standby_pool_boot_hbm_mib`` / ``idle_node_hbm_*`` from amdsmi device VRAM)
+and ``cold_spawn_*`` (one
 ``WARM_POOL=0`` cycle after the timed region: spawn -> import -> HIP
 context -> weights -> warm-start -> READY).
 
@@ -125,6 +127,12 @@ class Services(object):
     def start(self):
         args = self.args
         kredis = ensure_built(kernels=args.backend == 'hip')
+        # HBM reference points: before any process of the run exists, and
+        # once the standby pool (and its node communicator) has booted
+        self.vram0 = self.vram_pool = None
+        bdfs = managed_bdfs(self.n) if args.backend == 'hip' else None
+        if bdfs:
+            self.vram0 = gpu_util.vram_snapshot(bdfs)
         if os.path.exists(kredis):
             cmd = [kredis, '--port', str(self.port)]
         else:
@@ -139,6 +147,8 @@ class Services(object):
                                  decode_responses=True)
         wait_for(lambda: self._ping(), 20, what='redis')
         self.start_scaler(self.n, pool=self.n, timeout=args.pool_timeout)
+        if bdfs and self.vram0:
+            self.vram_pool = gpu_util.vram_snapshot(bdfs)
         return self
 
     def start_scaler(self, n_gpus, pool, timeout, tag='bench'):
@@ -612,6 +622,11 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
     from kiosk_autoscaler_amd.utils.events import drain_redis
     events = drain_redis(svc.redis)
     summary = metrics.summarize(events, episodes) if episodes else None
+    hbm = None
+    if episodes and sampler is not None and hasattr(sampler, 'vram'):
+        hbm = metrics.hbm_hold(events, sampler.vram(),
+                               episodes[0]['t_first'], episodes[-1]['t_end'],
+                               baseline=svc.vram0, pool_boot=svc.vram_pool)
     ref = reference_sim(episodes, events, args, same_grid=True)
     ref_ideal = reference_sim(episodes, events, args, same_grid=False)
     # context only (never vs_baseline): the same trace and ticks with the
@@ -639,6 +654,7 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
               'reference_sim_ideal_grid': ref_ideal,
               'reference_sim_pod_start': ref_pod,
               'derived_baseline': derived, 'cold_spawn': cold,
+              'hbm_hold': hbm,
               'args': vars(args), 'amdsmi': util,
               'amdsmi_error': getattr(sampler, 'error', None),
               'cycles_s': [ep['cycle_s'] for ep in episodes]}
@@ -666,6 +682,15 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         'gpu_alive_s': _r(summary['gpu_alive_s']),
         'gpu_busy_s': _r(summary['gpu_busy_s']),
         'gpu_idle_incl_standby_pct': _r(summary['gpu_idle_incl_standby_pct']),
+        # what that standby time holds: HBM only, no kernels (amdsmi device
+        # VRAM over the pre-run baseline, per GPU: fresh pool, and the
+        # median while no worker is alive -- recycled standbys keep their
+        # engine -- which includes this rank's own torch context)
+        'standby_pool_boot_hbm_mib': _r((hbm or {}).get('pool_boot_mib'), 1),
+        'idle_node_hbm_mib': _r((hbm or {}).get('idle_mib_median'), 1),
+        'idle_node_hbm_pct_of_gpu': _r((hbm or {}).get('idle_pct_of_gpu'),
+                                       3),
+        'serving_hbm_mib_max': _r((hbm or {}).get('serving_mib_max'), 1),
         'cold_starts': summary['cold_starts'],
         'first_key_latency_mean_s': _r(summary['first_key_latency_mean_s']),
         'latency_p50_s': _r(summary['latency_p50_s']),
@@ -702,21 +727,27 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
     return line
 
 
-def start_util_sampler(n_gpus):
-    """amdsmi gfx-activity sampling over the managed GPUs (None on CPU)."""
+def managed_bdfs(n_gpus):
+    """PCI addresses of the GPUs the run manages (None if not found)."""
     if os.environ.get('KIOSK_AMDSMI', '1') == '0':
         return None
-    bdfs = None
     try:
         from kiosk_autoscaler_amd.gpumgr import gpus
         slots = gpus.discover(','.join(str(i) for i in range(n_gpus)),
                               env={}, cpu_slots=0)
         found = [s.pci for s in slots if getattr(s, 'pci', None)]
         if len(found) == n_gpus:
-            bdfs = found
+            return found
     except Exception:  # pylint: disable=broad-except
         pass
-    sampler = gpu_util.UtilSampler(0.1, bdfs)
+    return None
+
+
+def start_util_sampler(n_gpus):
+    """amdsmi gfx-activity sampling over the managed GPUs (None on CPU)."""
+    if os.environ.get('KIOSK_AMDSMI', '1') == '0':
+        return None
+    sampler = gpu_util.UtilSampler(0.1, managed_bdfs(n_gpus))
     sampler.start()
     return sampler
 

@@ -191,6 +191,60 @@ def standby_gpu(events, t_lo, t_hi):
     return total / 1e9
 
 
+def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
+    """What the node holds in HBM, by phase (the memory behind
+    ``standby_gpu_s``; a standby runs no kernels, so HBM is all it holds).
+
+    ``vram`` is :meth:`..gpu_util.UtilSampler.vram` (per-device
+    ``(t_ns, vram_used MiB)`` samples); ``baseline`` / ``pool_boot`` are
+    :func:`..gpu_util.vram_snapshot` results taken before any process of
+    the run existed and after the standby pool booted (fresh standbys: HIP
+    context, code objects, node communicator; no engine yet).  Samples in
+    [t_lo, t_hi] are split by whether any worker was alive (assigned, not
+    exited): with none, the device holds the standbys -- recycled ones keep
+    their engine -- plus the benchmark rank's own context.  Figures are per
+    device over the baseline, the max over devices.  ``None`` without
+    samples."""
+    device = (vram or {}).get('device') or {}
+    if not any(device.values()):
+        return None
+    spans = []
+    open_at = {}
+    for e in sorted(events, key=lambda e: e.get('t', 0)):
+        if e.get('ev') == 'worker_assigned':
+            open_at.setdefault(e.get('worker'), e['t'])
+        elif e.get('ev') == 'worker_exit' and e.get('worker') in open_at:
+            spans.append((open_at.pop(e.get('worker')), e['t']))
+    spans += [(t, t_hi) for t in open_at.values()]
+
+    def serving(t):
+        return any(a <= t <= b for a, b in spans)
+    base = baseline or {}
+    idle, busy = [], []
+    for bdf, samples in device.items():
+        zero = base.get(bdf, 0.0)
+        for t, used in samples:
+            if t_lo <= t <= t_hi:
+                (busy if serving(t) else idle).append(used - zero)
+    totals = [v for v in ((vram or {}).get('total_mib') or {}).values() if v]
+    total = max(totals) if totals else None
+    boot = None
+    if pool_boot and baseline:
+        boot = max(pool_boot[b] - baseline.get(b, 0.0) for b in pool_boot)
+    idle_mib = _pct(idle, 0.5)
+    return {
+        'baseline_mib': max(base.values()) if base else None,
+        'pool_boot_mib': boot,
+        'idle_mib_median': idle_mib,
+        'serving_mib_max': max(busy) if busy else None,
+        'idle_pct_of_gpu': (100.0 * idle_mib / total
+                            if idle_mib is not None and total else None),
+        'hbm_total_mib': total,
+        'samples': {'idle': len(idle), 'serving': len(busy)},
+        'over_baseline': bool(base),
+    }
+
+
 def fence_stats(events):
     """N4 membership fences seen in the run: transport(s), count, mean wall
     time (manager: epoch start -> rank 0 ack), communicator set-up and

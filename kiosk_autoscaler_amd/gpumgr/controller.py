@@ -614,10 +614,14 @@ class GpuManager(object):
             if proc.popen.poll() is not None:
                 proc.pipe.close()
                 del self.standbys[index]
+                self.events.emit('standby_exit', pid=proc.pid, slot=index,
+                                 code=proc.popen.returncode)
         for proc in list(self.retiring):
             if proc.popen.poll() is not None:
                 proc.pipe.close()
                 self.retiring.remove(proc)
+                self.events.emit('standby_exit', pid=proc.pid, slot=proc.slot,
+                                 code=proc.popen.returncode, retired=True)
                 changed = True
         if self._park_pool():
             changed = True

@@ -204,6 +204,33 @@ def test_util_sampler_degrades_without_driver():
         == 20.0
 
 
+def test_hbm_hold_splits_device_vram_by_phase():
+    """Device VRAM samples are split by whether a worker was alive, over
+    the pre-run baseline; standby_exit closes a standby's GPU time."""
+    from kiosk_autoscaler_amd.bench import metrics
+    events = [
+        {'ev': 'standby_ready', 't': 100, 'pid': 7, 'preinit': 'device'},
+        {'ev': 'worker_assigned', 't': 200, 'pid': 7, 'worker': 'w0'},
+        {'ev': 'worker_exit', 't': 300, 'worker': 'w0'},
+        {'ev': 'standby_ready', 't': 300, 'pid': 7, 'recycled': True},
+        {'ev': 'standby_exit', 't': 400, 'pid': 7},
+    ]
+    vram = {'device': {'bdf': [(150, 900.0), (250, 3900.0), (350, 2900.0),
+                               (360, 2900.0), (2000, 5000.0)]},
+            'total_mib': {'bdf': 294912.0}}
+    out = metrics.hbm_hold(events, vram, 0, 1000, baseline={'bdf': 300.0},
+                           pool_boot={'bdf': 800.0})
+    assert out['samples'] == {'idle': 3, 'serving': 1}
+    assert out['pool_boot_mib'] == 500.0
+    assert out['idle_mib_median'] == 2600.0
+    assert out['serving_mib_max'] == 3600.0
+    assert abs(out['idle_pct_of_gpu'] - 100 * 2600 / 294912) < 1e-9
+    assert metrics.hbm_hold(events, None, 0, 1000) is None
+    assert metrics.hbm_hold(events, {'device': {'bdf': []}}, 0, 1) is None
+    # a standby that exited stops counting toward standby_gpu_s
+    assert metrics.standby_gpu(events, 0, 1000) == (100 + 100) / 1e9
+
+
 def test_bench_tick_inproc_runs():
     """tools/bench_tick.py (control-plane tick cost) on the in-proc fake."""
     proc = subprocess.run(
