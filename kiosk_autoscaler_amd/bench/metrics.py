@@ -262,6 +262,10 @@ def fence_stats(events):
             str(e.get('mode')) for e in done)),
         'node_comm_generations': sum(1 for e in events
                                      if e.get('ev') == 'node_comm_ready'),
+        # RCCL could not build the node communicator: the fallback
+        # transport (FENCE_FALLBACK) fenced instead
+        'node_comm_fallbacks': sum(1 for e in events
+                                   if e.get('ev') == 'node_comm_fallback'),
         'node_comm_init_ms_max': max([float(e.get('init_ms') or 0.0)
                                       for e in events
                                       if e.get('ev') == 'node_comm_ready'],

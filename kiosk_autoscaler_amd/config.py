@@ -171,6 +171,11 @@ EXTRA_DEFAULTS = (
     ('START_TIMEOUT', float, 0.0),
     ('WORKER_RECYCLE', bool, True),         # drained worker -> warm pool
     ('FENCE_COMM', str, 'node'),            # node (persistent) | epoch
+    # node communicator transport after FENCE_FALLBACK_AFTER consecutive
+    # failed generations ('' = keep retrying RCCL): membership keeps being
+    # fenced, over Redis, if RCCL cannot build the node communicator
+    ('FENCE_FALLBACK', str, 'store'),
+    ('FENCE_FALLBACK_AFTER', int, 2),
     ('METRICS_PORT', int, 0),               # Prometheus /metrics port (0 = off)
     ('METRICS_ADDR', str, '0.0.0.0'),
     ('DEBUG', bool, True),

@@ -116,7 +116,9 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
                          start_timeout=settings.START_TIMEOUT,
                          recycle=settings.WORKER_RECYCLE,
                          fence_comm=settings.FENCE_COMM,
-                         pool_idle_release_s=settings.POOL_IDLE_RELEASE_S)
+                         pool_idle_release_s=settings.POOL_IDLE_RELEASE_S,
+                         fence_fallback=settings.FENCE_FALLBACK,
+                         fence_fallback_after=settings.FENCE_FALLBACK_AFTER)
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

@@ -265,7 +265,8 @@ class GpuManager(object):
                  pool_mode='device', state_ttl=3600,
                  fence_timeout=60.0, max_restart_backoff=10.0,
                  worker_timeout=0.0, start_timeout=0.0, recycle=True,
-                 fence_comm='node', pool_idle_release_s=0.0):
+                 fence_comm='node', pool_idle_release_s=0.0,
+                 fence_fallback='store', fence_fallback_after=2):
         self.slots = list(slots)
         self.redis = redis_client
         self.pool_size = max(0, int(pool_size))
@@ -310,7 +311,9 @@ class GpuManager(object):
                 pool_template is not None and self.slots and
                 self.pool_size >= len(self.slots) and
                 (pool_mode == 'device' or pool_template.backend == 'cpu')):
-            self.node = NodeComm(self, fence_timeout=min(fence_timeout, 30.0))
+            self.node = NodeComm(self, fence_timeout=min(fence_timeout, 30.0),
+                                 fallback=fence_fallback,
+                                 fallback_after=fence_fallback_after)
 
     # ------------------------------------------------------------------
     # API (the kubernetes AppsV1Api / BatchV1Api analogs)

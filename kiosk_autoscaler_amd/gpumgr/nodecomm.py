@@ -25,8 +25,16 @@ NODE_EVENTS = ('comm_uid', 'comm_ready', 'fenced', 'node_agent')
 
 
 class NodeComm(object):
-    def __init__(self, manager, init_timeout=120.0, fence_timeout=30.0):
+    def __init__(self, manager, init_timeout=120.0, fence_timeout=30.0,
+                 fallback='store', fallback_after=2):
         self.m = manager
+        # after ``fallback_after`` consecutive failed generations the next
+        # ones use the ``fallback`` transport (every rank switches in its
+        # ``comm_init``): membership stays fenced when RCCL cannot build the
+        # node communicator; the JSON/metrics name the transport in use
+        self.fallback = fallback or None
+        self.fallback_after = max(1, int(fallback_after))
+        self.transport_override = None
         self.init_timeout = float(init_timeout)
         self.fence_timeout = float(fence_timeout)
         self.gen = 0
@@ -107,11 +115,15 @@ class NodeComm(object):
         self.t_start = now
         n = len(members)
         for rank, (_, proc) in enumerate(members):
-            proc.pipe.send({'cmd': 'comm_init', 'gen': self.gen, 'rank': rank,
-                            'nranks': n})
+            message = {'cmd': 'comm_init', 'gen': self.gen, 'rank': rank,
+                       'nranks': n}
+            if self.transport_override:
+                message['transport'] = self.transport_override
+            proc.pipe.send(message)
         self.m.events.emit('node_comm_init', gen=self.gen, n=n,
                            slots=[index for index, _ in members],
-                           pids=[proc.pid for _, proc in members])
+                           pids=[proc.pid for _, proc in members],
+                           transport=self.transport_override)
         logger.info('Node communicator generation %d: %d ranks.', self.gen, n)
         self.m._publish_pool()
 
@@ -133,6 +145,16 @@ class NodeComm(object):
             self.failures += 1
             self.retry_at = now + min(30.0, 0.25 * 2 ** min(self.failures - 1,
                                                              8))
+            if (self.fallback and self.transport_override is None and
+                    self.failures >= self.fallback_after):
+                self.transport_override = self.fallback
+                self.retry_at = now
+                self.m.events.emit('node_comm_fallback', gen=self.gen,
+                                   transport=self.fallback,
+                                   failures=self.failures)
+                logger.warning('Node communicator: %d failed generations, '
+                               'falling back to the %s transport.',
+                               self.failures, self.fallback)
         else:
             self.retry_at = now
         self.m.events.emit('node_comm_break', gen=self.gen, reason=reason,

@@ -237,9 +237,13 @@ class NodeFenceAgent(object):
     kernel is not queued behind a whole key of GEMMs."""
 
     def __init__(self, slot, transport, channel=None, events=None,
-                 uid_timeout=60.0):
+                 uid_timeout=60.0, transport_factory=None):
         self.slot = int(slot)
         self.transport = transport
+        # kind -> transport, for a manager-requested switch (the fallback
+        # after failed RCCL generations, gpumgr/nodecomm.py)
+        self.transport_factory = transport_factory or (
+            lambda kind: choose_node_transport(kind, 'hip'))
         self.channel = channel
         self.events = events
         self.uid_timeout = float(uid_timeout)
@@ -303,6 +307,13 @@ class NodeFenceAgent(object):
         gen, rank = int(message['gen']), int(message['rank'])
         nranks = int(message['nranks'])
         self._drop()
+        wanted = message.get('transport')
+        if wanted and wanted != self.transport.name:
+            try:
+                self.transport = self.transport_factory(wanted)
+            except Exception as err:  # pylint: disable=broad-except
+                logger.warning('cannot switch to transport %s: %s', wanted,
+                               err)
         t0 = time.perf_counter()
         try:
             if self._aborted(gen):

@@ -191,6 +191,107 @@ def test_fence_on_a_stale_generation_fails():
     assert agent.close()
 
 
+def test_agent_switches_transport_when_the_manager_asks():
+    """A ``comm_init`` naming another transport (the manager's fallback
+    after failed RCCL generations) swaps the agent's transport first."""
+    native = _FakeNative()
+    chan = _Channel()
+    made = []
+
+    class _Stub(object):
+        name = 'store'
+
+        def make_uid(self, gen):
+            return 'u%d' % gen
+
+        def connect(self, gen, rank, nranks, uid, should_abort=None):
+            made.append(('connect', gen, rank, nranks, uid))
+
+        def close(self):
+            made.append(('close',))
+
+        def request_abort(self):
+            pass
+    agent = NodeFenceAgent(0, nodefence.RcclNodeTransport(native=native),
+                           channel=chan,
+                           transport_factory=lambda kind: _Stub())
+    agent.submit({'cmd': 'comm_init', 'gen': 3, 'rank': 0, 'nranks': 2,
+                  'transport': 'store'})
+    ready = chan.next('comm_ready')
+    assert ready['ok'] and ready['transport'] == 'store'
+    assert ('connect', 3, 0, 2, 'u3') in made
+    assert not any(c[0] == 'connect' for c in native.calls)  # RCCL unused
+    assert agent.close()
+
+
+class _FakeProc(object):
+    def __init__(self, pid):
+        self.pid = pid
+        self.node_ok = True
+        self.eof = False
+        self.sent = []
+        self.pipe = self
+        self.popen = self
+
+    def poll(self):
+        return None
+
+    def send(self, message):
+        self.sent.append(message)
+
+
+class _FakeManager(object):
+    def __init__(self, n):
+        from kiosk_autoscaler_amd.gpumgr.gpus import GpuSlot
+        self.slots = [GpuSlot(i, str(i)) for i in range(n)]
+        self.standbys = {i: _FakeProc(100 + i) for i in range(n)}
+        self.resources = {}
+        self.retiring = []
+        self.emitted = []
+        self.events = self
+
+    def emit(self, ev, **fields):
+        self.emitted.append(dict(fields, ev=ev))
+
+    def _publish_pool(self):
+        pass
+
+
+def test_node_comm_falls_back_after_failed_generations():
+    """Two RCCL generations that fail to connect -> the third (and later)
+    ``comm_init`` asks every rank for the fallback transport."""
+    from kiosk_autoscaler_amd.gpumgr.nodecomm import NodeComm
+    manager = _FakeManager(2)
+    node = NodeComm(manager, fallback='store', fallback_after=2)
+    procs = [manager.standbys[0], manager.standbys[1]]
+    for gen in (1, 2):
+        node.step()
+        init = procs[1].sent[-1]
+        assert init['cmd'] == 'comm_init' and init['gen'] == gen
+        assert 'transport' not in init
+        node.on_message(procs[1], {'ev': 'comm_ready', 'gen': gen, 'rank': 1,
+                                   'ok': False, 'detail': 'rccl refused'})
+        node.retry_at = 0.0
+    assert [e['ev'] for e in manager.emitted].count('node_comm_fallback') == 1
+    node.step()
+    init = procs[0].sent[-1]
+    assert init['gen'] == 3 and init['transport'] == 'store'
+    for rank in (0, 1):
+        node.on_message(procs[rank], {'ev': 'comm_ready', 'gen': 3,
+                                      'rank': rank, 'ok': True,
+                                      'transport': 'store', 'init_ms': 1.0})
+    assert node.ready and node.transport == 'store'
+    # disabled: keeps retrying the configured transport
+    manager = _FakeManager(1)
+    node = NodeComm(manager, fallback='', fallback_after=1)
+    node.step()
+    node.on_message(manager.standbys[0], {'ev': 'comm_ready', 'gen': 1,
+                                          'rank': 0, 'ok': False})
+    node.retry_at = 0.0
+    node.step()
+    assert 'transport' not in manager.standbys[0].sent[-1]
+
+
 def test_store_node_transport_three_ranks(redis_client):
     transports = [nodefence.StoreNodeTransport(redis=redis_client, timeout=5)
                   for _ in range(3)]
