@@ -132,7 +132,14 @@ class Services(object):
         self.vram0 = self.vram_pool = None
         bdfs = managed_bdfs(self.n) if args.backend == 'hip' else None
         if bdfs:
-            self.vram0 = gpu_util.vram_snapshot(bdfs)
+            # min of a few reads: memory a previous tenant of the GPU left
+            # may still be draining (one box read 231 GB used here)
+            reads = []
+            for _ in range(5):
+                reads.append(gpu_util.vram_snapshot(bdfs) or {})
+                time.sleep(0.2)
+            self.vram0 = {b: min(r[b] for r in reads if b in r)
+                          for b in reads[-1]} or None
         if os.path.exists(kredis):
             cmd = [kredis, '--port', str(self.port)]
         else:
@@ -149,6 +156,12 @@ class Services(object):
         self.start_scaler(self.n, pool=self.n, timeout=args.pool_timeout)
         if bdfs and self.vram0:
             self.vram_pool = gpu_util.vram_snapshot(bdfs)
+            if self.vram_pool and any(self.vram_pool.get(b, 0.0) < v
+                                      for b, v in self.vram0.items()):
+                log('HBM baseline %s above the booted pool %s: not a '
+                    'baseline, HBM reported absolute' % (self.vram0,
+                                                         self.vram_pool))
+                self.vram0 = None
         return self
 
     def start_scaler(self, n_gpus, pool, timeout, tag='bench'):

@@ -220,6 +220,8 @@ def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
     def serving(t):
         return any(a <= t <= b for a, b in spans)
     base = baseline or {}
+    if pool_boot and any(pool_boot.get(b, 0.0) < v for b, v in base.items()):
+        base = {}      # the "baseline" held memory the run later did not
     idle, busy = [], []
     for bdf, samples in device.items():
         zero = base.get(bdf, 0.0)
@@ -229,8 +231,8 @@ def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
     totals = [v for v in ((vram or {}).get('total_mib') or {}).values() if v]
     total = max(totals) if totals else None
     boot = None
-    if pool_boot and baseline:
-        boot = max(pool_boot[b] - baseline.get(b, 0.0) for b in pool_boot)
+    if pool_boot:
+        boot = max(pool_boot[b] - base.get(b, 0.0) for b in pool_boot)
     idle_mib = _pct(idle, 0.5)
     return {
         'baseline_mib': max(base.values()) if base else None,

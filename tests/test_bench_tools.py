@@ -227,6 +227,12 @@ def test_hbm_hold_splits_device_vram_by_phase():
     assert abs(out['idle_pct_of_gpu'] - 100 * 2600 / 294912) < 1e-9
     assert metrics.hbm_hold(events, None, 0, 1000) is None
     assert metrics.hbm_hold(events, {'device': {'bdf': []}}, 0, 1) is None
+    # a baseline above the booted pool is no baseline: absolute figures
+    out = metrics.hbm_hold(events, vram, 0, 1000,
+                           baseline={'bdf': 231000.0},
+                           pool_boot={'bdf': 800.0})
+    assert not out['over_baseline'] and out['pool_boot_mib'] == 800.0
+    assert out['idle_mib_median'] == 2900.0
     # a standby that exited stops counting toward standby_gpu_s
     assert metrics.standby_gpu(events, 0, 1000) == (100 + 100) / 1e9
 
