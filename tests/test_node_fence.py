@@ -521,7 +521,8 @@ def test_gpu_failing_node_comm_never_blocks_serving(resp_server):
     generation fails (RCCL refuses a duplicate GPU) and is retried with
     backoff -- the multi-GPU failure this pool cannot stage otherwise.
     Scale-up, READY and serving must not wait on it: the fence is off the
-    critical path."""
+    critical path.  After FENCE_FALLBACK_AFTER (2) refused generations the
+    ranks switch to the store transport and membership is fenced again."""
     from kiosk_autoscaler_amd import Autoscaler, gpumgr
     from kiosk_autoscaler_amd.config import Config, Settings
     from kiosk_autoscaler_amd.redisq import RedisClient, StrictRedis
@@ -547,7 +548,11 @@ def test_gpu_failing_node_comm_never_blocks_serving(resp_server):
         # the first generation has been tried (and, normally, refused)
         wait_for(lambda: any(e['ev'] in ('node_comm_break', 'node_comm_ready')
                              for e in events.records), timeout=120)
+        refused = any(e['ev'] == 'node_comm_break' for e in events.records)
         for cycle in range(2):
+            if cycle == 1 and refused:
+                # by now the fallback generation (store) is up
+                wait_for(lambda: manager.node.ready, timeout=90)
             item = 'predict:dup%d' % cycle
             client.hset(item, mapping={'status': 'new', 'rows': 256})
             client.lpush('predict', item)
@@ -560,13 +565,26 @@ def test_gpu_failing_node_comm_never_blocks_serving(resp_server):
             wait_for(lambda: not [w for r in manager.resources.values()
                                   for w in r.workers.values()
                                   if w.state == 'ready'], timeout=60)
+        if refused:
+            wait_for(lambda: any(e['ev'] == 'fence_done' and
+                                 e.get('transport') == 'store'
+                                 for e in events.records), timeout=60)
     finally:
         manager.stop(timeout=20)
     breaks = [e for e in events.records if e['ev'] == 'node_comm_break']
     ready = [e for e in events.records if e['ev'] == 'node_comm_ready']
+    print('node communicator events:', [
+        (e['ev'], e.get('gen'), e.get('transport'))
+        for e in events.records
+        if e['ev'].startswith('node_comm') or e['ev'] == 'fence_done'])
     # either RCCL refused the pair (failed generations, retried) or it
     # accepted it; serving never depended on which
     assert (breaks and all(b['failed'] for b in breaks)) or ready
+    if refused:
+        fallback = [e for e in events.records
+                    if e['ev'] == 'node_comm_fallback']
+        assert len(fallback) == 1 and fallback[0]['transport'] == 'store'
+        assert any(e.get('transport') == 'store' for e in ready)
 
 
 _RANK_SCRIPT = r'''
