@@ -204,6 +204,64 @@ def test_util_sampler_degrades_without_driver():
         == 20.0
 
 
+class _FakeAmdSmi(object):
+    """The amdsmi calls gpu_util makes, for a CPU run."""
+
+    def __init__(self, bdfs=('0000:f4:00.0', '0000:75:00.0')):
+        self.handles = list(bdfs)
+        self.calls = 0
+        self.down = 0
+
+    def amdsmi_init(self):
+        pass
+
+    def amdsmi_shut_down(self):
+        self.down += 1
+
+    def amdsmi_get_processor_handles(self):
+        return list(self.handles)
+
+    def amdsmi_get_gpu_device_bdf(self, handle):
+        return handle.upper()
+
+    def amdsmi_get_gpu_activity(self, handle):
+        self.calls += 1
+        return {'gfx_activity': 40 if handle.endswith('f4:00.0') else 'N/A'}
+
+    def amdsmi_get_gpu_vram_usage(self, handle):
+        return {'vram_total': 294896, 'vram_used': 1000 + self.calls}
+
+
+def test_util_sampler_with_fake_amdsmi(monkeypatch):
+    """Activity and device-VRAM sampling on a stand-in amdsmi (the GPU box
+    has the real one): matching devices only, timestamps on the event
+    clock, vram_snapshot for the bench's reference points."""
+    import time
+    from kiosk_autoscaler_amd.bench import gpu_util
+    fake = _FakeAmdSmi()
+    monkeypatch.setitem(sys.modules, 'amdsmi', fake)
+    sampler = gpu_util.UtilSampler(0.005, bdfs=['0000:F4:00.0'],
+                                   proc_period_s=0.005)
+    t0 = time.monotonic_ns()
+    assert sampler.start()
+    time.sleep(0.1)
+    result = sampler.stop()
+    assert list(result) == ['0000:f4:00.0']
+    assert result['0000:f4:00.0']['gfx_busy_pct'] == 40.0
+    vram = sampler.vram()
+    samples = vram['device']['0000:f4:00.0']
+    assert samples and all(t >= t0 and used > 1000 for t, used in samples)
+    assert vram['total_mib'] == {'0000:f4:00.0': 294896.0}
+    assert fake.down == 1
+    snap = gpu_util.vram_snapshot()
+    assert set(snap) == {'0000:f4:00.0', '0000:75:00.0'}
+    assert gpu_util.vram_snapshot(['0000:75:00.0']).keys() == {'0000:75:00.0'}
+    # a device filter that matches nothing is an error, not a silent run
+    sampler = gpu_util.UtilSampler(0.005, bdfs=['0000:00:00.0'])
+    assert not sampler.start() and 'no matching' in sampler.error
+    assert gpu_util.sample_for(0.02, 0.005, sleep=time.sleep) is not None
+
+
 def test_hbm_hold_splits_device_vram_by_phase():
     """Device VRAM samples are split by whether a worker was alive, over
     the pre-run baseline; standby_exit closes a standby's GPU time."""
