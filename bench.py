@@ -118,6 +118,7 @@ class Services(object):
         self.args = args
         self.n = n_gpus
         self.procs = []
+        self.bdfs = None
         self.port = free_port()
         self.scaler_proc = None
         self.stdout = None
@@ -131,6 +132,7 @@ class Services(object):
         # once the standby pool (and its node communicator) has booted
         self.vram0 = self.vram_pool = None
         bdfs = managed_bdfs(self.n) if args.backend == 'hip' else None
+        self.bdfs = bdfs
         if bdfs:
             # min of a few reads: memory a previous tenant of the GPU left
             # may still be draining (one box read 231 GB used here)
@@ -735,6 +737,8 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
             'gpu_idle_pct')),
         'baseline_md_n8': {'latency_s': BASELINE_N8_LATENCY_S,
                            'gpu_idle_pct': BASELINE_N8_IDLE_PCT},
+        # the PCI devices the run managed (N distinct GPUs at N > 1)
+        'gpu_bdfs': getattr(svc, 'bdfs', None),
         'wall_s': round(time.monotonic() - T_PROCESS_START, 1),
     })
     return line
