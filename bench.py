@@ -157,7 +157,20 @@ class Services(object):
         wait_for(lambda: self._ping(), 20, what='redis')
         self.start_scaler(self.n, pool=self.n, timeout=args.pool_timeout)
         if bdfs and self.vram0:
-            self.vram_pool = gpu_util.vram_snapshot(bdfs)
+            reads = []
+            for _ in range(3):
+                reads.append(gpu_util.vram_snapshot(bdfs) or {})
+                time.sleep(0.2)
+            self.vram_pool = {b: min(r[b] for r in reads if b in r)
+                              for b in reads[-1]} or None
+            if self.vram_pool and any(
+                    v - self.vram0.get(b, 0.0) > 64 * 1024
+                    for b, v in self.vram_pool.items()):
+                # a standby holds ~1.3 GiB: tens of GiB more is someone
+                # else's memory coming or going on the device
+                log('HBM after pool boot %s: not ours, dropped'
+                    % self.vram_pool)
+                self.vram_pool = None
             if self.vram_pool and any(self.vram_pool.get(b, 0.0) < v
                                       for b, v in self.vram0.items()):
                 log('HBM baseline %s above the booted pool %s: not a '

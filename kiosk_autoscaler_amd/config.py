@@ -149,7 +149,9 @@ EXTRA_DEFAULTS = (
     ('WORKER_MODULE', str, 'kiosk_autoscaler_amd.worker.main'),
     ('WORKER_BACKEND', str, 'auto'),        # auto | hip | cpu
     ('WARM_POOL', int, -1),                 # standby processes (-1 = MAX_PODS)
-    ('WARM_POOL_MODE', str, 'device'),      # device (HIP ctx preinit) | import
+    # device (HIP context + code objects + queue) | context (HIP context
+    # only: no HBM) | import (imports only)
+    ('WARM_POOL_MODE', str, 'device'),
     # s with no demand after which the standbys exit (0 = keep them): the
     # node then holds no GPU, the next scale-up is a cold spawn (~0.13 s)
     ('POOL_IDLE_RELEASE_S', float, 0.0),

@@ -305,6 +305,11 @@ class FenceAgent(object):
                 if self.channel is not None:
                     self.channel.emit('fenced', **report)
 
+    def abandon(self):
+        """The process is about to exit: stop taking epochs and leave the
+        communicator (and any collective still in flight) to process exit."""
+        self._queue.put(None)
+
     def close(self, timeout=5.0):
         """Stop the fence thread and release the communicator.  Returns
         ``False`` if the thread is still inside a collective: the

@@ -6,9 +6,12 @@ Two start modes (both spawned by :mod:`kiosk_autoscaler_amd.gpumgr`):
   anything loads, import the native kernel module (not PyTorch) and --
   with ``WARM_POOL_MODE=device``, the default -- create the HIP context,
   load every code object and size the LDS ring (``preinit_device``).  Such a
-  standby **holds its GPU** (context + code objects, no weights); the
-  benchmark reports that time as ``standby_gpu_s``.  With
-  ``WARM_POOL_MODE=import`` it stops after the imports and holds no GPU.
+  standby **holds its GPU** (context + code objects + a hardware queue,
+  ~1.3 GiB of HBM with the node communicator, no weights); the benchmark
+  reports that time as ``standby_gpu_s`` and the HBM as
+  ``standby_pool_boot_hbm_mib``.  ``WARM_POOL_MODE=context`` opens the HIP
+  context only (no queue, no RCCL: no HBM); ``import`` stops after the
+  imports and holds no GPU.
   Report ``standby`` and block on the command pipe.
 * **cold** (``--assign JSON``): start immediately.  The HIP context and
   the code objects are created on a helper thread (``preinit_device``
@@ -259,6 +262,19 @@ def main(argv=None):
                 # RCCL's one-time init costs seconds: pay it while idle (with
                 # the node communicator its first generation pays it)
                 preinit['rccl_warmup_ms'] = mod.fence_warmup(60.0)
+        except Exception as err:  # pylint: disable=broad-except
+            channel.emit('error', message='preinit failed: %s' % err)
+            return 4
+    elif pin and pin.get('preinit') == 'context' and backend == 'hip':
+        # the HIP context alone: no hardware queue (the first kernel launch
+        # creates one, ~0.5 GiB of device-side state) and no RCCL, so this
+        # standby holds no HBM (profiles/r2_hbm_hold/); the assignment pays
+        # the queue, code objects and engine
+        from ..ops import native
+        try:
+            t0 = time.monotonic_ns()
+            native.load().mem_info()
+            preinit = {'context_open': t0, 'context_done': time.monotonic_ns()}
         except Exception as err:  # pylint: disable=broad-except
             channel.emit('error', message='preinit failed: %s' % err)
             return 4

@@ -324,6 +324,78 @@ def test_gpu_cold_spawn_opens_the_device_in_parallel(resp_server):
         manager.stop()
 
 
+def test_pool_mode_is_validated():
+    from kiosk_autoscaler_amd.config import Config, Settings
+    env = {'RESOURCE_NAME': 'x', 'WORKER_BACKEND': 'cpu',
+           'WARM_POOL_MODE': 'devcie'}
+    with pytest.raises(ValueError, match='WARM_POOL_MODE'):
+        gpumgr.build_manager(Settings(Config(environ=env, use_files=False)))
+
+
+@pytest.mark.gpu
+def test_gpu_context_standby_holds_no_hbm_and_serves(resp_server):
+    """MI355X, ``WARM_POOL_MODE=context``: the standby opens its HIP context
+    (and measures free HBM through it) but creates no hardware queue and no
+    RCCL state, so the device's used VRAM does not move while it waits; an
+    assignment then builds the queue, code objects and engine and serves."""
+    import time
+    from kiosk_autoscaler_amd.bench import gpu_util
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict', 'RESOURCE_NAME': 'ctx', 'MAX_PODS': '1',
+           'WORKER_BACKEND': 'hip', 'WARM_POOL': '1',
+           'WARM_POOL_MODE': 'context', 'WORKER_RECYCLE': '0',
+           'FENCE': 'none', 'REDIS_INTERVAL': '0', 'GPU_IDS': '0',
+           'MODEL_DIM': '1024', 'MODEL_HIDDEN': '4096', 'MODEL_LAYERS': '2',
+           'ROWS_PER_KEY': '256'}
+    s = Settings(Config(environ=env, use_files=False))
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    events = EventLog(source='test')
+    events.keep = True
+
+    def until(predicate, timeout):
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            value = predicate()
+            if value:
+                return value
+            time.sleep(0.02)
+        raise AssertionError('timed out')
+
+    def vram():
+        snap = gpu_util.vram_snapshot()
+        return max(snap.values()) if snap else None
+    before = vram()
+    manager = gpumgr.build_manager(s, redis_client=client,
+                                   events=events).start()
+    try:
+        booted = until(lambda: [e for e in events.records
+                                if e['ev'] == 'standby_ready'], 120)
+        assert 'context_done' in (booted[0].get('preinit') or {})
+        standby = list(manager.standbys.values())[0]
+        assert standby.hbm_free, 'free HBM measured through the context'
+        held = vram()
+        if before is not None and held is not None:
+            assert held - before < 64, (before, held)   # MiB: no queue
+        client.hset('predict:x0', mapping={'status': 'new', 'rows': 256})
+        client.lpush('predict', 'predict:x0')
+        manager.patch_namespaced_deployment(
+            'ctx', 'default', {'spec': {'replicas': 1}})
+        until(lambda: client.hget('predict:x0', 'status') == 'done', 120)
+        assigned = [e for e in events.records if e['ev'] == 'worker_assigned']
+        assert assigned and assigned[0]['from_pool']
+        manager.patch_namespaced_deployment(
+            'ctx', 'default', {'spec': {'replicas': 0}})
+        until(lambda: not [w for r in manager.resources.values()
+                           for w in r.workers.values()
+                           if w.state != 'exited'], 60)
+    finally:
+        manager.stop()
+
+
 def test_pool_parks_after_idle_and_refills_on_demand(resp_server):
     """``POOL_IDLE_RELEASE_S``: after that long without demand the standbys
     exit (the node holds no GPU, like the reference at zero replicas); the

@@ -121,3 +121,42 @@ def test_cold_spawn_opens_the_device_on_a_helper_thread(monkeypatch):
     worker_main._join_device_open()
     assert 'no device' in worker_main._DEVICE_OPEN['error']
     worker_main._DEVICE_OPEN.clear()
+
+
+class _FenceAgent(object):
+    def __init__(self):
+        self.calls = []
+
+    def submit(self, message):
+        self.calls.append(('submit', message.get('cmd')))
+
+    def close(self):
+        self.calls.append(('close',))
+        return True
+
+    def abandon(self):
+        self.calls.append(('abandon',))
+
+
+@pytest.mark.parametrize('recycle', [True, False])
+def test_exiting_worker_leaves_the_communicator_to_process_exit(
+        redis_client, recycle):
+    """A drained worker that goes back to the pool releases its fence
+    communicator gracefully; one that exits abandons it (its process exit
+    frees it: a graceful RCCL finalize only kept the GPU alive longer)."""
+    import queue
+    channel = _Channel()
+    channel.commands = queue.Queue()
+    channel.start_reader = lambda: None
+    channel.commands.put({'cmd': 'drain', 'recycle': recycle})
+    env = {'ROWS_PER_KEY': '64', 'MOCK_WORK_MS': '0', 'QUEUES': 'predict',
+           'WARM_START': '1'}
+    cfg = rt.WorkerConfig(env, {'worker_id': 'w-g0-x-2', 'recycle': True})
+    agent = _FenceAgent()
+    run = rt.WorkerRuntime(cfg, lambda c, stage: mlp.CpuMlpEngine(c),
+                           channel, lambda: redis_client,
+                           fence_factory=lambda runtime: agent)
+    assert run.run() == 0
+    assert run.recycle is recycle
+    assert agent.calls == [('close',) if recycle else ('abandon',)]
+    assert 'fence' not in channel.direct      # unhooked either way
