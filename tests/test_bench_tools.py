@@ -307,3 +307,32 @@ def test_bench_tick_inproc_runs():
             if l.startswith('{')]
     assert {r['tally'] for r in rows} == {'reference', 'atomic'}
     assert all(r['mean_ms'] > 0 for r in rows)
+
+
+@pytest.mark.gpu
+def test_gpu_bench_contract(tmp_path):
+    """MI355X: the driver's bench contract end to end at a tiny scale --
+    one JSON line, the timed steps, every key served, the RCCL node
+    communicator, the managed device named, HBM figures in range."""
+    env = dict(os.environ, PYTHONPATH=ROOT, KIOSK_BENCH_OUT=str(tmp_path))
+    proc = subprocess.run(
+        [sys.executable, os.path.join(ROOT, 'bench.py'), '--steps', '2',
+         '--warmup', '1', '--interval', '1', '--on', '1', '--lam-per-gpu',
+         '2', '--service-ms', '100', '--budget-s', '150', '--dim', '1024',
+         '--hidden', '4096', '--layers', '2', '--rows', '256'],
+        env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+        timeout=240)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    lines = [l for l in proc.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, proc.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line['n_gpus'] == 1 and line['steps'] == 2 and 'error' not in line
+    assert line['value'] is not None and line['vs_baseline'] is not None
+    assert line['keys_done'] == line['keys'] > 0
+    assert line['fence_transport'] == 'rccl' and line['fence_max_ranks'] == 1
+    assert line['gpu_bdfs'] and len(line['gpu_bdfs']) == 1
+    assert line['actuation_mean_s'] < 0.5
+    boot = line['standby_pool_boot_hbm_mib']
+    assert boot is None or 0 < boot < 8192, boot
+    assert line['idle_node_hbm_mib'] is None or \
+        line['idle_node_hbm_mib'] < 16384
