@@ -265,7 +265,10 @@ class Services(object):
         value = self.redis.get('kiosk:pool')
         if not value:
             return False
-        booted, _total = (int(v) for v in value.split()[:2])
+        fields = value.split()
+        if len(fields) > 3 and fields[3] == '1':
+            return True     # parked on purpose (POOL_IDLE_RELEASE_S)
+        booted, _total = (int(v) for v in fields[:2])
         return booted >= self.pool
 
     def node_state(self):

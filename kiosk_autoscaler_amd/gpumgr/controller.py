@@ -693,11 +693,13 @@ class GpuManager(object):
         if self.redis is None:
             return
         try:
-            # booted standbys, standbys, node communicator state
-            self.redis.set(POOL_KEY, '%d %d %s' % (
+            # booted standbys, standbys, node communicator state, parked
+            # (POOL_IDLE_RELEASE_S: the pool is empty on purpose)
+            self.redis.set(POOL_KEY, '%d %d %s %d' % (
                 sum(1 for p in self.standbys.values() if p.booted),
                 len(self.standbys),
-                self.node.state if self.node is not None else 'off'))
+                self.node.state if self.node is not None else 'off',
+                int(self.pool_parked)))
         except Exception:  # pylint: disable=broad-except
             pass
 

@@ -165,7 +165,11 @@ def test_bench_cpu_smoke(tmp_path):
     assert pod['ready_delay_s'] == 10.0 and line['reference_pod_start_s'] == 10
     assert line['reference_sim_pod_start_latency_s'] == pytest.approx(
         pod['latency_mean_s'], abs=1e-3)
-    assert pod['latency_mean_s'] >= ref['latency_mean_s'] + 9.9
+    # every cold start waits for its tick and then the whole pod start (the
+    # two runs' cold-start sets differ -- keys landing during a pod start
+    # start no new cycle -- so their means are not offset by exactly D)
+    assert pod['latency_mean_s'] >= 10.0 - 1e-6
+    assert pod['latency_mean_s'] > ref['latency_mean_s'] + 5.0
 
 
 @pytest.mark.slow

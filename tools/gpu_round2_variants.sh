@@ -5,6 +5,7 @@
 #   bash tools/gpu_round2_variants.sh C   -> PyTorch plug-in engine (WORKER_ENGINE)
 #   bash tools/gpu_round2_variants.sh D   -> INTERVAL=0.1 (reference loop, fast cadence)
 #   bash tools/gpu_round2_variants.sh E   -> POOL_IDLE_RELEASE_S=3 (no GPU held when idle)
+#   bash tools/gpu_round2_variants.sh F   -> WARM_POOL_MODE=context (no HBM held)
 set -o pipefail
 OUT=${OUT:-gpurun_out/r2_variants}
 mkdir -p $OUT
@@ -32,6 +33,9 @@ elif [ "$1" = "E" ]; then
   # deep idle: standbys exit after 3 s without demand (no GPU held between
   # bursts), every scale-up is then a cold spawn
   POOL_IDLE_RELEASE_S=3 run pool_idle_release_3s 200 --gpus 1 --steps 10 --warmup 1 --budget-s 180 --cold-cycles 0
+elif [ "$1" = "F" ]; then
+  # standbys with a HIP context and no HBM (WARM_POOL_MODE=context)
+  run context_norecycle 200 --gpus 1 --steps 10 --warmup 1 --budget-s 180 --pool-mode context --no-recycle --cold-cycles 0
 elif [ "$1" = "C" ]; then
   # a user's PyTorch model as the engine (WORKER_ENGINE plug-in): the same
   # standby / recycle / cache path, torch imported by the standby at boot
