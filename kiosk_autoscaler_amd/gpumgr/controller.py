@@ -613,19 +613,8 @@ class GpuManager(object):
                 self._stopping:
             return
         changed = False
-        for index, proc in list(self.standbys.items()):
-            if proc.popen.poll() is not None:
-                proc.pipe.close()
-                del self.standbys[index]
-                self.events.emit('standby_exit', pid=proc.pid, slot=index,
-                                 code=proc.popen.returncode)
-        for proc in list(self.retiring):
-            if proc.popen.poll() is not None:
-                proc.pipe.close()
-                self.retiring.remove(proc)
-                self.events.emit('standby_exit', pid=proc.pid, slot=proc.slot,
-                                 code=proc.popen.returncode, retired=True)
-                changed = True
+        if self._reap_standbys():
+            changed = True
         if self._park_pool():
             changed = True
         if self.pool_parked:
@@ -965,14 +954,27 @@ class GpuManager(object):
                 # drain remaining messages (the READY/exit of a short job)
                 self._on_worker_messages(worker)
                 self._on_exit(resource, worker, code)
+        self._reap_standbys()
+
+    def _reap_standbys(self):
+        """Forget exited standby / retired processes (``standby_exit``
+        closes their standby GPU time in the metrics).  True if a retired
+        process was reaped."""
+        retired = False
         for index, proc in list(self.standbys.items()):
             if proc.popen.poll() is not None:
                 proc.pipe.close()
                 del self.standbys[index]
+                self.events.emit('standby_exit', pid=proc.pid, slot=index,
+                                 code=proc.popen.returncode)
         for proc in list(self.retiring):
             if proc.popen.poll() is not None:
                 proc.pipe.close()
                 self.retiring.remove(proc)
+                self.events.emit('standby_exit', pid=proc.pid, slot=proc.slot,
+                                 code=proc.popen.returncode, retired=True)
+                retired = True
+        return retired
 
     def _on_exit(self, resource, worker, code, recycled=False):
         was_ready = worker.state in (READY, DRAINING) and worker.t_ready

@@ -433,6 +433,8 @@ def test_pool_parks_after_idle_and_refills_on_demand(resp_server):
         until(lambda: not manager.standbys and not manager.retiring)
         assert client.get('kiosk:pool').split()[:2] == ['0', '0']
         assert client.get('kiosk:pool').split()[3] == '1'     # parked
+        # the retired standby's GPU time is closed in the metrics
+        until(lambda: 'standby_exit' in kinds())
         client.hset('predict:k', mapping={'status': 'new'})
         client.lpush('predict', 'predict:k')
         manager.patch_namespaced_deployment('park', 'default',
