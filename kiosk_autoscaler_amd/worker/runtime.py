@@ -94,6 +94,7 @@ class QueueConsumer(object):
         self.queues = list(queues)
         self.poll_block = poll_block
         self._rotate = 0
+        self._sweep = 0
 
     def processing_key(self, queue, slot=0):
         suffix = '' if slot == 0 else '.%d' % slot
@@ -102,12 +103,16 @@ class QueueConsumer(object):
     def pull(self, limit=1, block=True):
         """Return up to ``limit`` ``(queue, item, processing_key)`` tuples.
 
-        Sweeps every queue with non-blocking ``LMOVE`` first; when all are
-        empty, blocks on one queue (rotating) for ``poll_block`` seconds
-        (``BLMOVE`` wakes the instant a key lands on that queue; the bound
-        keeps a drain command from waiting long)."""
+        Sweeps every queue with non-blocking ``LMOVE`` first, starting one
+        queue further on each call (round robin: a busy first queue cannot
+        starve the others of a multi-queue resource); when all are empty,
+        blocks on one queue (rotating) for ``poll_block`` seconds (``BLMOVE``
+        wakes the instant a key lands on that queue; the bound keeps a drain
+        command from waiting long)."""
         taken = []
-        for queue in self.queues:
+        start = self._sweep % len(self.queues)
+        self._sweep += 1
+        for queue in self.queues[start:] + self.queues[:start]:
             while len(taken) < limit:
                 pkey = self.processing_key(queue, len(taken))
                 item = self.redis.lmove(queue, pkey, 'RIGHT', 'LEFT')

@@ -160,3 +160,19 @@ def test_exiting_worker_leaves_the_communicator_to_process_exit(
     assert run.recycle is recycle
     assert agent.calls == [('close',) if recycle else ('abandon',)]
     assert 'fence' not in channel.direct      # unhooked either way
+
+
+def test_multi_queue_pull_is_round_robin(redis_client):
+    """QUEUES=predict,track: a backlog on the first queue does not starve
+    the second (each sweep starts one queue further)."""
+    for i in range(4):
+        redis_client.lpush('predict', 'predict:%d' % i)
+        redis_client.lpush('track', 'track:%d' % i)
+    consumer = rt.QueueConsumer(redis_client, 'w-g0-x-3',
+                                ['predict', 'track'])
+    order = []
+    for _ in range(4):
+        for queue, item, pkey in consumer.pull(limit=1, block=False):
+            order.append(queue)
+            consumer.complete(pkey)
+    assert order == ['predict', 'track', 'predict', 'track']
