@@ -197,7 +197,10 @@ class Services(object):
             'SCALE_POLICY': args.policy,
             'SCALE_DOWN_DELAY': str(args.scale_down_delay),
             'IDLE_INTERVAL': str(args.idle_interval),
-            'GPU_IDS': ','.join(str(i) for i in range(n_gpus)),
+            # BENCH_GPU_IDS (rehearsal only): e.g. '0,0' puts two slots on
+            # the one GPU of a 1-GPU box to run the N=2 launch path there
+            'GPU_IDS': os.environ.get('BENCH_GPU_IDS') or
+            ','.join(str(i) for i in range(n_gpus)),
             'WORKER_BACKEND': args.backend, 'WARM_POOL': str(pool),
             'WARM_POOL_MODE': args.pool_mode,
             'WORKER_RECYCLE': '0' if args.no_recycle else '1',
@@ -537,7 +540,9 @@ def main():
                 os.close(saved)
         use_cuda = torch.cuda.is_available() and args.backend == 'hip'
         if use_cuda:
-            torch.cuda.set_device(local_rank)
+            # modulo: the N>1 launch path can be rehearsed on a box with
+            # fewer devices than ranks (BENCH_GPU_IDS); identity on a node
+            torch.cuda.set_device(local_rank % torch.cuda.device_count())
 
         def barrier():
             if dist is not None:
