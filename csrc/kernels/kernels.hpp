@@ -33,6 +33,10 @@ hipError_t launch_gemm(const uint16_t* A, const uint16_t* B, uint16_t* C,
                        int K, int epilogue, hipStream_t stream);
 bool gemm_shape_ok(int M, int N, int K);
 hipError_t gemm_prepare();  // call once before launching / capturing
+// Code-object loads without a launch (no hardware queue, no HBM beyond the
+// code itself): what a `context` standby pre-pays.
+hipError_t misc_prepare();
+hipError_t warmstart_prepare();
 
 // Kernel variants: 0 = auto (256x256 ring kernel -- the 4-wave one where
 // its 32-bit offsets reach -- when it yields >= 256 tiles, else split-K 256x256 when a workspace is given, else the 256x128

@@ -155,4 +155,12 @@ hipError_t launch_spin(double ms, unsigned int* done, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// Loads this file's code object (first use of any of its kernels does;
+// querying attributes does it without a launch, so no hardware queue).
+hipError_t misc_prepare() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr,
+                              reinterpret_cast<const void*>(&init_bf16_kernel));
+}
+
 }  // namespace kiosk

@@ -103,4 +103,10 @@ hipError_t launch_warmstart(const uint16_t* w, size_t n, uint32_t* record,
   return hipGetLastError();
 }
 
+hipError_t warmstart_prepare() {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(&warmstart_kernel),
+                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                             kGemmRingLdsBytes);
+}
+
 }  // namespace kiosk

@@ -154,6 +154,19 @@ PYBIND11_MODULE(_kiosk_hip, m) {
         return d;
       },
       py::arg("device") = 0);
+  m.def(
+      "preload_modules",
+      [](int device) {
+        std::vector<std::pair<std::string, long long>> stages;
+        {
+          py::gil_scoped_release release;
+          stages = kiosk::preload_modules(device);
+        }
+        py::dict d;
+        for (const auto& kv : stages) d[py::str(kv.first)] = kv.second;
+        return d;
+      },
+      py::arg("device") = 0);
   // (free, total) HBM bytes of the current device: a device-mode standby
   // reports it so KEYS_PER_POD is sized against what is actually free
   m.def("mem_info", [] {

@@ -98,6 +98,20 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   return stages;
 }
 
+std::vector<std::pair<std::string, long long>> preload_modules(int device) {
+  TraceRange range("kiosk.preload");
+  std::vector<std::pair<std::string, long long>> stages;
+  stages.emplace_back("preload_enter", monotonic_ns());
+  check_hip(hipSetDevice(device), "hipSetDevice");
+  check_hip(hipFree(nullptr), "hip context init");
+  stages.emplace_back("preload_context", monotonic_ns());
+  check_hip(gemm_prepare(), "gemm_prepare");
+  check_hip(misc_prepare(), "misc_prepare");
+  check_hip(warmstart_prepare(), "warmstart_prepare");
+  stages.emplace_back("preload_done", monotonic_ns());
+  return stages;
+}
+
 void Engine::stage(const char* name) {
   stages_.emplace_back(name, monotonic_ns());
 }

@@ -21,6 +21,9 @@ long long monotonic_ns();
 // and nothing running; the later Engine ctor then skips ~150 ms of
 // runtime init + code-object loading.  Returns stage timestamps.
 std::vector<std::pair<std::string, long long>> preinit_device(int device);
+// `context` standby: HIP context + every kernel's code object, no launch (so
+// no hardware queue and no HBM beyond the code objects).
+std::vector<std::pair<std::string, long long>> preload_modules(int device);
 
 struct WarmStartResult {
   int blocks = 0;

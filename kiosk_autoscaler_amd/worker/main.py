@@ -268,13 +268,17 @@ def main(argv=None):
     elif pin and pin.get('preinit') == 'context' and backend == 'hip':
         # the HIP context alone: no hardware queue (the first kernel launch
         # creates one, ~0.5 GiB of device-side state) and no RCCL, so this
-        # standby holds no HBM (profiles/r2_hbm_hold/); the assignment pays
-        # the queue, code objects and engine
+        # standby holds no HBM (profiles/r2_hbm_hold/).  Code objects load
+        # without a launch (CONTEXT_PRELOAD=1, default), so the assignment
+        # pays only the queue and the engine
         from ..ops import native
         try:
             t0 = time.monotonic_ns()
-            native.load().mem_info()
+            mod = native.load()
+            mod.mem_info()
             preinit = {'context_open': t0, 'context_done': time.monotonic_ns()}
+            if os.environ.get('CONTEXT_PRELOAD', '1') == '1':
+                preinit.update(mod.preload_modules(0))
         except Exception as err:  # pylint: disable=broad-except
             channel.emit('error', message='preinit failed: %s' % err)
             return 4

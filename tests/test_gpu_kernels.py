@@ -238,6 +238,16 @@ def test_fence_warmup_and_preinit(mod):
     assert list(stages) == ['preinit_enter', 'preinit_context', 'preinit_done']
 
 
+def test_preload_modules_stamps(mod):
+    """The context standby's code-object preload (no launch) reports its
+    stages in order."""
+    stages = mod.preload_modules(0)
+    assert list(stages) == ['preload_enter', 'preload_context',
+                            'preload_done']
+    assert stages['preload_enter'] <= stages['preload_context'] <= \
+        stages['preload_done']
+
+
 @pytest.mark.parametrize('M,N,K', [(256, 256, 32), (300, 512, 96),
                                    (2048, 1024, 4096), (1, 256, 64),
                                    (520, 384, 160), (777, 768, 192),

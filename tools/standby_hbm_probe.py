@@ -47,6 +47,9 @@ def main():
     from kiosk_autoscaler_amd.ops import native
     mod = native.load()
     mark('HIP context (hipMemGetInfo)')
+    stages = mod.preload_modules(0)
+    mark('code objects loaded without a launch (context standby, %.1f ms)'
+         % ((stages['preload_done'] - stages['preload_context']) / 1e6))
     mod.preinit_device(0)
     mark('preinit (code objects, one launch of each kernel)')
     fence = mod.Fence(1, 0, 30.0)
