@@ -268,16 +268,17 @@ def main(argv=None):
     elif pin and pin.get('preinit') == 'context' and backend == 'hip':
         # the HIP context alone: no hardware queue (the first kernel launch
         # creates one, ~0.5 GiB of device-side state) and no RCCL, so this
-        # standby holds no HBM (profiles/r2_hbm_hold/).  Code objects load
-        # without a launch (CONTEXT_PRELOAD=1, default), so the assignment
-        # pays only the queue and the engine
+        # standby holds no HBM (profiles/r2_hbm_hold/).  CONTEXT_PRELOAD=1
+        # (opt-in) also loads the code objects without a launch: measured
+        # +314 MiB of HBM for -3 ms of actuation (profiles/r2_context_preload/),
+        # so by default the assignment pays queue, code objects and engine
         from ..ops import native
         try:
             t0 = time.monotonic_ns()
             mod = native.load()
             mod.mem_info()
             preinit = {'context_open': t0, 'context_done': time.monotonic_ns()}
-            if os.environ.get('CONTEXT_PRELOAD', '1') == '1':
+            if os.environ.get('CONTEXT_PRELOAD', '0') == '1':
                 preinit.update(mod.preload_modules(0))
         except Exception as err:  # pylint: disable=broad-except
             channel.emit('error', message='preinit failed: %s' % err)
