@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <set>
 
 #include "../kernels/kernels.hpp"
@@ -28,6 +29,34 @@ long long monotonic_ns() {
 
 namespace {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// The stream preinit_device warmed up (its first launches paid the queue
+// setup): kept for the next Engine instead of being destroyed, so a fresh
+// standby's first assignment does not pay hipStreamCreate again (~14 ms on
+// MI355X, profiles/r2_worker_final/).  The engine takes ownership.
+std::mutex g_kept_mu;
+hipStream_t g_kept_stream = nullptr;
+int g_kept_device = -1;
+
+hipStream_t take_kept_stream(int device) {
+  std::lock_guard<std::mutex> lock(g_kept_mu);
+  if (g_kept_device != device) return nullptr;
+  hipStream_t s = g_kept_stream;
+  g_kept_stream = nullptr;
+  g_kept_device = -1;
+  return s;
+}
+
+void keep_stream(hipStream_t s, int device) {
+  hipStream_t old = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(g_kept_mu);
+    old = g_kept_stream;
+    g_kept_stream = s;
+    g_kept_device = device;
+  }
+  if (old) hipStreamDestroy(old);
+}
 }  // namespace
 
 std::vector<std::pair<std::string, long long>> preinit_device(int device) {
@@ -38,9 +67,11 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   check_hip(hipFree(nullptr), "hip context init");
   stages.emplace_back("preinit_context", monotonic_ns());
   check_hip(gemm_prepare(), "gemm_prepare");
-  hipStream_t stream = nullptr;
-  check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking),
-            "hipStreamCreate");
+  hipStream_t stream = take_kept_stream(device);
+  if (!stream) {
+    check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking),
+              "hipStreamCreate");
+  }
   // 128x128 operands + bias + output + sums + warm-start record
   const size_t elems = 128 * 128;
   char* scratch = nullptr;
@@ -93,7 +124,7 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
             "preinit warmstart");
   check_hip(hipStreamSynchronize(stream), "preinit sync");
   check_hip(hipFree(scratch), "hipFree(preinit)");
-  check_hip(hipStreamDestroy(stream), "hipStreamDestroy");
+  keep_stream(stream, device);
   stages.emplace_back("preinit_done", monotonic_ns());
   return stages;
 }
@@ -151,8 +182,11 @@ void Engine::init(int device, unsigned long long seed) {
   check_hip(hipDeviceGetAttribute(&cu_count_, hipDeviceAttributeMultiprocessorCount,
                                   device),
             "hipDeviceGetAttribute");
-  check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking),
-            "hipStreamCreate");
+  stream_ = take_kept_stream(device);
+  if (!stream_) {
+    check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking),
+              "hipStreamCreate");
+  }
   check_hip(hipEventCreate(&ev0_), "hipEventCreate");
   check_hip(hipEventCreate(&ev1_), "hipEventCreate");
   check_hip(gemm_prepare(), "gemm_prepare");
