@@ -229,8 +229,11 @@ class Services(object):
             # the node communicator's first generation pays RCCL's one-time
             # init (~2 s; its code-object load slows an engine built
             # meanwhile): let it finish, bounded -- a broken communicator
-            # only costs fences, never the run
-            deadline = time.time() + 30.0
+            # only costs fences, never the run.  A hung first init falls
+            # back to the shm transport within FENCE_FALLBACK_AFTER (2) x
+            # FENCE_INIT_TIMEOUT: wait that long plus the fallback's init
+            init_timeout = float(os.environ.get('FENCE_INIT_TIMEOUT', 12.0))
+            deadline = time.time() + max(30.0, 2 * init_timeout + 8.0)
             while time.time() < deadline and self.node_state() not in (
                     'ready', 'off', None):
                 time.sleep(0.1)

@@ -1,0 +1,24 @@
+// `_kiosk_fence_cpu`: the node-communicator bindings of `_kiosk_hip`
+// (bind_comm.cpp) built for a CPU host against the shared-memory fake HIP +
+// RCCL (fake_hip_rccl.cpp), so the production Fence / RcclNodeTransport /
+// node agent run unchanged in N CPU processes (tests/test_node_fence.py,
+// FENCE=rccl with KIOSK_NATIVE=fake).  Never loaded on a GPU box.
+#include <pybind11/pybind11.h>
+
+#include <stdexcept>
+
+#include "runtime/bind_comm.hpp"
+#include "runtime/fence.hpp"
+
+namespace kiosk {
+// engine.cpp's helper (the fence needs it for its HIP calls)
+void check_hip(hipError_t err, const char* what) {
+  if (err != hipSuccess) throw std::runtime_error(what);
+}
+}  // namespace kiosk
+
+PYBIND11_MODULE(_kiosk_fence_cpu, m) {
+  m.doc() = "kiosk node-communicator bindings over the CPU fake HIP + RCCL";
+  m.attr("arch") = "cpu-fake";
+  kiosk::bind_comm(m);
+}

@@ -1,0 +1,300 @@
+// Host-only, multi-process stand-in for the HIP runtime calls and the RCCL
+// entry points csrc/runtime/fence.cpp uses.  It lets the REAL fence code --
+// Fence, RcclNodeTransport, the node agent -- run unchanged in N CPU
+// processes (tools/build_native.py --fake-hip builds `_kiosk_fence_cpu`
+// against this library; KIOSK_RCCL_LIB points the fence's dlopen at it),
+// and under ASan / UBSan / TSan (tests/native/fence_asan_main.cpp).
+//
+// Semantics kept from RCCL, since they are what fence.cpp must handle:
+// * the communicator is non-blocking: init / shrink / finalize report
+//   ncclInProgress through ncclCommGetAsyncError until every rank joined;
+// * ncclAllReduce only enqueues; the sum lands when the stream is queried
+//   after every rank posted (a ShmComm in a file under FAKE_RCCL_DIR or
+//   /dev/shm carries the values between processes);
+// * a dead peer is NOT detected: a collective waiting on it stays pending
+//   until the caller times out or aborts (ncclCommAbort drops this rank's
+//   queued work, which is what unblocks the real kernel);
+// * ncclCommShrink(NCCL_SHRINK_ABORT) terminates the parent's queued work
+//   and builds a child over the survivors, renumbered in order.
+// Every communicator and stream is a heap object: a second abort, a
+// destroy after an abort, or any use after either is an ASan report.
+//
+// FAKE_RCCL_MODE (read at each call): ok | init_error | init_hang |
+// allreduce_hang | finalize_hang.
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <thread>
+
+#include "runtime/shmcomm.hpp"
+
+#define FAKE_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+std::string mode() {
+  const char* m = std::getenv("FAKE_RCCL_MODE");
+  return m ? m : "ok";
+}
+
+struct FakeComm {
+  std::unique_ptr<kiosk::ShmComm> shm;
+  int polls_left = 3;        // ncclInProgress this many times, then settle
+  bool init_fails = false;
+  bool init_hangs = false;
+  bool finalize_hangs = false;
+  bool finalizing = false;
+};
+
+struct Op {
+  bool copy = true;
+  void* dst = nullptr;
+  const void* src = nullptr;
+  size_t bytes = 0;
+  FakeComm* comm = nullptr;   // all-reduce
+  int count = 0;
+  uint64_t seq = 0;
+  bool posted = false;
+  bool hang = false;
+};
+
+struct FakeStream {
+  std::deque<Op> ops;
+};
+
+std::mutex g_mu;                       // streams, their queues, comm lifetime
+std::set<FakeStream*> g_streams;
+std::atomic<long> g_live_comms{0};
+
+// Runs the stream's queue in order as far as it can (g_mu held).  An
+// all-reduce posts its send buffer when it reaches the front (stream
+// order: after the upload copy) and completes once every rank posted.
+bool progress(FakeStream* s) {
+  while (!s->ops.empty()) {
+    Op& op = s->ops.front();
+    if (op.copy) {
+      std::memcpy(op.dst, op.src, op.bytes);
+      s->ops.pop_front();
+      continue;
+    }
+    if (op.hang) return false;
+    if (!op.posted) {
+      op.seq = op.comm->shm->post(static_cast<const long long*>(op.src),
+                                  op.count);
+      op.posted = true;
+    }
+    if (!op.comm->shm->try_complete(op.seq, static_cast<long long*>(op.dst),
+                                    op.count)) {
+      return false;
+    }
+    s->ops.pop_front();
+  }
+  return true;
+}
+
+void drop_ops_of(FakeComm* c) {
+  for (FakeStream* s : g_streams) {
+    for (auto it = s->ops.begin(); it != s->ops.end();) {
+      it = (!it->copy && it->comm == c) ? s->ops.erase(it) : std::next(it);
+    }
+  }
+}
+
+FakeComm* new_comm(std::unique_ptr<kiosk::ShmComm> shm) {
+  auto* c = new FakeComm();
+  c->shm = std::move(shm);
+  const std::string m = mode();
+  c->init_fails = m == "init_error";
+  c->init_hangs = m == "init_hang";
+  c->finalize_hangs = m == "finalize_hang";
+  g_live_comms++;
+  return c;
+}
+
+}  // namespace
+
+FAKE_API long fake_rccl_live_comms() { return g_live_comms.load(); }
+
+// ---- HIP (host memory stands in for HBM) ---------------------------------
+FAKE_API hipError_t hipStreamCreateWithFlags(hipStream_t* stream,
+                                             unsigned int) {
+  auto* s = new FakeStream();
+  std::lock_guard<std::mutex> lock(g_mu);
+  g_streams.insert(s);
+  *stream = reinterpret_cast<hipStream_t>(s);
+  return hipSuccess;
+}
+FAKE_API hipError_t hipStreamDestroy(hipStream_t stream) {
+  auto* s = reinterpret_cast<FakeStream*>(stream);
+  std::lock_guard<std::mutex> lock(g_mu);
+  g_streams.erase(s);
+  delete s;
+  return hipSuccess;
+}
+FAKE_API hipError_t hipMalloc(void** ptr, size_t size) {
+  *ptr = std::calloc(1, size);
+  return *ptr ? hipSuccess : hipErrorOutOfMemory;
+}
+FAKE_API hipError_t hipFree(void* ptr) {
+  std::free(ptr);
+  return hipSuccess;
+}
+FAKE_API hipError_t hipHostMalloc(void** ptr, size_t size, unsigned int) {
+  *ptr = std::calloc(1, size);
+  return *ptr ? hipSuccess : hipErrorOutOfMemory;
+}
+FAKE_API hipError_t hipHostFree(void* ptr) {
+  std::free(ptr);
+  return hipSuccess;
+}
+FAKE_API hipError_t hipMemcpyAsync(void* dst, const void* src, size_t bytes,
+                                   hipMemcpyKind, hipStream_t stream) {
+  auto* s = reinterpret_cast<FakeStream*>(stream);
+  std::lock_guard<std::mutex> lock(g_mu);
+  if (s->ops.empty()) {
+    std::memcpy(dst, src, bytes);
+  } else {
+    Op op;
+    op.dst = dst;
+    op.src = src;
+    op.bytes = bytes;
+    s->ops.push_back(op);
+  }
+  return hipSuccess;
+}
+FAKE_API hipError_t hipStreamQuery(hipStream_t stream) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  return progress(reinterpret_cast<FakeStream*>(stream)) ? hipSuccess
+                                                         : hipErrorNotReady;
+}
+FAKE_API hipError_t hipStreamSynchronize(hipStream_t stream) {
+  const auto deadline =
+      std::chrono::steady_clock::now() + std::chrono::seconds(10);
+  while (true) {
+    {
+      std::lock_guard<std::mutex> lock(g_mu);
+      if (progress(reinterpret_cast<FakeStream*>(stream))) return hipSuccess;
+    }
+    if (std::chrono::steady_clock::now() > deadline) return hipErrorUnknown;
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+}
+FAKE_API const char* hipGetErrorString(hipError_t) {
+  return "fake hip error";
+}
+
+// ---- RCCL -------------------------------------------------------------------
+FAKE_API ncclResult_t ncclGetVersion(int* version) {
+  *version = 22707;
+  return ncclSuccess;
+}
+FAKE_API ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
+  const char* dir = std::getenv("FAKE_RCCL_DIR");
+  const std::string path = kiosk::shm_unique_id(dir ? dir : "");
+  std::memset(id->internal, 0, sizeof(id->internal));
+  std::memcpy(id->internal, path.data(), path.size());
+  return ncclSuccess;
+}
+FAKE_API ncclResult_t ncclCommInitRankConfig(ncclComm_t* comm, int nranks,
+                                             ncclUniqueId id, int rank,
+                                             ncclConfig_t*) {
+  std::string path(id.internal, strnlen(id.internal, sizeof(id.internal)));
+  std::unique_ptr<kiosk::ShmComm> shm;
+  try {
+    // like RCCL: no dead-peer detection, a 1 h bound the caller never hits
+    shm.reset(new kiosk::ShmComm(path, nranks, rank, 3600.0, false));
+  } catch (const std::exception&) {
+    return ncclInvalidArgument;
+  }
+  std::lock_guard<std::mutex> lock(g_mu);
+  *comm = reinterpret_cast<ncclComm_t>(new_comm(std::move(shm)));
+  return ncclInProgress;
+}
+FAKE_API ncclResult_t ncclCommGetAsyncError(ncclComm_t comm,
+                                            ncclResult_t* state) {
+  auto* c = reinterpret_cast<FakeComm*>(comm);
+  std::lock_guard<std::mutex> lock(g_mu);
+  if (c->finalizing) {
+    *state = c->finalize_hangs ? ncclInProgress : ncclSuccess;
+  } else if (c->init_hangs) {
+    *state = ncclInProgress;
+  } else if (c->polls_left > 0) {
+    c->polls_left--;
+    *state = ncclInProgress;
+  } else if (c->init_fails) {
+    *state = ncclInvalidUsage;
+  } else {
+    *state = c->shm->poll_ready() ? ncclSuccess : ncclInProgress;
+  }
+  return ncclSuccess;
+}
+FAKE_API ncclResult_t ncclCommAbort(ncclComm_t comm) {
+  auto* c = reinterpret_cast<FakeComm*>(comm);
+  std::lock_guard<std::mutex> lock(g_mu);
+  drop_ops_of(c);                  // what unblocks the real kernel
+  g_live_comms--;
+  delete c;                        // a second abort is a double free
+  return ncclSuccess;
+}
+FAKE_API ncclResult_t ncclCommFinalize(ncclComm_t comm) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  reinterpret_cast<FakeComm*>(comm)->finalizing = true;
+  return ncclInProgress;
+}
+FAKE_API ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+  auto* c = reinterpret_cast<FakeComm*>(comm);
+  std::lock_guard<std::mutex> lock(g_mu);
+  drop_ops_of(c);
+  g_live_comms--;
+  delete c;
+  return ncclSuccess;
+}
+FAKE_API ncclResult_t ncclAllReduce(const void* send, void* recv,
+                                    size_t count, ncclDataType_t,
+                                    ncclRedOp_t, ncclComm_t comm,
+                                    hipStream_t stream) {
+  auto* c = reinterpret_cast<FakeComm*>(comm);
+  auto* s = reinterpret_cast<FakeStream*>(stream);
+  if (count < 1 || count > static_cast<size_t>(kiosk::kShmMaxValues)) {
+    return ncclInvalidArgument;
+  }
+  Op op;
+  op.copy = false;
+  op.comm = c;
+  op.src = send;
+  op.dst = recv;
+  op.count = static_cast<int>(count);
+  op.hang = mode() == "allreduce_hang";   // a peer that never joins
+  std::lock_guard<std::mutex> lock(g_mu);
+  c->polls_left = 0;
+  s->ops.push_back(op);
+  progress(s);
+  return ncclSuccess;
+}
+FAKE_API const char* ncclGetErrorString(ncclResult_t) {
+  return "fake rccl error";
+}
+FAKE_API ncclResult_t ncclCommShrink(ncclComm_t comm, int* excluded,
+                                     int count, ncclComm_t* out,
+                                     ncclConfig_t*, int flags) {
+  auto* c = reinterpret_cast<FakeComm*>(comm);
+  std::lock_guard<std::mutex> lock(g_mu);
+  if (flags & NCCL_SHRINK_ABORT) drop_ops_of(c);
+  std::unique_ptr<kiosk::ShmComm> child;
+  try {
+    child = c->shm->shrink(std::vector<int>(excluded, excluded + count));
+  } catch (const std::exception&) {
+    return ncclInvalidArgument;
+  }
+  *out = reinterpret_cast<ncclComm_t>(new_comm(std::move(child)));
+  return ncclInProgress;
+}

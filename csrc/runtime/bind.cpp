@@ -9,7 +9,7 @@
 
 #include "../kernels/kernels.hpp"
 #include "engine.hpp"
-#include "fence.hpp"
+#include "bind_comm.hpp"
 #include "trace.hpp"
 
 namespace py = pybind11;
@@ -240,62 +240,5 @@ PYBIND11_MODULE(_kiosk_hip, m) {
       .def_property_readonly("layers", &kiosk::Engine::layers)
       .def_property_readonly("max_rows", &kiosk::Engine::max_rows);
 
-  // every RCCL entry point releases the GIL: the first call initialises
-  // the library (seconds) and must not stall the worker's serving thread
-  m.def("rccl_library", &kiosk::rccl_library,
-        py::call_guard<py::gil_scoped_release>());
-  m.def("rccl_version", &kiosk::rccl_version,
-        py::call_guard<py::gil_scoped_release>());
-  m.def("fence_can_shrink", &kiosk::rccl_can_shrink,
-        py::call_guard<py::gil_scoped_release>());
-  m.def("fence_warmup", &kiosk::rccl_warmup, py::arg("timeout") = 60.0,
-        py::call_guard<py::gil_scoped_release>());
-  m.def("fence_unique_id", [] {
-    std::string id;
-    {
-      py::gil_scoped_release release;
-      id = kiosk::rccl_unique_id();
-    }
-    return py::bytes(id);
-  });
-
-  py::class_<kiosk::Fence>(m, "Fence")
-      .def(py::init([](py::bytes uid, int nranks, int rank, double timeout) {
-             std::string id = uid;
-             py::gil_scoped_release release;
-             return new kiosk::Fence(id, nranks, rank, timeout);
-           }),
-           py::arg("unique_id"), py::arg("nranks"), py::arg("rank"),
-           py::arg("timeout") = 60.0)
-      .def(py::init<int, int, double>(), py::arg("nranks"), py::arg("rank"),
-           py::arg("timeout") = 60.0)
-      .def(
-          "connect",
-          [](kiosk::Fence& f, py::bytes uid) {
-            std::string id = uid;
-            py::gil_scoped_release release;
-            f.connect(id);
-          },
-          py::arg("unique_id"))
-      .def("allreduce", &kiosk::Fence::allreduce,
-           py::call_guard<py::gil_scoped_release>())
-      .def(
-          "shrink",
-          [](kiosk::Fence& f, const std::vector<int>& excluded,
-             double timeout) -> kiosk::Fence& {
-            py::gil_scoped_release release;
-            f.shrink(excluded, timeout);
-            return f;
-          },
-          py::arg("excluded"), py::arg("timeout") = 60.0,
-          py::return_value_policy::reference)
-      .def("destroy", &kiosk::Fence::destroy,
-           py::call_guard<py::gil_scoped_release>())
-      .def("abort", &kiosk::Fence::abort,
-           py::call_guard<py::gil_scoped_release>())
-      .def("request_abort", &kiosk::Fence::request_abort)
-      .def_property_readonly("abort_requested",
-                             &kiosk::Fence::abort_requested)
-      .def_property_readonly("nranks", &kiosk::Fence::nranks)
-      .def_property_readonly("rank", &kiosk::Fence::rank);
+  kiosk::bind_comm(m);
 }

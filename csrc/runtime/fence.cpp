@@ -225,6 +225,10 @@ std::pair<std::vector<long long>, double> Fence::allreduce(
   if (values.empty() || values.size() > 64) {
     throw std::invalid_argument("fence vector must have 1..64 entries");
   }
+  if (stalled_) {
+    throw std::runtime_error("fence has an interrupted all-reduce queued: "
+                             "shrink or destroy it");
+  }
   TraceRange range("kiosk.fence.allreduce");
   const size_t n = values.size();
   const double t0 = now_s();
@@ -247,6 +251,12 @@ std::pair<std::vector<long long>, double> Fence::allreduce(
   // bounded wait: a dead peer must not hang the worker forever
   const double deadline = now_s() + timeout_s_;
   while (hipStreamQuery(stream_) == hipErrorNotReady) {
+    if (interrupt_requested_.exchange(false, std::memory_order_relaxed)) {
+      // the manager shrinks the dead rank out: keep the communicator (the
+      // kernel still waits on the peer; NCCL_SHRINK_ABORT ends it)
+      stalled_ = true;
+      throw FenceInterrupted("fence all-reduce interrupted for a shrink");
+    }
     const bool late = now_s() > deadline;
     if (late || abort_requested_.load(std::memory_order_relaxed)) {
       abort();   // unblocks the kernel waiting on a dead peer
@@ -260,31 +270,70 @@ std::pair<std::vector<long long>, double> Fence::allreduce(
   return {out, (now_s() - t0) * 1e6};
 }
 
-void Fence::shrink(const std::vector<int>& excluded, double timeout_s) {
+void Fence::shrink(const std::vector<int>& excluded, double timeout_s,
+                   bool abort_parent) {
   if (!comm_) throw std::runtime_error("fence communicator is closed");
   if (!rccl().CommShrink) {
     throw std::runtime_error("this RCCL has no ncclCommShrink");
   }
+  std::vector<bool> gone(nranks_, false);
+  for (int r : excluded) {
+    if (r < 0 || r >= nranks_ || gone[r] || r == rank_) {
+      throw std::invalid_argument("shrink: bad excluded rank list");
+    }
+    gone[r] = true;
+  }
   TraceRange range("kiosk.fence.shrink");
   std::vector<int> ex(excluded);
   ncclComm_t next = nullptr;
-  check_nccl(rccl().CommShrink(static_cast<ncclComm_t>(comm_), ex.data(),
-                               static_cast<int>(ex.size()), &next, nullptr,
-                               NCCL_SHRINK_DEFAULT),
-             "ncclCommShrink");
+  const int flags = abort_parent ? NCCL_SHRINK_ABORT : NCCL_SHRINK_DEFAULT;
+  ncclResult_t res = rccl().CommShrink(static_cast<ncclComm_t>(comm_),
+                                       ex.data(), static_cast<int>(ex.size()),
+                                       &next, nullptr, flags);
+  if (res != ncclSuccess && res != ncclInProgress) {
+    // the parent is unusable either way: a half-failed shrink is never
+    // retried on it
+    abort();
+    throw std::runtime_error(std::string("ncclCommShrink: ") +
+                             rccl().GetErrorString(res));
+  }
   try {
     wait_ready(next, timeout_s, "ncclCommShrink");
+    if (stalled_) {
+      // the interrupted all-reduce was terminated by NCCL_SHRINK_ABORT:
+      // its stream work (kernel + download) must drain before the stream
+      // and buffers serve the child
+      const double deadline = now_s() + timeout_s;
+      while (hipStreamQuery(stream_) == hipErrorNotReady) {
+        if (now_s() > deadline) {
+          throw std::runtime_error("interrupted all-reduce did not drain "
+                                   "after ncclCommShrink");
+        }
+        std::this_thread::yield();
+      }
+    }
   } catch (...) {
-    rccl().CommAbort(next);   // the child is ours to abort; the parent stays
+    if (next) rccl().CommAbort(next);   // the child is ours to abort
+    abort();
     throw;
   }
   void* old = comm_;
   comm_ = next;
+  stalled_ = false;
+  interrupt_requested_.store(false, std::memory_order_relaxed);
   int below = 0;
   for (int r : excluded) below += (r < rank_);
   rank_ -= below;
   nranks_ -= static_cast<int>(excluded.size());
-  rccl().CommDestroy(static_cast<ncclComm_t>(old));
+  if (abort_parent) {
+    rccl().CommAbort(static_cast<ncclComm_t>(old));   // a peer is gone
+  } else {
+    rccl().CommDestroy(static_cast<ncclComm_t>(old));
+  }
+}
+
+void Fence::request_interrupt() {
+  interrupt_requested_.store(true, std::memory_order_relaxed);
 }
 
 void Fence::abort() {
@@ -300,7 +349,7 @@ void Fence::request_abort() {
 void Fence::destroy() {
   if (comm_) {
     bool finalized = false;
-    if (!abort_requested_.load(std::memory_order_relaxed)) {
+    if (!abort_requested_.load(std::memory_order_relaxed) && !stalled_) {
       rccl().CommFinalize(static_cast<ncclComm_t>(comm_));
       try {
         wait_ready(comm_, timeout_s_, "ncclCommFinalize");

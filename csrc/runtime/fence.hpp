@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <stdexcept>
 #include <string>
 #include <utility>
 #include <vector>
@@ -24,6 +25,12 @@ std::string rccl_unique_id();     // 128 raw bytes
 // loads the library, builds and destroys a 1-rank communicator on the
 // current device (RCCL device code + proxy setup), returns elapsed ms.
 double rccl_warmup(double timeout_s);
+
+// A blocked collective given up on request_interrupt(): the communicator
+// is NOT aborted, so the survivors can still shrink it (a peer died).
+struct FenceInterrupted : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
 
 class Fence {
  public:
@@ -42,7 +49,11 @@ class Fence {
   std::pair<std::vector<long long>, double> allreduce(
       const std::vector<long long>& values);
   // Collective over the surviving ranks: drop `excluded` (old rank ids).
-  void shrink(const std::vector<int>& excluded, double timeout_s);
+  // `abort_parent` (NCCL_SHRINK_ABORT): first terminate what the parent
+  // still runs -- an all-reduce blocked on the dead peer -- then shrink;
+  // the parent is aborted, not finalized (a peer is gone).
+  void shrink(const std::vector<int>& excluded, double timeout_s,
+              bool abort_parent = true);
   void destroy();
   // Owner thread only: aborts the communicator once (idempotent).
   void abort();
@@ -50,6 +61,10 @@ class Fence {
   // thread abort and throw at its next poll (a peer died mid-collective).
   void request_abort();
   bool abort_requested() const { return abort_requested_.load(); }
+  // Any thread: a blocked allreduce of the owner thread throws
+  // FenceInterrupted at its next poll and leaves the communicator intact
+  // for shrink() (the manager is excluding a dead rank).
+  void request_interrupt();
   int nranks() const { return nranks_; }
   int rank() const { return rank_; }
 
@@ -65,6 +80,8 @@ class Fence {
   int rank_ = 0;
   double timeout_s_ = 60.0;
   std::atomic<bool> abort_requested_{false};
+  std::atomic<bool> interrupt_requested_{false};
+  bool stalled_ = false;        // an interrupted op may still be queued
 };
 
 }  // namespace kiosk

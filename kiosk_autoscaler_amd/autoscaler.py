@@ -25,6 +25,7 @@ import timeit
 from . import policy as policies
 from .gpumgr.resources import ActuatorError
 from .utils.events import NULL as NULL_EVENTS
+from .utils.keys import worker_of
 
 
 class Autoscaler(object):
@@ -95,7 +96,7 @@ class Autoscaler(object):
             else:
                 waiting, keys = counted
             running = len(keys)
-            busy.update(k.split(':', 1)[1].split('.', 1)[0] for k in keys)
+            busy.update(worker_of(k) for k in keys)
             self.in_progress[queue] = running
             self.redis_keys[queue] = waiting + running
         self.busy_workers = busy

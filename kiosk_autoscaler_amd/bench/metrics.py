@@ -254,6 +254,16 @@ def fence_stats(events):
     rank reported (``n`` of ``fence_rank``)."""
     done = [e for e in events if e.get('ev') == 'fence_done']
     ranks = [e for e in events if e.get('ev') == 'fence_rank' and e.get('ok')]
+    ready = [e for e in events if e.get('ev') == 'node_comm_ready']
+    inits = [e for e in ready if e.get('mode', 'init') != 'shrink']
+    shrinks = [e for e in ready if e.get('mode') == 'shrink']
+    # communicator set-up time per rank count (the first 8-rank RCCL init
+    # on a fresh node is the number to watch)
+    init_by_n = collections.defaultdict(list)
+    for e in inits:
+        init_by_n[str(int(e.get('n') or 0))].append(
+            float(e.get('init_ms') or 0.0))
+    fallbacks = [e for e in events if e.get('ev') == 'node_comm_fallback']
     return {
         'fences': len(done),
         'fence_max_ranks': max([int(e.get('n') or 0) for e in ranks + done]
@@ -262,16 +272,23 @@ def fence_stats(events):
                                default=0),
         'fence_modes': dict(collections.Counter(
             str(e.get('mode')) for e in done)),
-        'node_comm_generations': sum(1 for e in events
-                                     if e.get('ev') == 'node_comm_ready'),
+        'node_comm_generations': len(inits),
+        # a slot's process died or retired: the survivors shrank it out
+        'node_comm_shrinks': len(shrinks),
+        'node_comm_shrink_ms_max': max([float(e.get('init_ms') or 0.0)
+                                        for e in shrinks], default=None),
         # RCCL could not build the node communicator: the fallback
         # transport (FENCE_FALLBACK) fenced instead
-        'node_comm_fallbacks': sum(1 for e in events
-                                   if e.get('ev') == 'node_comm_fallback'),
+        'node_comm_fallbacks': len(fallbacks),
+        'node_comm_fallback_transport': (fallbacks[-1].get('transport')
+                                         if fallbacks else None),
         'node_comm_init_ms_max': max([float(e.get('init_ms') or 0.0)
-                                      for e in events
-                                      if e.get('ev') == 'node_comm_ready'],
-                                     default=None),
+                                      for e in inits], default=None),
+        'node_comm_init_ms_by_ranks': {
+            n: {'count': len(v), 'max': max(v), 'mean': sum(v) / len(v)}
+            for n, v in sorted(init_by_n.items())},
+        'node_comm_transports': sorted({str(e.get('transport'))
+                                        for e in inits}),
         'fence_transport': sorted({str(e.get('transport')) for e in done}),
         'fence_wall_ms_mean': _mean([1e3 * e['wall_s'] for e in done
                                      if e.get('wall_s') is not None]),

@@ -156,7 +156,9 @@ EXTRA_DEFAULTS = (
     # node then holds no GPU, the next scale-up is a cold spawn (~0.13 s)
     ('POOL_IDLE_RELEASE_S', float, 0.0),
     ('WARM_START', bool, True),             # run the N1 warm-start kernel
-    ('FENCE', str, 'auto'),                 # auto | rccl | store | none
+    # auto (rccl with device standbys, shm otherwise; store on CPU) | rccl
+    # | shm | store | gloo | none
+    ('FENCE', str, 'auto'),
     ('MODEL_DIM', int, 4096),
     ('MODEL_HIDDEN', int, 16384),
     ('MODEL_LAYERS', int, 4),
@@ -175,9 +177,13 @@ EXTRA_DEFAULTS = (
     ('FENCE_COMM', str, 'node'),            # node (persistent) | epoch
     # node communicator transport after FENCE_FALLBACK_AFTER consecutive
     # failed generations ('' = keep retrying RCCL): membership keeps being
-    # fenced, over Redis, if RCCL cannot build the node communicator
-    ('FENCE_FALLBACK', str, 'store'),
+    # fenced, over host shared memory, if RCCL cannot build the node
+    # communicator
+    ('FENCE_FALLBACK', str, 'shm'),
     ('FENCE_FALLBACK_AFTER', int, 2),
+    # s a node-communicator generation (or shrink) may take to connect; a
+    # hung first init falls back within FENCE_FALLBACK_AFTER x this
+    ('FENCE_INIT_TIMEOUT', float, 12.0),
     ('METRICS_PORT', int, 0),               # Prometheus /metrics port (0 = off)
     ('METRICS_ADDR', str, '0.0.0.0'),
     ('DEBUG', bool, True),

@@ -52,6 +52,7 @@ def worker_env(settings, keys_per_pod=None):
         'MODEL_LAYERS': settings.MODEL_LAYERS,
         'ROWS_PER_KEY': settings.ROWS_PER_KEY,
         'WARM_START': int(settings.WARM_START), 'FENCE': settings.FENCE,
+        'FENCE_INIT_TIMEOUT': settings.FENCE_INIT_TIMEOUT,
         'RESOURCE_NAMESPACE': settings.RESOURCE_NAMESPACE,
         'RESOURCE_NAME': settings.RESOURCE_NAME,
     }
@@ -66,7 +67,9 @@ def worker_env(settings, keys_per_pod=None):
                         'KIOSK_RCCL_LIB', 'WORKER_EVENTS', 'KIOSK_FAULTS',
                         'KIOSK_ROCTX', 'WORKER_KEEP_ENGINE',
                         'WORKER_IMPORT_TORCH', 'WORKER_ENGINE',
-                        'WORKER_PYTHON_SITE'):
+                        'WORKER_PYTHON_SITE', 'KIOSK_SHM_DIR',
+                        'KIOSK_NATIVE', 'FAKE_RCCL_DIR', 'FAKE_RCCL_MODE',
+                        'ENGINE_IDLE_RELEASE_S', 'WORKER_MAX_RECYCLES'):
         if passthrough in os.environ:
             env[passthrough] = os.environ[passthrough]
     return env
@@ -121,7 +124,8 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
                          fence_comm=settings.FENCE_COMM,
                          pool_idle_release_s=settings.POOL_IDLE_RELEASE_S,
                          fence_fallback=settings.FENCE_FALLBACK,
-                         fence_fallback_after=settings.FENCE_FALLBACK_AFTER)
+                         fence_fallback_after=settings.FENCE_FALLBACK_AFTER,
+                         fence_init_timeout=settings.FENCE_INIT_TIMEOUT)
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

@@ -50,6 +50,7 @@ import threading
 import time
 
 from ..utils.events import NULL as NULL_EVENTS
+from ..utils.keys import worker_of
 from .nodecomm import NODE_EVENTS, NodeComm
 from .resources import ActuatorError, ResourceList, ResourceView, \
     desired_from_body
@@ -215,6 +216,8 @@ class Resource(object):
         self.fence_fresh = False     # force re-init after a failed epoch
         self.fence_failures = 0      # consecutive failed/abandoned epochs
         self.fence_retry_at = 0.0    # monotonic s; backoff after failures
+        self.fence_error = None      # detail of the last failed epoch
+        self.fence_enabled = True
 
     @property
     def key(self):
@@ -227,6 +230,19 @@ class Resource(object):
     def ready(self):
         return [w for w in self.workers.values() if w.state == READY]
 
+    def fenced_ready(self):
+        """READY workers that are in the last agreed (fenced) membership."""
+        return [wid for wid in self.fenced_members
+                if wid in self.workers and self.workers[wid].state == READY]
+
+    def fence_status(self):
+        ready = sorted(w.id for w in self.ready())
+        return {'epoch': self.fenced_epoch,
+                'in_sync': sorted(self.fenced_members) == ready,
+                'pending': bool(self.fence_wanted or self.fence_inflight),
+                'failures': self.fence_failures,
+                'last_error': self.fence_error}
+
     def view(self):
         live = self.live()
         return ResourceView.build(
@@ -234,7 +250,9 @@ class Resource(object):
             ready=len([w for w in live if w.state == READY]),
             active=len(live), succeeded=self.succeeded, failed=self.failed,
             generation=self.generation, epoch=self.fenced_epoch,
-            gpus=[w.slot.index for w in live])
+            gpus=[w.slot.index for w in live],
+            fenced=len(self.fenced_ready()) if self.fence_enabled else None,
+            fence=self.fence_status() if self.fence_enabled else None)
 
 
 class GpuManager(object):
@@ -266,7 +284,8 @@ class GpuManager(object):
                  fence_timeout=60.0, max_restart_backoff=10.0,
                  worker_timeout=0.0, start_timeout=0.0, recycle=True,
                  fence_comm='node', pool_idle_release_s=0.0,
-                 fence_fallback='store', fence_fallback_after=2):
+                 fence_fallback='shm', fence_fallback_after=2,
+                 fence_init_timeout=12.0, fence_transport=None):
         self.slots = list(slots)
         self.redis = redis_client
         self.pool_size = max(0, int(pool_size))
@@ -302,18 +321,27 @@ class GpuManager(object):
         self.history = []   # exited workers, for accounting
         # persistent node-wide communicator: needs one long-lived process
         # per slot (a standby for every GPU, recycled workers); otherwise
-        # every epoch bootstraps its own communicator (round-1 mode)
+        # every epoch bootstraps its own communicator (round-1 mode).  In
+        # every pool mode: standbys that hold no GPU (context / import, and
+        # the cold spawns after a deep-idle park) run it over the native
+        # shared-memory transport instead of RCCL, which would need a
+        # hardware queue and ~0.8 GiB of HBM per GPU (profiles/r2_hbm_hold)
         self.fence_comm = fence_comm
         self.node = None
-        # (an import-mode standby must not create a HIP context: a
-        # communicator in it would, so that mode fences per epoch)
         if (fence and fence_comm == 'node' and self.recycle and
                 pool_template is not None and self.slots and
-                self.pool_size >= len(self.slots) and
-                (pool_mode == 'device' or pool_template.backend == 'cpu')):
+                self.pool_size >= len(self.slots)):
+            transport = fence_transport
+            if transport is None and pool_template.backend == 'hip' and \
+                    pool_mode != 'device':
+                transport = 'shm'
             self.node = NodeComm(self, fence_timeout=min(fence_timeout, 30.0),
+                                 init_timeout=fence_init_timeout,
                                  fallback=fence_fallback,
-                                 fallback_after=fence_fallback_after)
+                                 fallback_after=fence_fallback_after,
+                                 transport=transport)
+        for resource in self.resources.values():
+            resource.fence_enabled = bool(fence)
 
     # ------------------------------------------------------------------
     # API (the kubernetes AppsV1Api / BatchV1Api analogs)
@@ -331,6 +359,7 @@ class GpuManager(object):
             key = (kind, namespace, name)
             if key not in self.resources:
                 resource = Resource(kind, namespace, name, template)
+                resource.fence_enabled = bool(self.fence_enabled)
                 self.resources[key] = resource
                 if restore:
                     self._restore(resource)
@@ -400,7 +429,7 @@ class GpuManager(object):
             try:
                 for key in list(self.redis.scan_iter(match=pattern,
                                                      count=1000)):
-                    wid = key.split(':', 1)[1].split('.', 1)[0]
+                    wid = worker_of(key)
                     if wid in live or not ours.match(wid):
                         continue
                     while self.redis.rpoplpush(key, queue) is not None:
@@ -460,6 +489,8 @@ class GpuManager(object):
                 'standbys': [{'pid': p.pid, 'booted': p.booted,
                               'slot': index}
                              for index, p in self.standbys.items()],
+                'node_comm': (self.node.summary() if self.node is not None
+                              else None),
                 'resources': [dict(r.view().to_dict(), workers=[
                     w.summary() for w in r.workers.values()])
                     for r in self.resources.values()],
@@ -702,6 +733,12 @@ class GpuManager(object):
     def _on_standby_message(self, proc, message):
         if self.node is not None and message.get('ev') in NODE_EVENTS:
             self.node.on_message(proc, message)
+            return
+        if message.get('ev') == 'engine_released':
+            proc.hbm_free = message.get('hbm_free')
+            self.events.emit('engine_released', pid=proc.pid, slot=proc.slot,
+                             released_bytes=message.get('released_bytes'),
+                             hbm_free=proc.hbm_free)
             return
         if message.get('ev') == 'standby':
             proc.booted = True
@@ -1102,12 +1139,16 @@ class GpuManager(object):
     def _maybe_node_fence(self, resource):
         """One 72-B all-reduce over the persistent communicator; waits
         (fence_wanted stays set) while a generation is being built or
-        another resource's epoch is in flight."""
+        shrunk, another resource's epoch is in flight, or a member runs on a
+        process that is not a rank yet (a replacement awaiting the regrow)."""
         if not resource.fence_wanted or not self.node.ready or \
                 self.node.inflight is not None:
             return
         members = sorted((w.id for w in resource.ready()),
                          key=lambda wid: resource.workers[wid].slot.index)
+        if not self.node.can_fence([resource.workers[wid].proc
+                                    for wid in members]):
+            return
         resource.fence_wanted = False
         if members == resource.fenced_members:
             return
@@ -1138,13 +1179,24 @@ class GpuManager(object):
         if not message.get('ok', False):
             logger.warning('Fence epoch %d failed: %s', epoch,
                            message.get('detail'))
+            resource.fence_error = str(message.get('detail'))[:300]
             self._fence_failed(resource)
             return
         self._fence_completed(resource, epoch, members, started, message)
 
+    def _fence_failed_node(self, resource, message):
+        """A node fence failed (not a shrink's interrupt): visible in the
+        resource's ``status.fence`` until an epoch succeeds."""
+        resource.fence_failures += 1
+        resource.fence_error = str(message.get('detail'))[:300]
+        self.events.emit('fence_failed', name=resource.name,
+                         detail=resource.fence_error,
+                         failures=resource.fence_failures)
+
     def _fence_completed(self, resource, epoch, members, started, message):
         resource.fence_fresh = False
         resource.fence_failures = 0
+        resource.fence_error = None
         resource.fenced_epoch = epoch
         resource.fenced_members = members
         self.events.emit('fence_done', epoch=epoch, members=members,

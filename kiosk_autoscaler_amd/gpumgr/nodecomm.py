@@ -2,13 +2,20 @@
 
 See :mod:`kiosk_autoscaler_amd.parallel.nodefence` for the protocol.  The
 manager owns the communicator's *generation*: it starts one when every
-managed GPU slot has a live process running a node agent (pool boot), relays
-rank 0's communicator id to the other ranks, and breaks it -- ``comm_abort``
-to the survivors, a fresh generation once the slot is repopulated -- only
-when a slot's process dies or is retired.  Scale events never touch it: a
-membership change is one ``fence`` all-reduce over the existing
+managed GPU slot has a live process running a node agent (pool boot) and
+relays rank 0's communicator id to the other ranks.  Scale events never
+touch it: a membership change is one ``fence`` all-reduce over the existing
 communicator, serialized node-wide (every rank takes part in every
 collective, in the same order).
+
+When a slot's process dies or retires (a forced recycle exit, a deep-idle
+park) the survivors **shrink** it out (``comm_shrink``: RCCL's
+``ncclCommShrink`` with ``NCCL_SHRINK_ABORT``, which also ends an
+all-reduce blocked on the dead peer) and keep fencing, with that slot's bit
+at 0, while the replacement boots.  RCCL has no grow, so once every slot
+has a live process again the next full generation is built (``regrow``).
+Only a failed shrink, a transport that cannot shrink (gloo) or losing every
+rank drops the generation outright (``comm_abort``).
 
 This replaces the per-event ``ncclCommInitRank`` that the round-1 design
 paid at every READY-set change (the actuation the fence gates is the
@@ -19,14 +26,24 @@ import time
 
 logger = logging.getLogger('NodeComm')
 
-NONE, INIT, READY = 'none', 'init', 'ready'
+NONE, INIT, READY, SHRINK = 'none', 'init', 'ready', 'shrink'
 # worker -> manager messages of the node agent (parallel.nodefence)
 NODE_EVENTS = ('comm_uid', 'comm_ready', 'fenced', 'node_agent')
 
 
 class NodeComm(object):
-    def __init__(self, manager, init_timeout=120.0, fence_timeout=30.0,
-                 fallback='store', fallback_after=2):
+    """Args:
+        transport: what every ``comm_init`` asks the ranks for (``None``:
+            each agent's own default, ``FENCE``); the manager picks ``shm``
+            for pool modes whose standbys hold no GPU.
+        init_timeout: ``FENCE_INIT_TIMEOUT`` -- a generation (or a shrink)
+            not connected by then fails; after ``fallback_after`` failed
+            generations in a row the ``fallback`` transport takes over.
+    """
+
+    def __init__(self, manager, init_timeout=12.0, fence_timeout=30.0,
+                 fallback='shm', fallback_after=2, transport=None,
+                 shrink=True):
         self.m = manager
         # after ``fallback_after`` consecutive failed generations the next
         # ones use the ``fallback`` transport (every rank switches in its
@@ -34,25 +51,51 @@ class NodeComm(object):
         # node communicator; the JSON/metrics name the transport in use
         self.fallback = fallback or None
         self.fallback_after = max(1, int(fallback_after))
-        self.transport_override = None
+        self.transport_override = transport or None
+        self.shrink_enabled = bool(shrink)
         self.init_timeout = float(init_timeout)
         self.fence_timeout = float(fence_timeout)
         self.gen = 0
+        self.sub = 0             # shrinks applied to this generation
         self.state = NONE
         self.members = []        # [(slot index, _Process)] in rank order
         self.ready_ranks = {}
         self.t_start = 0.0
-        self.failures = 0
+        self.failures = 0        # consecutive failed generations
+        self.failed_total = 0
         self.retry_at = 0.0
         self.seq = 0             # node-wide fence sequence number
         self.inflight = None     # dict: resource, epoch, seq, members, t
         self.generations = 0     # communicators built (for tests/metrics)
+        self.shrinks = 0         # successful shrinks (for tests/metrics)
         self.transport = None
+        self.can_shrink = False
+        self.fallback_used = None
+        self.last_error = None   # why the last generation / shrink failed
 
     # ------------------------------------------------------------------
     @property
     def ready(self):
         return self.state == READY
+
+    @property
+    def full(self):
+        """The communicator spans every managed slot (not shrunk)."""
+        return self.ready and len(self.members) == len(self.m.slots)
+
+    def member_procs(self):
+        return set(id(proc) for _, proc in self.members)
+
+    def summary(self):
+        """What ``status()`` reports about the node communicator."""
+        return {'state': self.state, 'gen': self.gen, 'sub': self.sub,
+                'ranks': len(self.members),
+                'slots': [index for index, _ in self.members],
+                'transport': self.transport or self.transport_override,
+                'fallback': self.fallback_used, 'failures': self.failures,
+                'failed_total': self.failed_total,
+                'generations': self.generations, 'shrinks': self.shrinks,
+                'last_error': self.last_error}
 
     def _bound(self):
         """slot index -> the process currently serving that slot."""
@@ -66,9 +109,12 @@ class NodeComm(object):
         return bound
 
     @staticmethod
-    def _usable(proc):
+    def _alive(proc):
+        return not proc.eof and proc.popen.poll() is None
+
+    def _usable(self, proc):
         return (proc is not None and getattr(proc, 'node_ok', False) and
-                not proc.eof and proc.popen.poll() is None)
+                self._alive(proc))
 
     def candidates(self):
         """``[(slot, proc)]`` over every managed slot, or ``None`` while one
@@ -86,16 +132,28 @@ class NodeComm(object):
     def step(self, now=None):
         """Called from every manager poll (under the manager lock)."""
         now = time.monotonic() if now is None else now
-        if self.state in (INIT, READY):
+        if self.state in (INIT, READY, SHRINK):
             bound = self._bound()
-            lost = [index for index, proc in self.members
+            lost = [rank for rank, (index, proc) in enumerate(self.members)
                     if not self._usable(proc) or proc in self.m.retiring or
                     bound.get(index) is not proc]
             if lost:
-                self.break_('slot(s) %s lost their process' % lost)
-            elif self.state == INIT and now - self.t_start > self.init_timeout:
-                self.break_('generation %d init timed out' % self.gen,
-                            failed=True)
+                if (self.state == READY and self.shrink_enabled and
+                        self.can_shrink and len(lost) < len(self.members)):
+                    self._shrink(lost, now)
+                else:
+                    self.break_('slot(s) %s lost their process' % [
+                        self.members[r][0] for r in lost])
+            elif self.state in (INIT, SHRINK) and \
+                    now - self.t_start > self.init_timeout:
+                self.break_('generation %d.%d %s timed out after %.1f s' % (
+                    self.gen, self.sub, self.state, self.init_timeout),
+                    failed=True)
+        if self.state == READY and self.inflight is None and \
+                len(self.members) < len(self.m.slots):
+            members = self.candidates()
+            if members:
+                self._regrow(members, now)
         if self.state == NONE and now >= self.retry_at:
             members = self.candidates()
             if members:
@@ -109,6 +167,7 @@ class NodeComm(object):
 
     def _start(self, members, now):
         self.gen += 1
+        self.sub = 0
         self.state = INIT
         self.members = list(members)
         self.ready_ranks = {}
@@ -127,13 +186,58 @@ class NodeComm(object):
         logger.info('Node communicator generation %d: %d ranks.', self.gen, n)
         self.m._publish_pool()
 
+    def _cancel_inflight(self, procs):
+        """A fence whose communicator changes under it is re-run after."""
+        if self.inflight is None:
+            return
+        seq = self.inflight['seq']
+        for proc in procs:
+            if self._alive(proc):
+                proc.pipe.send({'cmd': 'fence_abort', 'seq': seq})
+        self.inflight['resource'].fence_wanted = True
+        self.inflight = None
+
+    def _shrink(self, lost, now):
+        """Survivors drop the ranks in ``lost`` and keep fencing."""
+        gone = [self.members[r] for r in lost]
+        survivors = [m for r, m in enumerate(self.members) if r not in lost]
+        self._cancel_inflight([proc for _, proc in survivors])
+        for _, proc in gone:
+            if self._alive(proc):     # a retiring process drops its rank
+                proc.pipe.send({'cmd': 'comm_abort', 'gen': self.gen})
+        self.sub += 1
+        for _, proc in survivors:
+            proc.pipe.send({'cmd': 'comm_shrink', 'gen': self.gen,
+                            'sub': self.sub, 'excluded': list(lost)})
+        self.members = survivors
+        self.state = SHRINK
+        self.ready_ranks = {}
+        self.t_start = now
+        self.m.events.emit('node_comm_shrink', gen=self.gen, sub=self.sub,
+                           excluded_slots=[index for index, _ in gone],
+                           n=len(survivors), transport=self.transport)
+        logger.warning('Node communicator generation %d: slot(s) %s lost; '
+                       'shrinking to %d ranks.', self.gen,
+                       [index for index, _ in gone], len(survivors))
+        self.m._publish_pool()
+
+    def _regrow(self, members, now):
+        """Every slot has a live process again: replace the shrunk
+        communicator by a full generation (RCCL has no grow)."""
+        for _, proc in self.members:
+            if self._alive(proc):
+                proc.pipe.send({'cmd': 'comm_abort', 'gen': self.gen})
+        self.m.events.emit('node_comm_regrow', gen=self.gen, sub=self.sub,
+                           n=len(members))
+        self._start(members, now)
+
     def break_(self, reason, failed=False):
         """Drop the current generation (survivors abort; a fence in flight
         is re-run on the next one)."""
         if self.state == NONE:
             return
         for _, proc in self.members:
-            if not proc.eof and proc.popen.poll() is None:
+            if self._alive(proc):
                 proc.pipe.send({'cmd': 'comm_abort', 'gen': self.gen})
         if self.inflight is not None:
             self.inflight['resource'].fence_wanted = True
@@ -142,16 +246,20 @@ class NodeComm(object):
         self.members = []
         now = time.monotonic()
         if failed:
+            self.last_error = reason
             self.failures += 1
+            self.failed_total += 1
             self.retry_at = now + min(30.0, 0.25 * 2 ** min(self.failures - 1,
                                                              8))
-            if (self.fallback and self.transport_override is None and
+            if (self.fallback and self.transport_override != self.fallback
+                    and self.fallback_used is None and
                     self.failures >= self.fallback_after):
                 self.transport_override = self.fallback
+                self.fallback_used = self.fallback
                 self.retry_at = now
                 self.m.events.emit('node_comm_fallback', gen=self.gen,
                                    transport=self.fallback,
-                                   failures=self.failures)
+                                   failures=self.failures, reason=reason)
                 logger.warning('Node communicator: %d failed generations, '
                                'falling back to the %s transport.',
                                self.failures, self.fallback)
@@ -176,25 +284,39 @@ class NodeComm(object):
                     other.pipe.send({'cmd': 'comm_uid', 'gen': gen,
                                      'uid': message.get('uid')})
         elif kind == 'comm_ready':
-            if self.state != INIT or gen != self.gen:
+            sub = int(message.get('sub') or 0)
+            if self.state not in (INIT, SHRINK) or gen != self.gen or \
+                    sub != self.sub:
                 return
             if not message.get('ok'):
-                self.break_('rank %s failed to connect: %s' % (
-                    message.get('rank'), message.get('detail')), failed=True)
+                what = 'shrink' if self.state == SHRINK else 'connect'
+                # a failed shrink is not a failed generation: the next full
+                # one starts once the lost slot has a process again
+                self.break_('rank %s failed to %s: %s' % (
+                    message.get('rank'), what, message.get('detail')),
+                    failed=self.state == INIT)
                 return
             self.ready_ranks[message.get('rank')] = message
             if len(self.ready_ranks) == len(self.members):
+                shrunk = self.state == SHRINK
                 self.state = READY
-                self.failures = 0
-                self.generations += 1
-                self.transport = message.get('transport')
                 init_ms = max(float(r.get('init_ms') or 0.0)
                               for r in self.ready_ranks.values())
+                self.transport = message.get('transport')
+                self.can_shrink = all(r.get('can_shrink')
+                                      for r in self.ready_ranks.values())
+                if shrunk:
+                    self.shrinks += 1
+                else:
+                    self.failures = 0
+                    self.generations += 1
                 self.m.events.emit('node_comm_ready', gen=self.gen,
-                                   n=len(self.members), init_ms=init_ms,
-                                   transport=self.transport)
-                logger.info('Node communicator generation %d ready (%d ranks,'
-                            ' %.0f ms).', self.gen, len(self.members), init_ms)
+                                   sub=self.sub, n=len(self.members),
+                                   init_ms=init_ms, transport=self.transport,
+                                   mode='shrink' if shrunk else 'init')
+                logger.info('Node communicator generation %d.%d ready (%d '
+                            'ranks, %s, %.0f ms).', self.gen, self.sub,
+                            len(self.members), self.transport, init_ms)
                 self.m._publish_pool()
         elif kind == 'fenced':
             inflight = self.inflight
@@ -203,9 +325,12 @@ class NodeComm(object):
             self.inflight = None
             resource = inflight['resource']
             if not message.get('ok'):
+                resource.fence_wanted = True
+                if message.get('interrupted'):
+                    return          # a peer died: the shrink re-runs it
                 logger.warning('Node fence seq %s failed: %s',
                                inflight['seq'], message.get('detail'))
-                resource.fence_wanted = True
+                self.m._fence_failed_node(resource, message)
                 self.break_('fence failed on rank %s' % message.get('rank'),
                             failed=True)
                 return
@@ -214,14 +339,20 @@ class NodeComm(object):
                                     message)
 
     # ------------------------------------------------------------------
+    def can_fence(self, procs):
+        """Every process in ``procs`` is a rank of the current communicator
+        (a worker on a replacement process waits for the regrow)."""
+        ranks = self.member_procs()
+        return all(id(proc) in ranks for proc in procs)
+
     def fence(self, resource, members):
         """Start one membership epoch of ``resource`` (caller checked
-        ``ready`` and that nothing is in flight)."""
+        ``ready``, ``can_fence`` and that nothing is in flight)."""
         self.seq += 1
         resource.epoch += 1
         slots = [resource.workers[wid].slot.index for wid in members]
         message = {'cmd': 'fence', 'epoch': resource.epoch, 'seq': self.seq,
-                   'gen': self.gen, 'slots': slots,
+                   'gen': self.gen, 'sub': self.sub, 'slots': slots,
                    'width': len(self.m.slots),
                    'group': '%s/%s' % (resource.namespace, resource.name)}
         for _, proc in self.members:
@@ -230,4 +361,5 @@ class NodeComm(object):
                          'seq': self.seq, 'members': list(members),
                          't': time.monotonic()}
         self.m.events.emit('fence_start', epoch=resource.epoch,
-                           members=members, seq=self.seq, gen=self.gen)
+                           members=members, seq=self.seq, gen=self.gen,
+                           sub=self.sub)

@@ -7,8 +7,14 @@ n}}`` / ``{'spec': {'parallelism': n}}`` (``autoscaler.py:230-237``).  The GPU
 manager exposes the same shape so the reconcile core keeps its logic:
 
 * ``spec.replicas`` / ``spec.parallelism`` = declared worker count;
-* ``status.available_replicas`` / ``status.ready_replicas`` = workers that
-  published READY (weights in HBM + warm-start kernel done);
+* ``status.ready_replicas`` = workers that published READY (weights in HBM
+  + warm-start kernel done);
+* ``status.available_replicas`` = READY workers in the last *fenced*
+  membership (the set every GPU's process agreed on over the node
+  communicator) -- what the reference's observer reads with
+  ``only_running`` (``autoscaler.py:176-179``).  It lags READY by one fence
+  (~1 ms) and stays behind while fencing fails; ``status.fence`` says why.
+  Without fencing it equals ``ready_replicas``;
 * ``status.active`` / ``status.succeeded`` / ``status.failed`` for jobs.
 """
 
@@ -58,19 +64,23 @@ class ResourceView(_Bag):
 
     @classmethod
     def build(cls, kind, namespace, name, declared, ready, active, succeeded=0,
-              failed=0, generation=0, epoch=0, gpus=()):
+              failed=0, generation=0, epoch=0, gpus=(), fenced=None,
+              fence=None):
         metadata = Metadata(name=name, namespace=namespace,
                             generation=generation)
+        available = ready if fenced is None else fenced
         if kind == 'deployment':
             spec = Spec(replicas=declared)
-            status = Status(replicas=active, available_replicas=ready,
-                            ready_replicas=ready, restarts=failed,
-                            fenced_epoch=epoch, gpus=list(gpus))
+            status = Status(replicas=active, available_replicas=available,
+                            ready_replicas=ready, fenced_replicas=available,
+                            restarts=failed, fenced_epoch=epoch,
+                            gpus=list(gpus), fence=dict(fence or {}))
         else:
             spec = Spec(parallelism=declared, completions=None)
             status = Status(active=active, ready=ready, succeeded=succeeded,
-                            failed=failed, fenced_epoch=epoch,
-                            gpus=list(gpus))
+                            failed=failed, fenced_replicas=available,
+                            fenced_epoch=epoch, gpus=list(gpus),
+                            fence=dict(fence or {}))
         return cls(kind=kind, metadata=metadata, spec=spec, status=status)
 
     def to_dict(self):

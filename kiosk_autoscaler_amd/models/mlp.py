@@ -78,6 +78,16 @@ class CpuMlpEngine(object):
         self.forward(8, 1, 0)
         return {'backend': 'cpu', 'cus_touched': 0}
 
+    def hbm_bytes(self):
+        """What the HIP engine of this config would hold in HBM (weights +
+        activations of its row capacity): the mock standby's
+        ``MOCK_HBM_FREE_BYTES`` accounting uses it."""
+        from ..utils import hbm
+        cfg = self.cfg
+        rows = max(cfg.rows * cfg.batch, 256)
+        return hbm.model_bytes(cfg.dim, cfg.hidden, cfg.layers) + \
+            hbm.per_key_bytes(rows, cfg.dim, cfg.hidden)
+
     def forward(self, rows, passes, seed):
         import numpy as np
         t0 = time.perf_counter()
@@ -141,6 +151,14 @@ class HipMlpEngine(object):
         info['pass_ms'] = self.pass_ms[self.cfg.rows]
         info['reused'] = self.reused
         return info
+
+    def hbm_bytes(self):
+        """Device bytes this engine holds (arena: weights + activations,
+        plus the split-K workspace)."""
+        if self.engine is None:
+            return 0
+        info = self.engine.info()
+        return int(info.get('arena_bytes', 0) + info.get('workspace_bytes', 0))
 
     def measure(self, rows, passes=2):
         out = self.engine.forward(int(rows), passes, 0)

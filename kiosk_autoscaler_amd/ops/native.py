@@ -14,6 +14,12 @@ RCCL is *not* a link-time dependency: the fence code ``dlopen``s a full RCCL
 
 There is no silent fallback: on a machine with a GPU a missing or stale
 extension raises :class:`NativeUnavailable` with the build command.
+
+``KIOSK_NATIVE=fake`` (CPU tests only) loads ``build/fake/_kiosk_fence_cpu``
+instead: the same node-communicator bindings (RCCL ``Fence``, ``ShmComm``)
+compiled for the host against the shared-memory fake HIP + RCCL
+(``tools/build_native.py --fake-hip``), so the production fence path runs in
+N CPU processes.  It has no kernels and no engine.
 """
 import glob
 import importlib
@@ -30,8 +36,31 @@ class NativeUnavailable(ImportError):
     pass
 
 
+ROOT = os.path.dirname(os.path.dirname(HERE))
+FAKE_DIR = os.path.join(ROOT, 'build', 'fake')
+
+
 def extension_candidates():
     return sorted(glob.glob(os.path.join(HERE, '_kiosk_hip*.so')))
+
+
+def fake_requested():
+    return os.environ.get('KIOSK_NATIVE', '') == 'fake'
+
+
+def _load_fake():
+    paths = sorted(glob.glob(os.path.join(FAKE_DIR, '_kiosk_fence_cpu*.so')))
+    if not paths:
+        raise NativeUnavailable('KIOSK_NATIVE=fake but build/fake is not '
+                                'built; run `python tools/build_native.py '
+                                '--fake-hip`')
+    # the fence dlopen()s RCCL: point it at the fake (already mapped as the
+    # module's dependency, so both resolve to one library)
+    os.environ.setdefault('KIOSK_RCCL_LIB', os.path.join(
+        FAKE_DIR, 'libkiosk_fake_hip_rccl.so'))
+    if FAKE_DIR not in sys.path:
+        sys.path.insert(0, FAKE_DIR)
+    return importlib.import_module('_kiosk_fence_cpu')
 
 
 def load(torch_first=True):
@@ -40,6 +69,9 @@ def load(torch_first=True):
     import torch (the worker)."""
     global _MOD
     if _MOD is not None:
+        return _MOD
+    if fake_requested():
+        _MOD = _load_fake()
         return _MOD
     if not extension_candidates():
         raise NativeUnavailable('native module _kiosk_hip is not built; '
@@ -66,5 +98,6 @@ def available():
 
 
 def loaded_path():
-    mod = sys.modules.get('kiosk_autoscaler_amd.ops._kiosk_hip')
+    mod = sys.modules.get('kiosk_autoscaler_amd.ops._kiosk_hip') or \
+        sys.modules.get('_kiosk_fence_cpu')
     return getattr(mod, '__file__', None)

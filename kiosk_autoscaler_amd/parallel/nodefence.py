@@ -17,14 +17,22 @@ membership change is fenced by the 72-byte all-reduce alone:
   ``{epoch, bit(own slot in slots)}`` to the int64[1 + 8] sum; standbys and
   other resources' workers contribute zeros.  The result must equal
   ``{epoch * nranks, membership mask}``; rank 0 acknowledges (``fenced``).
-* ``comm_abort {gen}`` -- a peer died: any blocked collective is aborted
-  (``Fence::request_abort`` is safe from the reader thread) and the
-  communicator is dropped; the next generation replaces it.
+* ``comm_shrink {gen, sub, excluded}`` -- a slot's process died or retired:
+  the survivors drop its rank (``ncclCommShrink`` with
+  ``NCCL_SHRINK_ABORT``: an all-reduce blocked on the dead peer is first
+  *interrupted* -- ``Fence::request_interrupt`` from the reader thread, the
+  communicator is kept -- then terminated by the shrink) and keep fencing
+  with that slot's bit at 0 while its replacement boots; the manager starts
+  the next full generation once every slot has a live process again.
+* ``comm_abort {gen}`` -- the generation is dropped: any blocked collective
+  is aborted (``Fence::request_abort`` is safe from the reader thread).
 
 Transports: :class:`RcclNodeTransport` (production, RCCL over xGMI through
-``_kiosk_hip.Fence``), :class:`GlooNodeTransport` (CPU test fake, one
-persistent gloo group per generation) and :class:`StoreNodeTransport`
-(Redis lists; mock CPU workers).
+``_kiosk_hip.Fence``), :class:`ShmNodeTransport` (production when the
+standbys hold no GPU, and the default fallback: a native host shared-memory
+all-reduce, ``_kiosk_hip.ShmComm``), :class:`GlooNodeTransport` (CPU test
+fake, one persistent gloo group per generation, cannot shrink) and
+:class:`StoreNodeTransport` (Redis lists; mock CPU workers).
 """
 import json
 import logging
@@ -39,7 +47,8 @@ from .fence import MIN_SLOTS, FenceError
 
 logger = logging.getLogger('NodeFence')
 
-NODE_COMMANDS = ('comm_init', 'comm_uid', 'comm_abort', 'fence', 'fence_abort')
+NODE_COMMANDS = ('comm_init', 'comm_uid', 'comm_shrink', 'comm_abort', 'fence',
+                 'fence_abort')
 NODE_EVENTS = ('comm_uid', 'comm_ready', 'fenced', 'node_agent')
 STORE_KEY = 'kiosk:nodefence:{uid}:{epoch}'
 
@@ -62,6 +71,15 @@ def node_expected(epoch, nranks, member_slots, width):
 
 def node_width(slot_count):
     return max(MIN_SLOTS, int(slot_count))
+
+
+class FenceInterrupted(FenceError):
+    """A collective given up because the manager is shrinking a rank out:
+    the communicator is still usable for the shrink (not dropped)."""
+
+
+def _survivor_rank(rank, excluded):
+    return rank - sum(1 for r in excluded if int(r) < rank)
 
 
 # ---------------------------------------------------------------------------
@@ -91,9 +109,34 @@ class RcclNodeTransport(object):
             self.comm.request_abort()
         self.comm.connect(bytes.fromhex(uid))
 
+    @property
+    def can_shrink(self):
+        try:
+            return bool(self.native.fence_can_shrink())
+        except Exception:  # pylint: disable=broad-except
+            return False
+
     def allreduce(self, epoch, vec):
-        result, us = self.comm.allreduce(list(vec))
+        interrupted = getattr(self.native, 'FenceInterrupted', None)
+        try:
+            result, us = self.comm.allreduce(list(vec))
+        except Exception as err:
+            if interrupted is not None and isinstance(err, interrupted):
+                raise FenceInterrupted(str(err))
+            raise
         return list(result), {'allreduce_us': us}
+
+    def request_interrupt(self):
+        comm = self.comm
+        if comm is not None:
+            comm.request_interrupt()
+
+    def shrink(self, excluded, timeout=None):
+        """Survivors only: ``ncclCommShrink(NCCL_SHRINK_ABORT)``."""
+        if self.comm is None:
+            raise FenceError('no communicator to shrink')
+        self.comm.shrink([int(r) for r in excluded],
+                         self.timeout if timeout is None else timeout, True)
 
     def request_abort(self):
         comm = self.comm
@@ -107,6 +150,75 @@ class RcclNodeTransport(object):
                 comm.destroy()   # aborts instead when an abort was requested
             except Exception:  # pylint: disable=broad-except
                 pass
+
+
+class ShmNodeTransport(object):
+    """Native host shared-memory all-reduce (``_kiosk_hip.ShmComm``): the
+    node communicator of the pool modes whose standbys hold no GPU
+    (``context`` / ``import`` / deep idle) -- an RCCL communicator would
+    need a hardware queue and ~0.8 GiB of HBM per GPU to agree on 9
+    integers -- and the fallback when RCCL cannot build one.  Notices a dead
+    peer by itself (its pid), which RCCL does not."""
+
+    name = 'shm'
+    can_shrink = True
+
+    def __init__(self, timeout=30.0, native=None, shm_dir=''):
+        if native is None:
+            from ..ops import native as native_ops
+            native = native_ops.load(torch_first=False)
+        self.native = native
+        self.timeout = float(timeout)
+        self.shm_dir = shm_dir or os.environ.get('KIOSK_SHM_DIR', '')
+        self.comm = None
+        self._interrupt = False
+
+    def make_uid(self, gen):
+        return self.native.shm_unique_id(self.shm_dir)
+
+    def connect(self, gen, rank, nranks, uid, should_abort=None):
+        self._interrupt = False
+        self.comm = self.native.ShmComm(uid, nranks, rank, self.timeout)
+        if should_abort is not None and should_abort():
+            self.comm.request_abort()
+        self.comm.wait_ready()
+
+    def allreduce(self, epoch, vec):
+        try:
+            result, us = self.comm.allreduce(list(vec))
+        except RuntimeError as err:
+            text = str(err)
+            # a peer that died / left, or the manager's interrupt: the
+            # communicator itself is fine, the survivors shrink it
+            if self._interrupt or 'died' in text or 'left' in text:
+                raise FenceInterrupted(text)
+            raise
+        return list(result), {'allreduce_us': us}
+
+    def request_interrupt(self):
+        self._interrupt = True
+        comm = self.comm
+        if comm is not None:
+            comm.request_abort()   # per object: the shrunk child is fresh
+
+    def shrink(self, excluded, timeout=None):
+        if self.comm is None:
+            raise FenceError('no communicator to shrink')
+        child = self.comm.shrink([int(r) for r in excluded])
+        self.comm.close()
+        self.comm = child
+        self._interrupt = False
+        child.wait_ready()
+
+    def request_abort(self):
+        comm = self.comm
+        if comm is not None:
+            comm.request_abort()
+
+    def close(self):
+        comm, self.comm = self.comm, None
+        if comm is not None:
+            comm.close()
 
 
 class GlooNodeTransport(object):
@@ -142,8 +254,16 @@ class GlooNodeTransport(object):
         return tensor.tolist(), {'allreduce_us': (time.perf_counter() - t0)
                                  * 1e6}
 
+    can_shrink = False
+
     def request_abort(self):
         self._aborted = True   # gloo cannot be interrupted: its timeout ends it
+
+    def request_interrupt(self):
+        pass
+
+    def shrink(self, excluded, timeout=None):
+        raise FenceError('a gloo group cannot shrink')
 
     def close(self):
         self.pg = None
@@ -161,6 +281,10 @@ class StoreNodeTransport(object):
         self.nranks = 0
         self.rank = 0
         self._aborted = False
+        self._interrupt = False
+        self._shrinks = 0
+
+    can_shrink = True
 
     @property
     def redis(self):
@@ -178,6 +302,8 @@ class StoreNodeTransport(object):
     def connect(self, gen, rank, nranks, uid, should_abort=None):
         self.uid, self.rank, self.nranks = uid, rank, nranks
         self._aborted = bool(should_abort and should_abort())
+        self._interrupt = False
+        self._shrinks = 0
 
     def allreduce(self, epoch, vec):
         key = STORE_KEY.format(uid=self.uid, epoch=epoch)
@@ -190,6 +316,8 @@ class StoreNodeTransport(object):
             entries = self.redis.lrange(key, 0, -1)
             if len(set(json.loads(e)[0] for e in entries)) >= self.nranks:
                 break
+            if self._interrupt:
+                raise FenceInterrupted('store all-reduce interrupted')
             if self._aborted:
                 raise FenceError('communicator aborted')
             if time.monotonic() > deadline:
@@ -206,6 +334,18 @@ class StoreNodeTransport(object):
             total = [a + b for a, b in zip(total, values)]
         return total, {'allreduce_us': (time.perf_counter() - t0) * 1e6}
 
+    def request_interrupt(self):
+        self._interrupt = True
+
+    def shrink(self, excluded, timeout=None):
+        if self.uid is None:
+            raise FenceError('no communicator to shrink')
+        self._shrinks += 1
+        self.uid = '%s.s%d' % (self.uid.split('.s')[0], self._shrinks)
+        self.rank = _survivor_rank(self.rank, excluded)
+        self.nranks -= len(excluded)
+        self._interrupt = False
+
     def request_abort(self):
         self._aborted = True
 
@@ -213,11 +353,23 @@ class StoreNodeTransport(object):
         self.uid = None
 
 
-def choose_node_transport(kind, backend, timeout=60.0):
+def init_timeout(default=12.0):
+    """``FENCE_INIT_TIMEOUT``: seconds a node-communicator generation may
+    take to connect (and an all-reduce to complete) before it is failed."""
+    try:
+        return float(os.environ.get('FENCE_INIT_TIMEOUT', default))
+    except ValueError:
+        return default
+
+
+def choose_node_transport(kind, backend, timeout=None):
+    timeout = init_timeout() if timeout is None else float(timeout)
     if kind in ('auto', ''):
         kind = 'rccl' if backend == 'hip' else 'store'
     if kind == 'rccl':
         return RcclNodeTransport(timeout)
+    if kind == 'shm':
+        return ShmNodeTransport(timeout)
     if kind == 'gloo':
         return GlooNodeTransport(min(timeout, 30.0))
     if kind == 'store':
@@ -237,7 +389,7 @@ class NodeFenceAgent(object):
     kernel is not queued behind a whole key of GEMMs."""
 
     def __init__(self, slot, transport, channel=None, events=None,
-                 uid_timeout=60.0, transport_factory=None):
+                 uid_timeout=None, transport_factory=None):
         self.slot = int(slot)
         self.transport = transport
         # kind -> transport, for a manager-requested switch (the fallback
@@ -246,10 +398,17 @@ class NodeFenceAgent(object):
             lambda kind: choose_node_transport(kind, 'hip'))
         self.channel = channel
         self.events = events
-        self.uid_timeout = float(uid_timeout)
+        self.uid_timeout = float(init_timeout() if uid_timeout is None
+                                 else uid_timeout)
         self.gen = 0          # generation of the connected communicator
+        self.sub = 0          # shrinks applied to it
         self.rank = None
         self.nranks = 0
+        # group -> (seq, epoch, mask): the last membership this rank agreed
+        # on per resource (its own all-reduce result; the worker gates its
+        # queue pulls on it, worker/runtime.py)
+        self.agreed = {}
+        self.agreed_cv = threading.Condition()
         self._uids = {}
         self._uid_cv = threading.Condition()
         self._abort_gen = 0   # highest generation the manager aborted
@@ -273,6 +432,13 @@ class NodeFenceAgent(object):
         if cmd == 'fence_abort':
             self._aborted_epochs.add(message.get('seq'))
             return
+        if cmd == 'comm_shrink':
+            # a collective blocked on the dead peer gives up now -- without
+            # dropping the communicator the shrink needs
+            if int(message.get('gen', 0)) == self.gen:
+                interrupt = getattr(self.transport, 'request_interrupt', None)
+                if interrupt is not None:
+                    interrupt()
         if cmd == 'comm_abort':
             gen = int(message.get('gen', 0))
             with self._uid_cv:
@@ -331,25 +497,58 @@ class NodeFenceAgent(object):
             self._emit('comm_ready', gen=gen, rank=rank, ok=False,
                        detail=str(err), transport=self.transport.name)
             return
-        self.gen, self.rank, self.nranks = gen, rank, nranks
+        self.gen, self.rank, self.nranks, self.sub = gen, rank, nranks, 0
         init_ms = (time.perf_counter() - t0) * 1e3
         self._emit('comm_ready', gen=gen, rank=rank, ok=True, init_ms=init_ms,
-                   transport=self.transport.name, n=nranks)
+                   transport=self.transport.name, n=nranks, sub=0,
+                   mode='init',
+                   can_shrink=bool(getattr(self.transport, 'can_shrink',
+                                           False)))
+
+    def _comm_shrink(self, message):
+        gen, sub = int(message['gen']), int(message['sub'])
+        excluded = [int(r) for r in message.get('excluded', [])]
+        t0 = time.perf_counter()
+        try:
+            if self.rank is None or gen != self.gen or sub != self.sub + 1:
+                raise FenceError('cannot shrink generation %d.%d (have %s)'
+                                 % (gen, sub, '%d.%d' % (self.gen, self.sub)
+                                    if self.rank is not None else 'none'))
+            if self.rank in excluded:
+                raise FenceError('rank %d is excluded' % self.rank)
+            self.transport.shrink(excluded)
+        except Exception as err:  # pylint: disable=broad-except
+            logger.warning('shrink of generation %d failed: %s', gen, err)
+            rank = self.rank
+            self._drop()
+            self._emit('comm_ready', gen=gen, sub=sub, rank=rank, ok=False,
+                       detail=str(err), transport=self.transport.name,
+                       mode='shrink')
+            return
+        self.rank = _survivor_rank(self.rank, excluded)
+        self.nranks -= len(excluded)
+        self.sub = sub
+        self._emit('comm_ready', gen=gen, sub=sub, rank=self.rank, ok=True,
+                   init_ms=(time.perf_counter() - t0) * 1e3,
+                   transport=self.transport.name, n=self.nranks,
+                   mode='shrink', can_shrink=True)
 
     def _drop(self):
         self.transport.close()
         self.rank = None
         self.nranks = 0
+        self.sub = 0
 
     def run_fence(self, message):
         epoch = int(message['epoch'])
         gen = int(message['gen'])
+        sub = int(message.get('sub', 0))
         members = [int(s) for s in message.get('slots', [])]
         width = node_width(message.get('width', MIN_SLOTS))
-        if self.rank is None or gen != self.gen:
-            raise FenceError('no communicator for generation %d (have %s)'
-                             % (gen, self.gen if self.rank is not None
-                                else 'none'))
+        if self.rank is None or gen != self.gen or sub != self.sub:
+            raise FenceError('no communicator for generation %d.%d (have %s)'
+                             % (gen, sub, '%d.%d' % (self.gen, self.sub)
+                                if self.rank is not None else 'none'))
         vec = node_vector(epoch, self.slot, members, width)
         t0 = time.perf_counter()
         # node-wide sequence number: epochs are per resource
@@ -359,13 +558,28 @@ class NodeFenceAgent(object):
         expected = node_expected(epoch, self.nranks, members, width)
         ok = list(result) == expected
         report = {'epoch': epoch, 'seq': message.get('seq'), 'gen': gen,
-                  'ok': ok, 'rank': self.rank,
+                  'sub': sub, 'ok': ok, 'rank': self.rank,
                   'n': self.nranks, 'transport': self.transport.name,
-                  'wall_ms': wall_ms, 'init_ms': 0.0, 'mode': 'node'}
+                  'wall_ms': wall_ms, 'init_ms': 0.0,
+                  'mode': 'shrink' if sub else 'node'}
         report.update(info)
-        if not ok:
+        if ok:
+            # the agreed membership, read from this rank's own result
+            mask = [i for i, bit in enumerate(result[1:]) if bit]
+            with self.agreed_cv:
+                self.agreed[message.get('group')] = {
+                    'seq': int(message.get('seq', 0)), 'epoch': epoch,
+                    'slots': mask}
+                self.agreed_cv.notify_all()
+        else:
             report['detail'] = 'got %s expected %s' % (result, expected)
         return report
+
+    def agreement(self, group):
+        """``{'seq', 'epoch', 'slots'}`` of the last fence of ``group`` this
+        rank completed, or None."""
+        with self.agreed_cv:
+            return self.agreed.get(group)
 
     def _run(self):
         while True:
@@ -375,6 +589,9 @@ class NodeFenceAgent(object):
             cmd = message.get('cmd')
             if cmd == 'comm_init':
                 self._comm_init(message)
+                continue
+            if cmd == 'comm_shrink':
+                self._comm_shrink(message)
                 continue
             if cmd == 'comm_abort':
                 if int(message.get('gen', 0)) >= self.gen:
@@ -393,8 +610,10 @@ class NodeFenceAgent(object):
                 report = {'epoch': epoch, 'seq': message.get('seq'),
                           'gen': message.get('gen'),
                           'ok': False, 'detail': str(err), 'rank': self.rank,
-                          'transport': self.transport.name, 'mode': 'node'}
-                self._drop()   # a failed collective leaves no usable comm
+                          'transport': self.transport.name, 'mode': 'node',
+                          'interrupted': isinstance(err, FenceInterrupted)}
+                if not isinstance(err, FenceInterrupted):
+                    self._drop()   # a failed collective leaves no usable comm
             finally:
                 self.idle.set()
             self.completed.append(report)

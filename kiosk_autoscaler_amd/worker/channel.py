@@ -9,8 +9,12 @@ Manager -> worker (``--cmd-fd``), one JSON object per line:
 import json
 import os
 import queue
+import select
 import threading
 import time
+
+#: ``read_command(timeout=...)`` result when nothing arrived in time
+TIMEOUT = {'cmd': '__timeout__'}
 
 
 class Channel(object):
@@ -50,15 +54,23 @@ class Channel(object):
         line, self._buf = self._buf.split(b'\n', 1)
         return json.loads(line)
 
-    def read_command(self):
-        """Blocking read of the next command (``None`` on EOF).  Once the
-        reader thread runs (after the first assignment), commands come from
-        its queue."""
+    def read_command(self, timeout=None):
+        """Blocking read of the next command (``None`` on EOF; after
+        ``timeout`` seconds without one, :data:`TIMEOUT`).  Once the reader
+        thread runs (after the first assignment), commands come from its
+        queue."""
         if self.cmd_fd is None:
             return None
         if self._reader is not None:
-            message = self.commands.get()
+            try:
+                message = self.commands.get(timeout=timeout)
+            except queue.Empty:
+                return TIMEOUT
             return None if message.get('cmd') == 'eof' else message
+        if timeout is not None and b'\n' not in self._buf:
+            ready, _, _ = select.select([self.cmd_fd], [], [], timeout)
+            if not ready:
+                return TIMEOUT
         return self._read_line()
 
     def start_reader(self):

@@ -126,9 +126,9 @@ def _engine_key(backend, cfg):
     if spec:
         return ('plugin', spec, backend, cfg.dim, cfg.hidden, cfg.layers,
                 max(cfg.rows * cfg.batch, 256), cfg.seed)
-    if backend != 'hip':
-        return None
-    return ('hip', cfg.dim, cfg.hidden, cfg.layers,
+    # (the CPU mock engine is cached like the HIP one: the CPU tests of the
+    # recycle / HBM-tier paths exercise the same code)
+    return (backend, cfg.dim, cfg.hidden, cfg.layers,
             max(cfg.rows * cfg.batch, 256), cfg.seed)
 
 
@@ -161,9 +161,34 @@ def _cached_engine(backend, cfg, stage):
 
 def _release_engine(engine):
     """End of an assignment: a cached engine stays resident (freed when the
-    process exits or a different model needs the HBM)."""
+    process exits, a different model needs the HBM, or the standby has
+    been idle ``ENGINE_IDLE_RELEASE_S``)."""
     if engine is not None and engine not in _ENGINES.values():
         engine.close()
+
+
+def _cached_engine_bytes():
+    total = 0
+    for engine in _ENGINES.values():
+        size = getattr(engine, 'hbm_bytes', None)
+        if callable(size):
+            try:
+                total += int(size())
+            except Exception:  # pylint: disable=broad-except
+                pass
+    return total
+
+
+def _drop_cached_engines():
+    """Tier 1 of the standby's HBM (ENGINE_IDLE_RELEASE_S): free the kept
+    engine -- weights, arena, graphs -- and keep the HIP context, code
+    objects, queue and node communicator.  Returns the bytes released."""
+    released = _cached_engine_bytes()
+    for engine in list(_ENGINES.values()):
+        engine.close()
+    _ENGINES.clear()
+    gc.collect()
+    return released
 
 
 def _process_redis(role, host=None, port=None):
@@ -383,27 +408,47 @@ def _standalone(backend):
 
 
 def _hbm_free(backend, preinit):
-    """Free HBM bytes as this standby sees it, or None (not measurable:
-    no HIP context yet).  ``MOCK_HBM_FREE_BYTES`` stands in on CPU."""
+    """Free HBM bytes an assignment on this standby can use, or None (not
+    measurable: no HIP context yet).  A recycled standby's cached engine
+    counts as free: an assignment of the same model reuses it and any other
+    one frees it first (it was subtracted twice, under-sizing
+    KEYS_PER_POD exactly when HBM is tight).  ``MOCK_HBM_FREE_BYTES`` stands
+    in on CPU for the device's free memory with nothing of ours in it."""
+    cached = _cached_engine_bytes()
     mock = os.environ.get('MOCK_HBM_FREE_BYTES')
     if mock:
-        return int(mock)
-    if backend != 'hip' or not preinit:
+        measured = int(mock) - cached    # what hipMemGetInfo would say
+        return measured + cached
+    if backend != 'hip' or not (preinit or _ENGINES):
         return None
     try:
         from ..ops import native
         free, _total = native.load().mem_info()
-        return int(free)
+        return int(free) + cached
     except Exception:  # pylint: disable=broad-except
         return None
 
 
 def _wait_for_assignment(channel, pin, preload_ns, backend, preinit):
-    """Standby: report, then block until ``assign`` (or ``exit``/EOF)."""
+    """Standby: report, then block until ``assign`` (or ``exit``/EOF).
+    With ``ENGINE_IDLE_RELEASE_S`` a kept engine is freed after that long
+    without an assignment (``engine_released``, with the new free HBM)."""
+    from .channel import TIMEOUT
     channel.emit('standby', preload_ns=preload_ns, backend=backend,
-                 preinit=preinit, hbm_free=_hbm_free(backend, preinit))
+                 preinit=preinit, hbm_free=_hbm_free(backend, preinit),
+                 engine_cached=bool(_ENGINES))
+    try:
+        release_s = float(os.environ.get('ENGINE_IDLE_RELEASE_S', 0) or 0)
+    except ValueError:
+        release_s = 0.0
     while True:
-        message = channel.read_command()
+        timeout = release_s if release_s > 0 and _ENGINES else None
+        message = channel.read_command(timeout=timeout)
+        if message is TIMEOUT:
+            released = _drop_cached_engines()
+            channel.emit('engine_released', released_bytes=released,
+                         hbm_free=_hbm_free(backend, preinit))
+            continue
         if message is None or message.get('cmd') in ('exit', 'eof'):
             return None
         if message.get('cmd') == 'assign':

@@ -19,6 +19,7 @@ import time
 
 from ..redisq import exceptions as redis_errors
 from .pinning import apply_assignment_env, parse_assignment  # noqa: F401
+from ..utils import keys
 from ..utils.trace import trace_range
 
 logger = logging.getLogger('Worker')
@@ -52,6 +53,8 @@ class WorkerConfig(object):
         template = assignment.get('template', {})
         self.worker_id = assignment['worker_id']
         self.kind = assignment.get('kind', 'deployment')
+        self.group = '%s/%s' % (assignment.get('namespace', 'default'),
+                                assignment.get('resource', ''))
         self.slot = assignment.get('slot', 0)
         self.gpu = assignment.get('gpu', '')
         self.queues = template.get('queues') or env.get(
@@ -97,8 +100,7 @@ class QueueConsumer(object):
         self._sweep = 0
 
     def processing_key(self, queue, slot=0):
-        suffix = '' if slot == 0 else '.%d' % slot
-        return 'processing-%s:%s%s' % (queue, self.worker_id, suffix)
+        return keys.processing_key(queue, self.worker_id, slot)
 
     def pull(self, limit=1, block=True):
         """Return up to ``limit`` ``(queue, item, processing_key)`` tuples.
@@ -163,6 +165,11 @@ class WorkerRuntime(object):
         self.recycle = bool(config.recycle)
         self.stages = {}
         self.keys_done = 0
+        # membership gate: the agreement seq this assignment started after,
+        # and whether a fence has included this worker since
+        self._gate_base = None
+        self._gate_included = False
+        self.fenced_out = False
 
     def _stage(self, name, t=None):
         t = time.monotonic_ns() if t is None else int(t)
@@ -214,12 +221,40 @@ class WorkerRuntime(object):
                          stages=self.stages)
         if self.node_agent is not None:
             self.fence_agent = self.node_agent
+            agreed = self.node_agent.agreement(cfg.group)
+            self._gate_base = agreed['seq'] if agreed else 0
         elif self.fence_factory is not None:
             self.fence_agent = self.fence_factory(self)
             direct = getattr(self.channel, 'direct', None)
             if direct is not None and self.fence_agent is not None:
                 for cmd in ('fence', 'fence_abort'):
                     direct[cmd] = self.fence_agent.submit
+
+    def excluded(self):
+        """True once the node's agreed membership of this resource, read
+        from this rank's own all-reduce result, has included this worker and
+        a newer one no longer does: the manager's published active set is
+        authoritative, so a worker fenced out stops taking keys (it drains
+        or is told otherwise by the next fence).  The first keys before any
+        fence are served ungated (the fence is off the
+        first-inference critical path)."""
+        if self._gate_base is None:
+            return False
+        agreed = self.node_agent.agreement(self.config.group)
+        if not agreed or agreed['seq'] <= self._gate_base:
+            return False
+        inside = int(self.config.slot) in agreed['slots']
+        if inside:
+            self._gate_included = True
+        out = self._gate_included and not inside
+        if out != self.fenced_out:
+            self.fenced_out = out
+            self.channel.emit('fenced_out' if out else 'fenced_in',
+                              seq=agreed['seq'])
+            self._emit_event('worker_fenced_out' if out else
+                             'worker_fenced_in', seq=agreed['seq'],
+                             epoch=agreed['epoch'])
+        return out
 
     def run(self):
         cfg = self.config
@@ -242,6 +277,9 @@ class WorkerRuntime(object):
                 self._handle_commands()
                 if self.draining:
                     break
+                if self.excluded():
+                    time.sleep(cfg.poll_block)
+                    continue
                 try:
                     items = consumer.pull(limit=cfg.batch)
                 except redis_errors.ConnectionError as err:

@@ -213,6 +213,32 @@ def test_state_persist_restore_and_orphans():
     assert third.list_namespaced_deployment('ns').items[0].spec.replicas == 0
 
 
+def test_dotted_resource_names_recover_and_count(redis_client):
+    """Resource names may contain dots (DNS-1123 subdomains): orphan
+    recovery and the strict policy's busy-worker set strip only the batch
+    slot suffix."""
+    from kiosk_autoscaler_amd import Autoscaler
+    from kiosk_autoscaler_amd.utils.keys import processing_key, worker_of
+    assert worker_of('processing-q:my.app-g0-ab-3') == 'my.app-g0-ab-3'
+    assert worker_of('processing-q:my.app-g0-ab-3.2') == 'my.app-g0-ab-3'
+    assert processing_key('q', 'my.app-g1-ab-4', 1) == \
+        'processing-q:my.app-g1-ab-4.1'
+    redis = redis_client
+    slots = [gpus.GpuSlot(i, '', kind='cpu') for i in range(2)]
+    tpl = gpumgr.WorkerTemplate(queues=['q'], backend='cpu')
+    redis.rpush('processing-q:my.app-g0-1f2e3-3', 'job-a')
+    redis.rpush('processing-q:my.app-g1-1f2e3-4.1', 'job-b')
+    manager = gpumgr.GpuManager(slots, redis_client=redis, fence=False)
+    manager.register('deployment', 'ns', 'my.app', tpl)
+    assert sorted(redis.lrange('q', 0, -1)) == ['job-a', 'job-b']
+    redis.rpush('processing-q:my.app-g0-1f2e3-5', 'x')
+    redis.rpush('processing-q:my.app-g1-1f2e3-6', 'y')
+    redis.rpush('processing-q:my.app-g1-1f2e3-6.1', 'z')
+    scaler = Autoscaler(redis, 'q')
+    scaler.tally_queues()
+    assert scaler.busy_workers == {'my.app-g0-1f2e3-5', 'my.app-g1-1f2e3-6'}
+
+
 def test_worker_ids_unique_across_instances_and_fence_backoff():
     slots = [gpus.GpuSlot(0, '', kind='cpu')]
     a = gpumgr.GpuManager(slots, fence=False)

@@ -88,3 +88,72 @@ def test_gpu_job_kpp4_sized_from_hip_free(stack):
     starts = {client.hget('predict:job%d' % i, 'started_ns')
               for i in range(4)}
     assert len(starts) == 2
+
+
+@pytest.mark.slow
+def test_recycled_standby_reports_its_cached_engine_as_free(stack):
+    """ADVICE r2: a recycled standby keeps its engine (WORKER_KEEP_ENGINE);
+    the free HBM it reports must count that engine as available (the next
+    assignment reuses or frees it), else KEYS_PER_POD is sized twice
+    against the weights and the batch -- and the cached engine -- change.
+    The mock device reports MOCK_HBM_FREE_BYTES minus what the process
+    holds, as hipMemGetInfo would."""
+    from kiosk_autoscaler_amd.utils import hbm
+    weights = hbm.model_bytes(64, 256, 1)
+    per_key = 10 ** 9
+    s, client, manager, scaler, events = stack(
+        RESOURCE_TYPE='deployment', KEYS_PER_POD='4', MAX_PODS='1',
+        WARM_POOL='1', MODEL_DIM='64', MODEL_HIDDEN='256', MODEL_LAYERS='1',
+        HBM_PER_KEY_BYTES=str(per_key), HBM_FREE_RESERVE_BYTES='0',
+        extra_env={'MOCK_HBM_FREE_BYTES': str(int(weights + 3.5 * per_key)),
+                   'MOCK_WORK_MS': '20'})
+    for cycle in range(2):
+        wait_for(lambda: manager.standbys and all(
+            p.booted for p in manager.standbys.values()), timeout=30)
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 1}})
+        wait_for(lambda: len(_sizing(events)) == cycle + 1, timeout=30)
+        wait_for(lambda: manager.list_namespaced_deployment('default')
+                 .items[0].status.ready_replicas == 1, timeout=30)
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 0}})
+        wait_for(lambda: not manager.status()['resources'][0]['workers'],
+                 timeout=30)
+    first, second = _sizing(events)[:2]
+    assert first['keys_per_pod'] == second['keys_per_pod'] == 3
+    assert first['hbm_free'] == second['hbm_free']
+    recycled = [e for e in events.records if e['ev'] == 'worker_recycled']
+    assert recycled
+
+
+@pytest.mark.slow
+def test_engine_idle_release_frees_the_kept_engine(stack):
+    """ENGINE_IDLE_RELEASE_S: tier 1 of what a standby holds.  After that
+    long without an assignment the recycled standby frees its kept engine
+    (weights, arena, graphs), reports the new free HBM and keeps the rest
+    (process, context, node communicator): the next assignment builds the
+    engine again, no process boot."""
+    s, client, manager, scaler, events = stack(
+        MAX_PODS='1', WARM_POOL='1',
+        extra_env={'ENGINE_IDLE_RELEASE_S': '0.5', 'MOCK_WORK_MS': '10',
+                   'MOCK_HBM_FREE_BYTES': str(10 ** 11)})
+    wait_for(lambda: manager.standbys and all(
+        p.booted for p in manager.standbys.values()), timeout=30)
+    pid = manager.standbys[0].pid
+    manager.patch_namespaced_deployment('worker', 'default',
+                                        {'spec': {'replicas': 1}})
+    wait_for(lambda: manager.list_namespaced_deployment('default')
+             .items[0].status.ready_replicas == 1, timeout=30)
+    manager.patch_namespaced_deployment('worker', 'default',
+                                        {'spec': {'replicas': 0}})
+    released = wait_for(lambda: [e for e in events.records
+                                 if e['ev'] == 'engine_released'], timeout=30)
+    assert released[0]['pid'] == pid and released[0]['released_bytes'] > 0
+    assert released[0]['hbm_free'] == 10 ** 11
+    assert manager.standbys[0].pid == pid      # same process, still warm
+    manager.patch_namespaced_deployment('worker', 'default',
+                                        {'spec': {'replicas': 1}})
+    wait_for(lambda: manager.list_namespaced_deployment('default')
+             .items[0].status.ready_replicas == 1, timeout=30)
+    workers = manager.status()['resources'][0]['workers']
+    assert workers[0]['pid'] == pid and workers[0]['from_pool']

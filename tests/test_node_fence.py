@@ -358,29 +358,83 @@ def _converged(manager, client):
         manager.node.inflight is None
 
 
-@pytest.mark.slow
-@pytest.mark.parametrize('transport', ['store', 'gloo'])
-def test_eight_workers_churn_and_death(resp_server, transport):
-    from kiosk_autoscaler_amd import Autoscaler, gpumgr, policy
-    from kiosk_autoscaler_amd.bench import metrics
+TRANSPORTS = {
+    # name: (FENCE, extra worker env, can shrink)
+    'store': ('store', {}, True),
+    'gloo': ('gloo', {}, False),
+    # the production RcclNodeTransport -> _kiosk_hip-style Fence -> RCCL
+    # entry points, in 8 processes: the CPU build of the bindings over the
+    # shared-memory fake HIP + RCCL (csrc/fakes, KIOSK_NATIVE=fake)
+    'rccl-fake': ('rccl', {'KIOSK_NATIVE': 'fake'}, True),
+    # the native host shared-memory transport of the real module
+    'shm': ('shm', {}, True),
+}
+
+
+def _fake_built():
+    from kiosk_autoscaler_amd.ops import native
+    import glob
+    return bool(glob.glob(os.path.join(native.FAKE_DIR,
+                                       '_kiosk_fence_cpu*.so')))
+
+
+def _ensure_native(transport):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if transport == 'rccl-fake' and not _fake_built():
+        sys.path.insert(0, os.path.join(root, 'tools'))
+        import build_native
+        build_native.build_fake()
+    if transport == 'shm':
+        from kiosk_autoscaler_amd.ops import native
+        if not native.extension_candidates():
+            pytest.skip('_kiosk_hip not built')
+
+
+def _node_stack(resp_server, transport, tmp_path, extra=None, **overrides):
+    from kiosk_autoscaler_amd import Autoscaler, gpumgr
     from kiosk_autoscaler_amd.config import Config, Settings
     from kiosk_autoscaler_amd.redisq import RedisClient, StrictRedis
     from kiosk_autoscaler_amd.utils.events import EventLog
+    _ensure_native(transport)
+    fence, worker_env, _ = TRANSPORTS[transport]
     env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
            'QUEUES': 'predict,track', 'RESOURCE_NAME': 'worker',
            'MAX_PODS': '8', 'KEYS_PER_POD': '1', 'WORKER_BACKEND': 'cpu',
-           'WARM_POOL': '8', 'FENCE': transport, 'INTERVAL': '1',
+           'WARM_POOL': '8', 'FENCE': fence, 'INTERVAL': '1',
            'REDIS_INTERVAL': '0', 'EVENT_LOG': 'redis'}
+    env.update(overrides)
     s = Settings(Config(environ=env, use_files=False))
     client = StrictRedis(host=resp_server.host, port=resp_server.port,
                          decode_responses=True)
     events = EventLog(source='test')
     events.keep = True
+    worker_env = dict(worker_env, MOCK_WORK_MS='400',
+                      FAKE_RCCL_DIR=str(tmp_path), KIOSK_SHM_DIR=str(tmp_path))
+    worker_env.update(extra or {})
     manager = gpumgr.build_manager(s, redis_client=client, events=events,
-                                   extra_env={'MOCK_WORK_MS': '400'}).start()
+                                   extra_env=worker_env).start()
     proxy = RedisClient(host=resp_server.host, port=resp_server.port,
                         backoff=0)
     scaler = Autoscaler(proxy, s.QUEUES, actuator=manager)
+    return s, client, events, manager, scaler
+
+
+def _index(records, predicate):
+    for i, record in enumerate(records):
+        if predicate(record):
+            return i
+    return None
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize('transport', sorted(TRANSPORTS))
+def test_eight_workers_churn_and_death(resp_server, transport, tmp_path):
+    from kiosk_autoscaler_amd import policy
+    from kiosk_autoscaler_amd.bench import metrics
+    fence_kind, _, can_shrink = TRANSPORTS[transport]
+    s, client, events, manager, scaler = _node_stack(resp_server, transport,
+                                                      tmp_path)
     counter = [0]
 
     def enqueue(n_predict, n_track):
@@ -431,8 +485,9 @@ def test_eight_workers_churn_and_death(resp_server, transport):
                      len(_ready_ids(manager)) == 8, timeout=30)
             wait_for(lambda: all_done(batch), timeout=30)
         assert manager.node.generations == 1    # churn never re-inits
-        # kill -9 a busy worker: its item is requeued, the slot's new
-        # process joins a second generation, the set converges again
+        # kill -9 a busy worker: its item is requeued, the survivors shrink
+        # it out (or, gloo, drop the generation), the slot's new process
+        # joins the next full generation, the set converges again
         batch = enqueue(8, 8)
         victim = wait_for(lambda: [w for w in _ready_ids(manager)
                                    if client.exists('processing-%s:%s' % (
@@ -449,21 +504,81 @@ def test_eight_workers_churn_and_death(resp_server, transport):
         assert victim['id'] not in _active(client)['members']
         assert tick() == 0
         wait_for(lambda: _active(client)['members'] == [], timeout=30)
+        if can_shrink:
+            _death_mid_allreduce(manager, client, events)
     finally:
         manager.stop(timeout=15)
     from kiosk_autoscaler_amd.utils.events import drain_redis
     records = events.records + drain_redis(client)   # + workers' events
     done = [e for e in records if e['ev'] == 'fence_done']
-    assert done and all(e['n'] == 8 and e['mode'] == 'node' and
-                        e['transport'] == transport for e in done)
-    assert sum(1 for e in records if e['ev'] == 'node_comm_ready') == 2
+    assert done and all(e['transport'] == fence_kind for e in done)
+    assert all((e['n'], e['mode']) in ((8, 'node'), (7, 'shrink'))
+               for e in done), [(e['n'], e['mode']) for e in done]
+    generations = 3 if can_shrink else 2
+    inits = [e for e in records if e['ev'] == 'node_comm_ready' and
+             e.get('mode', 'init') == 'init']
+    assert len(inits) == generations
     breaks = [e for e in records if e['ev'] == 'node_comm_break']
-    assert len(breaks) == 1 and not breaks[0]['failed']
+    assert not any(b['failed'] for b in breaks)
+    if can_shrink:
+        # no generation was ever dropped: every loss was shrunk out
+        assert not breaks
+        assert sum(1 for e in records if e['ev'] == 'node_comm_shrink') == 2
+    else:
+        assert len(breaks) == 1
     idle, alive, busy = metrics.gpu_idle(records, 0, time.monotonic_ns())
     assert 0 < busy < alive and 0 < idle < 100
     stats = metrics.fence_stats(records)
     assert stats['fence_max_ranks'] == 8
-    assert stats['node_comm_generations'] == 2
+    assert stats['node_comm_generations'] == generations
+    # no shared-memory segment outlives its generation
+    assert not [f for f in os.listdir(str(tmp_path))
+                if f.startswith('kiosk-shm-')]
+
+
+def _death_mid_allreduce(manager, client, events):
+    """SIGSTOP slot 7's standby, scale 4 -> 5 so a fence starts (the frozen
+    rank never posts: the other seven block in the all-reduce), then
+    SIGKILL it.  The survivors' all-reduce is interrupted, they shrink the
+    dead rank out, and the re-run fence completes over 7 ranks -- before the
+    slot's replacement process joins the next full generation."""
+    manager.patch_namespaced_deployment('worker', 'default',
+                                        {'spec': {'replicas': 4}})
+    wait_for(lambda: _converged(manager, client) and
+             len(_ready_ids(manager)) == 4, timeout=30)
+    frozen = wait_for(lambda: manager.standbys.get(7), timeout=20)
+    wait_for(lambda: frozen.node_ok and manager.node.full, timeout=30)
+    gens = manager.node.generations
+    os.kill(frozen.pid, signal.SIGSTOP)
+    try:
+        mark = len(events.records)
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 5}})
+        wait_for(lambda: len(_ready_ids(manager)) == 5, timeout=30)
+        wait_for(lambda: manager.node.inflight is not None, timeout=10)
+        time.sleep(0.3)                     # the survivors are blocked now
+        assert manager.node.inflight is not None
+        assert not [e for e in events.records[mark:]
+                    if e['ev'] == 'fence_done']
+    finally:
+        os.kill(frozen.pid, signal.SIGKILL)
+        os.kill(frozen.pid, signal.SIGCONT)
+    wait_for(lambda: manager.node.generations == gens + 1, timeout=60)
+    wait_for(lambda: _converged(manager, client) and
+             len(_ready_ids(manager)) == 5, timeout=30)
+    tail = events.records[mark:]
+    shrunk = _index(tail, lambda e: e['ev'] == 'node_comm_ready' and
+                    e.get('mode') == 'shrink')
+    fenced7 = _index(tail, lambda e: e['ev'] == 'fence_done' and
+                     e['n'] == 7 and e['mode'] == 'shrink')
+    regrown = _index(tail, lambda e: e['ev'] == 'node_comm_ready' and
+                     e.get('mode') == 'init')
+    assert shrunk is not None and fenced7 is not None and regrown is not None
+    assert shrunk < fenced7 < regrown, [e['ev'] for e in tail]
+    assert len(tail[fenced7]['members']) == 5
+    manager.patch_namespaced_deployment('worker', 'default',
+                                        {'spec': {'replicas': 0}})
+    wait_for(lambda: _active(client)['members'] == [], timeout=30)
 
 
 @pytest.mark.gpu
@@ -699,3 +814,94 @@ def test_two_resources_share_the_node_communicator(resp_server):
     assert len(done) >= 2 and all(e['n'] == 2 for e in done)
     seqs = [e['seq'] for e in events.records if e['ev'] == 'fence_start']
     assert seqs == sorted(seqs) and len(set(seqs)) == len(seqs)
+
+
+@pytest.mark.slow
+def test_hung_rccl_init_at_eight_ranks_falls_back(resp_server, tmp_path):
+    """The driver's first 8-GPU run is the first time RCCL builds an 8-rank
+    communicator: if that init hangs, every rank's ``Fence.connect`` (the
+    real code, over the fake RCCL in ``init_hang`` mode) must give up after
+    FENCE_INIT_TIMEOUT, the manager must switch to the shm transport after
+    two such generations -- within 2 x FENCE_INIT_TIMEOUT (+ slack) of pool
+    boot -- and membership must be fenced (8 ranks) right after."""
+    timeout_s = 2.0
+    s, client, events, manager, scaler = _node_stack(
+        resp_server, 'rccl-fake', tmp_path,
+        extra={'FAKE_RCCL_MODE': 'init_hang'},
+        FENCE_INIT_TIMEOUT=str(timeout_s))
+    try:
+        assert manager.node.init_timeout == timeout_s
+        wait_for(lambda: any(e['ev'] == 'node_comm_init'
+                             for e in events.records), timeout=60)
+        t_init = [e['t'] for e in events.records
+                  if e['ev'] == 'node_comm_init'][0]
+        fallback = wait_for(lambda: [e for e in events.records
+                                     if e['ev'] == 'node_comm_fallback'],
+                            timeout=30)[0]
+        elapsed = (fallback['t'] - t_init) / 1e9
+        assert elapsed <= 2 * timeout_s + 1.5, elapsed
+        assert fallback['transport'] == 'shm'
+        wait_for(lambda: manager.node.ready, timeout=20)
+        assert manager.node.transport == 'shm' and \
+            len(manager.node.members) == 8
+        status = manager.status()['node_comm']
+        assert status['fallback'] == 'shm' and status['failed_total'] >= 2
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 2}})
+        wait_for(lambda: _converged(manager, client) and
+                 len(_ready_ids(manager)) == 2, timeout=30)
+    finally:
+        manager.stop(timeout=15)
+    from kiosk_autoscaler_amd.bench import metrics
+    stats = metrics.fence_stats(events.records)
+    assert stats['node_comm_fallbacks'] == 1
+    assert stats['node_comm_fallback_transport'] == 'shm'
+    assert stats['node_comm_init_ms_by_ranks']['8']['count'] == 1
+    done = [e for e in events.records if e['ev'] == 'fence_done']
+    assert done and all(e['transport'] == 'shm' and e['n'] == 8
+                        for e in done)
+
+
+@pytest.mark.slow
+def test_withheld_fence_holds_available_replicas(resp_server, tmp_path):
+    """The fenced membership is what the observer sees: while one rank is
+    frozen (SIGSTOP) the fence cannot complete, so READY moves to 2 but
+    ``status.available_replicas`` (= the reference's ``only_running`` read,
+    ``autoscaler.py:176-179``) and ``kiosk:active`` stay at the old agreed
+    set, ``status.fence`` says a fence is pending; after SIGCONT all
+    converge."""
+    from kiosk_autoscaler_amd import Autoscaler
+    s, client, events, manager, scaler = _node_stack(
+        resp_server, 'shm', tmp_path, MAX_PODS='4', WARM_POOL='4')
+
+    def view():
+        return manager.list_namespaced_deployment('default').items[0]
+    try:
+        wait_for(lambda: manager.node.ready and manager.node.full,
+                 timeout=60)
+        frozen = manager.standbys[3]
+        os.kill(frozen.pid, signal.SIGSTOP)
+        try:
+            manager.patch_namespaced_deployment('worker', 'default',
+                                                {'spec': {'replicas': 2}})
+            wait_for(lambda: view().status.ready_replicas == 2, timeout=30)
+            time.sleep(0.5)
+            v = view()
+            assert v.status.available_replicas == 0
+            assert v.status.fenced_replicas == 0
+            assert v.status.fence['pending'] and not v.status.fence['in_sync']
+            assert scaler.get_current_pods('default', 'deployment', 'worker',
+                                           only_running=True) == 0
+            assert scaler.get_current_pods('default', 'deployment',
+                                           'worker') == 2
+            assert not _active(client) or _active(client)['members'] == []
+        finally:
+            os.kill(frozen.pid, signal.SIGCONT)
+        wait_for(lambda: view().status.available_replicas == 2, timeout=30)
+        assert view().status.fence['in_sync']
+        assert len(_active(client)['members']) == 2
+        assert scaler.get_current_pods('default', 'deployment', 'worker',
+                                       only_running=True) == 2
+        assert isinstance(scaler, Autoscaler)
+    finally:
+        manager.stop(timeout=15)

@@ -176,3 +176,39 @@ def test_multi_queue_pull_is_round_robin(redis_client):
             order.append(queue)
             consumer.complete(pkey)
     assert order == ['predict', 'track', 'predict', 'track']
+
+
+class _Agreement(object):
+    """Stands in for NodeFenceAgent.agreement (the rank's own result)."""
+
+    def __init__(self):
+        self.by_group = {}
+
+    def agreement(self, group):
+        return self.by_group.get(group)
+
+
+def test_worker_fenced_out_stops_pulling(redis_client):
+    """A worker serves ungated until a fence includes it; once a newer
+    agreed membership excludes its slot it takes no more keys, and a later
+    fence that includes it again resumes it."""
+    agent = _Agreement()
+    group = 'default/w'
+    agent.by_group[group] = {'seq': 3, 'epoch': 2, 'slots': []}   # stale
+    env = {'ROWS_PER_KEY': '8', 'MOCK_WORK_MS': '0', 'QUEUES': 'predict'}
+    cfg = rt.WorkerConfig(env, {'worker_id': 'w-g1-x-1', 'slot': 1,
+                                'namespace': 'default', 'resource': 'w'})
+    run = rt.WorkerRuntime(cfg, None, _Channel(), lambda: redis_client,
+                           node_agent=agent)
+    run._gate_base = agent.agreement(group)['seq']
+    assert not run.excluded()                 # nothing newer: ungated
+    agent.by_group[group] = {'seq': 4, 'epoch': 3, 'slots': [0]}
+    assert not run.excluded()                 # never included yet
+    agent.by_group[group] = {'seq': 5, 'epoch': 4, 'slots': [0, 1]}
+    assert not run.excluded()
+    agent.by_group[group] = {'seq': 6, 'epoch': 5, 'slots': [0]}
+    assert run.excluded() and run.fenced_out
+    assert ('fenced_out', {'seq': 6}) in run.channel.events
+    agent.by_group[group] = {'seq': 7, 'epoch': 6, 'slots': [1]}
+    assert not run.excluded()
+    assert ('fenced_in', {'seq': 7}) in run.channel.events

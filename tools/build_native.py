@@ -6,6 +6,11 @@
   pybind11 bindings), compiled with ``hipcc --offload-arch=gfx950`` and
   linked ``-shared -fPIC``.  RCCL is dlopen'ed at run time (see fence.hpp).
 * ``build/kredis-server`` -- the native RESP server (csrc/kredis), g++.
+* ``--fake-hip``: ``build/fake/_kiosk_fence_cpu<ext>`` -- the node
+  communicator bindings (RCCL Fence + ShmComm, csrc/runtime/bind_comm.cpp)
+  built with g++ for the CPU against ``build/fake/libkiosk_fake_hip_rccl.so``
+  (csrc/fakes: shared-memory multi-process HIP + RCCL stand-ins), so the
+  production fence code runs in N CPU processes (``KIOSK_NATIVE=fake``).
 
 Objects are cached by source mtime under ``build/obj``; ``--clean`` rebuilds.
 """
@@ -25,6 +30,9 @@ HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 EXT = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
 EXT_PATH = os.path.join(ROOT, 'kiosk_autoscaler_amd', 'ops', '_kiosk_hip' + EXT)
 KREDIS = os.path.join(BUILD, 'kredis-server')
+FAKE_DIR = os.path.join(BUILD, 'fake')
+FAKE_LIB = os.path.join(FAKE_DIR, 'libkiosk_fake_hip_rccl.so')
+FAKE_EXT = os.path.join(FAKE_DIR, '_kiosk_fence_cpu' + EXT)
 
 
 def _includes():
@@ -139,10 +147,44 @@ def build_kredis(verbose=False, sanitize=False):
     return target
 
 
-def build(verbose=False, clean=False, jobs=4, kernels=True, sanitize=False):
+def build_fake(verbose=False):
+    """CPU build of the node-communicator bindings over the fake HIP + RCCL
+    (host code only: g++, no hipcc, no GPU)."""
+    csrc = os.path.join(ROOT, 'csrc')
+    runtime = os.path.join(csrc, 'runtime')
+    fakes = os.path.join(csrc, 'fakes')
+    os.makedirs(FAKE_DIR, exist_ok=True)
+    cxx = shutil.which('g++') or 'c++'
+    flags = ['-O2', '-g', '-std=c++17', '-fPIC', '-Wall', '-pthread',
+             '-fvisibility=hidden', '-D__HIP_PLATFORM_AMD__',
+             '-I/opt/rocm/include', '-I' + csrc, '-I' + runtime]
+    lib_src = [os.path.join(fakes, 'fake_hip_rccl.cpp'),
+               os.path.join(runtime, 'shmcomm.cpp')]
+    headers = [os.path.join(runtime, h) for h in ('shmcomm.hpp', 'fence.hpp',
+                                                  'bind_comm.hpp',
+                                                  'trace.hpp', 'engine.hpp')]
+    if _stale(FAKE_LIB, lib_src + headers):
+        _run([cxx] + flags + ['-shared'] + lib_src + ['-o', FAKE_LIB],
+             verbose)
+    ext_src = [os.path.join(fakes, 'bind_cpu.cpp'),
+               os.path.join(runtime, 'bind_comm.cpp'),
+               os.path.join(runtime, 'fence.cpp'),
+               os.path.join(runtime, 'trace.cpp'),
+               os.path.join(runtime, 'shmcomm.cpp')]
+    if _stale(FAKE_EXT, ext_src + headers + [FAKE_LIB]):
+        _run([cxx] + flags + _includes() + ['-shared'] + ext_src +
+             [FAKE_LIB, "-Wl,-rpath,$ORIGIN", '-ldl', '-o', FAKE_EXT],
+             verbose)
+    return FAKE_EXT
+
+
+def build(verbose=False, clean=False, jobs=4, kernels=True, sanitize=False,
+          fake=True):
     if clean and os.path.isdir(BUILD):
         shutil.rmtree(BUILD)
     out = {'kredis': build_kredis(verbose)}
+    if fake:
+        out['fake_fence'] = build_fake(verbose)
     if sanitize:
         out['kredis_asan'] = build_kredis(verbose, sanitize=True)
     if kernels:
@@ -159,7 +201,13 @@ def main():
     parser.add_argument('--no-kernels', action='store_true')
     parser.add_argument('--sanitize', action='store_true',
                         help='also build the ASan+UBSan kredis-server')
+    parser.add_argument('--fake-hip', action='store_true',
+                        help='only the CPU fence module over the fake '
+                             'HIP + RCCL (build/fake)')
     args = parser.parse_args()
+    if args.fake_hip:
+        print('fake_fence: %s' % build_fake(args.verbose))
+        return
     out = build(args.verbose, args.clean, args.jobs, not args.no_kernels,
                 args.sanitize)
     for key, value in out.items():
