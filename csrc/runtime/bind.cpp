@@ -177,6 +177,21 @@ PYBIND11_MODULE(_kiosk_hip, m) {
     }
     return py::make_tuple(free_b, total_b);
   });
+  // PCI address of a HIP ordinal ("dddd:bb:dd.f"): the manager checks it
+  // against the KFD-topology slot it pinned the process to (the
+  // ordinal <-> PCI mapping was assumed, never verified)
+  m.def(
+      "device_pci_bus_id",
+      [](int device) {
+        char buf[64] = {0};
+        {
+          py::gil_scoped_release release;
+          check_hip(hipDeviceGetPCIBusId(buf, sizeof(buf) - 1, device),
+                    "hipDeviceGetPCIBusId");
+        }
+        return std::string(buf);
+      },
+      py::arg("device") = 0);
   m.def("synchronize", [] { check_hip(hipDeviceSynchronize(), "sync"); },
         py::call_guard<py::gil_scoped_release>());
   m.def("roctx_available", &kiosk::roctx_available);

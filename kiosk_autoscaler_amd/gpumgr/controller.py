@@ -318,6 +318,7 @@ class GpuManager(object):
         self.instance = '%x' % ((os.getpid() << 20 ^ time.time_ns() >> 10)
                                 & 0xfffff)
         self._stopping = False
+        self.mapping_fixes = 0   # slots remapped after a PCI check
         self.history = []   # exited workers, for accounting
         # persistent node-wide communicator: needs one long-lived process
         # per slot (a standby for every GPU, recycled workers); otherwise
@@ -740,15 +741,61 @@ class GpuManager(object):
                              released_bytes=message.get('released_bytes'),
                              hbm_free=proc.hbm_free)
             return
+        if message.get('ev') == 'device':
+            self._check_device(proc, message.get('pci'))
+            return
         if message.get('ev') == 'standby':
             proc.booted = True
             proc.hbm_free = message.get('hbm_free')
+            if message.get('pci'):
+                if not self._check_device(proc, message.get('pci')):
+                    return   # retired: the pool respawns it re-pinned
             self._publish_pool()
             self.events.emit('standby_ready', pid=proc.pid, slot=proc.slot,
                              boot_s=(time.monotonic_ns() - proc.t_spawn)
                              / 1e9, preinit=message.get('preinit'),
                              recycled=proc.role == 'standby' and
                              proc.recycles > 0)
+
+    def _check_device(self, proc, pci):
+        """the slot table maps slot -> HIP ordinal -> PCI address
+        from KFD topology order, which drives the HIP_VISIBLE_DEVICES pin,
+        the NUMA-local CPU affinity and the BDF the benchmark's amdsmi
+        cross-check samples.  The process reports the PCI address HIP sees
+        for its ordinal; on a mismatch the slot is remapped to the device
+        actually behind that ordinal (its NUMA node and CPUs re-read) and a
+        standby pinned with the wrong affinity is respawned.  False when
+        ``proc`` was retired for that."""
+        from .gpus import local_cpus, normalize_pci
+        index = proc.slot
+        slot = next((s for s in self.slots if s.index == index), None)
+        actual = normalize_pci(pci)
+        if slot is None or slot.kind != 'gpu' or actual is None:
+            return True
+        expected = normalize_pci(slot.pci)
+        proc.pci = actual
+        if expected == actual:
+            if not getattr(slot, 'pci_verified', False):
+                self.events.emit('gpu_mapping', slot=index, pci=actual,
+                                 visible=slot.visible_id, verified=True)
+            slot.pci_verified = True
+            return True
+        slot.pci = actual
+        slot.numa_node, slot.cpus = local_cpus(actual)
+        slot.pci_verified = True
+        self.mapping_fixes += 1
+        self.events.emit('gpu_mapping_mismatch', slot=index,
+                         visible=slot.visible_id, expected=expected,
+                         actual=actual, numa_node=slot.numa_node)
+        logger.error('GPU slot %d (HIP_VISIBLE_DEVICES=%s) is %s, not %s as '
+                     'KFD order suggested: remapped (NUMA node %s).', index,
+                     slot.visible_id, actual, expected, slot.numa_node)
+        if self.standbys.get(index) is proc and expected is not None:
+            del self.standbys[index]
+            proc.pipe.send({'cmd': 'exit'})
+            self.retiring.append(proc)
+            return False
+        return True
 
     def _recycle_ok(self, resource):
         tpl = self.pool_template
@@ -941,8 +988,9 @@ class GpuManager(object):
                 self._on_fenced(worker.resource, message)
             elif kind == 'recycled':
                 self._on_recycled(worker, message)
-            elif kind == 'standby':
-                # the rest of a batch that also held 'recycled'
+            elif kind in ('standby', 'device'):
+                # the rest of a batch that also held 'recycled'; a cold
+                # spawn's device report
                 self._on_standby_message(worker.proc, message)
             elif kind == 'error':
                 logger.error('Worker %s reported: %s', worker.id,

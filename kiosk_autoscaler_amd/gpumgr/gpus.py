@@ -20,7 +20,7 @@ class GpuSlot(object):
     """One schedulable device slot."""
 
     __slots__ = ('index', 'visible_id', 'pci', 'numa_node', 'cpus', 'kind',
-                 'hbm_bytes', 'cu_count')
+                 'hbm_bytes', 'cu_count', 'pci_verified')
 
     def __init__(self, index, visible_id, pci=None, numa_node=-1, cpus=None,
                  kind='gpu', hbm_bytes=0, cu_count=0):
@@ -32,6 +32,8 @@ class GpuSlot(object):
         self.kind = kind
         self.hbm_bytes = hbm_bytes
         self.cu_count = cu_count
+        # a process pinned to it reported the same PCI address through HIP
+        self.pci_verified = False
 
     def to_dict(self):
         return {k: getattr(self, k) for k in self.__slots__}
@@ -77,6 +79,27 @@ def _pci_address(props):
     domain = props.get('domain', 0)
     return '%04x:%02x:%02x.%d' % (domain, (loc >> 8) & 0xff, (loc >> 3) & 0x1f,
                                   loc & 0x7)
+
+
+def normalize_pci(text):
+    """Canonical ``dddd:bb:dd.f`` (lower case) of a PCI address as KFD,
+    amdsmi or ``hipDeviceGetPCIBusId`` print it, or ``None``."""
+    if not text:
+        return None
+    try:
+        head, func = str(text).strip().lower().rsplit('.', 1)
+        parts = head.split(':')
+        if len(parts) == 2:
+            parts = ['0'] + parts
+        domain, bus, dev = (int(p, 16) for p in parts)
+        return '%04x:%02x:%02x.%d' % (domain, bus, dev, int(func, 16))
+    except (ValueError, TypeError):
+        return None
+
+
+def local_cpus(pci):
+    """``(numa node, [cpus])`` local to a PCI device (sysfs)."""
+    return _local_cpus(pci)
 
 
 def _local_cpus(pci):

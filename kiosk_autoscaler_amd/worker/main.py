@@ -115,6 +115,33 @@ def _join_device_open(stage=None):
 
 
 _CLIENTS = {}
+# the manager pipe (set in main): the engine path reports the device's PCI
+# address on it once a HIP context exists
+_CHANNEL = []
+
+
+def _device_pci(backend, preinit=None):
+    """PCI address of the device this process drives (HIP ordinal 0 under
+    its HIP_VISIBLE_DEVICES pin), or None before it opened a context."""
+    if backend != 'hip' or not (preinit or _ENGINES):
+        return None
+    try:
+        from ..ops import native
+        return native.load().device_pci_bus_id(0)
+    except Exception:  # pylint: disable=broad-except
+        return None
+
+
+def _report_device(backend):
+    """Once per process: a standby reports its device with ``standby``, a
+    cold spawn with its first engine."""
+    if not _CHANNEL or backend != 'hip' or \
+            getattr(_CHANNEL[0], 'device_reported', False):
+        return
+    pci = _device_pci(backend, True)
+    if pci:
+        _CHANNEL[0].device_reported = True
+        _CHANNEL[0].emit('device', pci=pci)
 # HIP engines kept across recycles (WORKER_KEEP_ENGINE=1): the recycled
 # standby's next assignment with the same model finds its weights, graph
 # and pass time resident and only re-runs the warm-start kernel
@@ -156,6 +183,7 @@ def _cached_engine(backend, cfg, stage):
         engine = create_engine(backend, cfg, stage)
     if key is not None and keep:
         _ENGINES[key] = engine
+    _report_device(backend)
     return engine
 
 
@@ -274,6 +302,7 @@ def main(argv=None):
         format='[%(asctime)s]:[%(levelname)s]:[%(name)s]: %(message)s')
     from .channel import Channel
     channel = Channel(args.cmd_fd, args.ev_fd)
+    _CHANNEL[:] = [channel]
     preinit = {}
     node = bool((early or {}).get('node_fence')) and os.environ.get(
         'FENCE', 'auto') not in ('none', 'off', '0')
@@ -434,9 +463,12 @@ def _wait_for_assignment(channel, pin, preload_ns, backend, preinit):
     With ``ENGINE_IDLE_RELEASE_S`` a kept engine is freed after that long
     without an assignment (``engine_released``, with the new free HBM)."""
     from .channel import TIMEOUT
+    pci = _device_pci(backend, preinit)
+    if pci:
+        channel.device_reported = True
     channel.emit('standby', preload_ns=preload_ns, backend=backend,
                  preinit=preinit, hbm_free=_hbm_free(backend, preinit),
-                 engine_cached=bool(_ENGINES))
+                 engine_cached=bool(_ENGINES), pci=pci)
     try:
         release_s = float(os.environ.get('ENGINE_IDLE_RELEASE_S', 0) or 0)
     except ValueError:

@@ -477,3 +477,50 @@ def test_pool_parks_after_idle_and_refills_on_demand(resp_server):
         until(lambda: kinds().count('pool_parked') == 2)
     finally:
         manager.stop()
+
+
+def test_pci_mapping_verified_and_remapped(monkeypatch):
+    """a process reports the PCI address HIP sees for its pinned
+    ordinal; a match verifies the slot, a mismatch remaps the slot to the
+    real device (NUMA/CPUs re-read) and respawns a standby whose affinity
+    was wrong -- never a silent mis-pin."""
+    from kiosk_autoscaler_amd.gpumgr import gpus as gpus_mod
+    from kiosk_autoscaler_amd.gpumgr.controller import _Process
+    assert gpus_mod.normalize_pci('0000:75:00.0') == '0000:75:00.0'
+    assert gpus_mod.normalize_pci('75:00.0') == '0000:75:00.0'
+    assert gpus_mod.normalize_pci('0000:0A:1f.1') == '0000:0a:1f.1'
+    assert gpus_mod.normalize_pci('junk') is None
+    monkeypatch.setattr(gpus_mod, '_local_cpus',
+                        lambda pci: (1, [8, 9]) if pci else (-1, []))
+
+    class Proc(object):
+        pid = 4242
+        slot = 0
+        sent = []
+
+        class pipe(object):
+            @staticmethod
+            def send(message):
+                Proc.sent.append(message)
+    slots = [gpus.GpuSlot(0, '0', pci='0000:05:00.0', numa_node=0,
+                          cpus=[0, 1]),
+             gpus.GpuSlot(1, '1', pci='0000:65:00.0', numa_node=1,
+                          cpus=[8, 9])]
+    manager = gpumgr.GpuManager(slots, fence=False)
+    records = []
+    manager.events = type('E', (), {'emit': lambda self, ev, **f:
+                                    records.append(dict(f, ev=ev))})()
+    proc = Proc()
+    assert manager._check_device(proc, '0000:05:00.0')
+    assert slots[0].pci_verified and records[-1]['ev'] == 'gpu_mapping'
+    # ordinal 1 turns out to be another device than KFD order said
+    proc1 = Proc()
+    proc1.slot = 1
+    manager.standbys[1] = proc1
+    assert not manager._check_device(proc1, '0000:E5:00.0')
+    assert slots[1].pci == '0000:e5:00.0' and manager.mapping_fixes == 1
+    assert records[-1]['ev'] == 'gpu_mapping_mismatch'
+    assert records[-1]['expected'] == '0000:65:00.0'
+    assert 1 not in manager.standbys and proc1 in manager.retiring
+    assert Proc.sent[-1] == {'cmd': 'exit'}
+    assert isinstance(manager, gpumgr.GpuManager) and _Process
