@@ -727,6 +727,9 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         # engine -- which includes this rank's own torch context)
         'standby_pool_boot_hbm_mib': _r((hbm or {}).get('pool_boot_mib'), 1),
         'idle_node_hbm_mib': _r((hbm or {}).get('idle_mib_median'), 1),
+        # ENGINE_IDLE_RELEASE_S tier: idle HBM once the kept engine is freed
+        'idle_node_hbm_released_mib': _r((hbm or {}).get(
+            'idle_released_mib_median'), 1),
         'idle_node_hbm_pct_of_gpu': _r((hbm or {}).get('idle_pct_of_gpu'),
                                        3),
         'serving_hbm_mib_max': _r((hbm or {}).get('serving_mib_max'), 1),
@@ -745,6 +748,11 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         'event_busy_wall_pct': _r(100.0 * summary['gpu_busy_s'] /
                                   max(1e-9, elapsed * args.gpus)),
         'amdsmi_gfx_busy_pct': _r(gpu_util.mean_busy(util)),
+        # each slot's HIP ordinal checked against its KFD PCI address
+        'gpu_mapping_verified': sum(1 for e in events
+                                    if e.get('ev') == 'gpu_mapping'),
+        'gpu_mapping_mismatches': sum(1 for e in events if e.get('ev') ==
+                                      'gpu_mapping_mismatch'),
         'fence_transport': ','.join(fence['fence_transport']) or None,
         'fence_max_ranks': fence['fence_max_ranks'],
         'fence': {k: _r(v) for k, v in fence.items()

@@ -219,15 +219,28 @@ def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
 
     def serving(t):
         return any(a <= t <= b for a, b in spans)
+    # ENGINE_IDLE_RELEASE_S: idle samples taken after the standby freed its
+    # kept engine (an ``engine_released`` since the last worker exit)
+    releases = sorted(e['t'] for e in events
+                      if e.get('ev') == 'engine_released')
+    exits = sorted(b for _, b in spans)
+
+    def released(t):
+        last_exit = max([b for b in exits if b <= t], default=None)
+        return any((last_exit is None or r >= last_exit) and r <= t
+                   for r in releases)
     base = baseline or {}
     if pool_boot and any(pool_boot.get(b, 0.0) < v for b, v in base.items()):
         base = {}      # the "baseline" held memory the run later did not
-    idle, busy = [], []
+    idle, busy, idle_released = [], [], []
     for bdf, samples in device.items():
         zero = base.get(bdf, 0.0)
         for t, used in samples:
             if t_lo <= t <= t_hi:
-                (busy if serving(t) else idle).append(used - zero)
+                on = serving(t)
+                (busy if on else idle).append(used - zero)
+                if not on and releases and released(t):
+                    idle_released.append(used - zero)
     totals = [v for v in ((vram or {}).get('total_mib') or {}).values() if v]
     total = max(totals) if totals else None
     boot = None
@@ -242,7 +255,9 @@ def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
         'idle_pct_of_gpu': (100.0 * idle_mib / total
                             if idle_mib is not None and total else None),
         'hbm_total_mib': total,
-        'samples': {'idle': len(idle), 'serving': len(busy)},
+        'idle_released_mib_median': _pct(idle_released, 0.5),
+        'samples': {'idle': len(idle), 'serving': len(busy),
+                    'idle_released': len(idle_released)},
         'over_baseline': bool(base),
     }
 

@@ -282,7 +282,8 @@ def test_hbm_hold_splits_device_vram_by_phase():
             'total_mib': {'bdf': 294912.0}}
     out = metrics.hbm_hold(events, vram, 0, 1000, baseline={'bdf': 300.0},
                            pool_boot={'bdf': 800.0})
-    assert out['samples'] == {'idle': 3, 'serving': 1}
+    assert out['samples'] == {'idle': 3, 'serving': 1, 'idle_released': 0}
+    assert out['idle_released_mib_median'] is None
     assert out['pool_boot_mib'] == 500.0
     assert out['idle_mib_median'] == 2600.0
     assert out['serving_mib_max'] == 3600.0
@@ -295,6 +296,12 @@ def test_hbm_hold_splits_device_vram_by_phase():
                            pool_boot={'bdf': 800.0})
     assert not out['over_baseline'] and out['pool_boot_mib'] == 800.0
     assert out['idle_mib_median'] == 2900.0
+    # ENGINE_IDLE_RELEASE_S: idle samples after the engine was freed
+    released = events + [{'ev': 'engine_released', 't': 355, 'pid': 7}]
+    out = metrics.hbm_hold(released, vram, 0, 1000, baseline={'bdf': 300.0},
+                           pool_boot={'bdf': 800.0})
+    assert out['samples']['idle_released'] == 1
+    assert out['idle_released_mib_median'] == 2600.0
     # a standby that exited stops counting toward standby_gpu_s
     assert metrics.standby_gpu(events, 0, 1000) == (100 + 100) / 1e9
 

@@ -1,0 +1,35 @@
+# Round-3 MI355X bench set: what the standby pool holds vs what it costs.
+#   bash tools/gpu_round3_tiers.sh A -> default (driver command, short) +
+#        ENGINE_IDLE_RELEASE_S=5 with 6 s idle gaps (engine tier)
+#   bash tools/gpu_round3_tiers.sh B -> context + recycle (node comm over
+#        shm) + deep idle (POOL_IDLE_RELEASE_S=3)
+#   bash tools/gpu_round3_tiers.sh C -> torch plug-in: warm pool, context,
+#        cold spawn
+set -o pipefail
+OUT=${OUT:-gpurun_out/r3_tiers}
+mkdir -p $OUT
+run() {
+  tag=$1; limit=$2; shift 2
+  echo "== $tag: bench.py $*"
+  timeout -k 10 $limit python bench.py "$@" > $OUT/$tag.json 2> $OUT/$tag.err
+  rc=$?
+  cp gpurun_out/bench_detail_n1.json $OUT/${tag}_detail.json 2>/dev/null
+  cp gpurun_out/bench_events_n1.jsonl $OUT/${tag}_events.jsonl 2>/dev/null
+  tail -1 $OUT/$tag.err
+  head -c 600 $OUT/$tag.json; echo
+  return $rc
+}
+if [ "$1" = "A" ]; then
+  run default 300 --gpus 1 --steps 8 --warmup 2 --budget-s 250 && \
+  ENGINE_IDLE_RELEASE_S=5 run engine_release_5s 300 --gpus 1 --steps 8 --warmup 1 --off 6 --budget-s 270 --cold-cycles 0
+elif [ "$1" = "B" ]; then
+  run context_recycle 260 --gpus 1 --steps 10 --warmup 1 --budget-s 230 --pool-mode context --cold-cycles 0 && \
+  POOL_IDLE_RELEASE_S=3 run pool_idle_release_3s 260 --gpus 1 --steps 10 --warmup 1 --budget-s 230 --cold-cycles 0
+elif [ "$1" = "C" ]; then
+  WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine \
+    run torch_device 260 --gpus 1 --steps 6 --warmup 1 --budget-s 230 && \
+  WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine \
+    run torch_context 260 --gpus 1 --steps 6 --warmup 1 --budget-s 230 --pool-mode context --cold-cycles 0 && \
+  WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine POOL_IDLE_RELEASE_S=3 \
+    run torch_deep_idle 260 --gpus 1 --steps 6 --warmup 1 --budget-s 230 --cold-cycles 0
+fi
