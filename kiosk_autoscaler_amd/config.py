@@ -174,6 +174,9 @@ EXTRA_DEFAULTS = (
     # s from assignment to READY -> kill (0 = off)
     ('START_TIMEOUT', float, 0.0),
     ('WORKER_RECYCLE', bool, True),         # drained worker -> warm pool
+    # spawn workers by fork() from a pre-imported zygote that holds no GPU
+    # (worker/zygote.py): cold spawns skip interpreter start + imports
+    ('WORKER_ZYGOTE', bool, True),
     ('FENCE_COMM', str, 'node'),            # node (persistent) | epoch
     # node communicator transport after FENCE_FALLBACK_AFTER consecutive
     # failed generations ('' = keep retrying RCCL): membership keeps being

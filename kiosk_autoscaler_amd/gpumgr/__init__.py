@@ -125,7 +125,8 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
                          pool_idle_release_s=settings.POOL_IDLE_RELEASE_S,
                          fence_fallback=settings.FENCE_FALLBACK,
                          fence_fallback_after=settings.FENCE_FALLBACK_AFTER,
-                         fence_init_timeout=settings.FENCE_INIT_TIMEOUT)
+                         fence_init_timeout=settings.FENCE_INIT_TIMEOUT,
+                         zygote=settings.WORKER_ZYGOTE)
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

@@ -285,7 +285,8 @@ class GpuManager(object):
                  worker_timeout=0.0, start_timeout=0.0, recycle=True,
                  fence_comm='node', pool_idle_release_s=0.0,
                  fence_fallback='shm', fence_fallback_after=2,
-                 fence_init_timeout=12.0, fence_transport=None):
+                 fence_init_timeout=12.0, fence_transport=None,
+                 zygote=False):
         self.slots = list(slots)
         self.redis = redis_client
         self.pool_size = max(0, int(pool_size))
@@ -318,6 +319,10 @@ class GpuManager(object):
         self.instance = '%x' % ((os.getpid() << 20 ^ time.time_ns() >> 10)
                                 & 0xfffff)
         self._stopping = False
+        # worker zygote (worker/zygote.py): spawns fork from a process that
+        # imported the worker (and torch, for a plug-in) without the GPU
+        self.zygote_enabled = bool(zygote)
+        self.zygote = None
         self.mapping_fixes = 0   # slots remapped after a PCI check
         self.history = []   # exited workers, for accounting
         # persistent node-wide communicator: needs one long-lived process
@@ -503,6 +508,7 @@ class GpuManager(object):
     def start(self):
         if self._thread is None:
             with self.lock:
+                self._start_zygote()
                 self._refill_pool()
             self._thread = threading.Thread(target=self._loop,
                                             name='gpumgr', daemon=True)
@@ -557,6 +563,9 @@ class GpuManager(object):
             self._thread = None
         with self.lock:
             self._reap_all()
+            if self.zygote is not None:
+                self.zygote.close()
+                self.zygote = None
 
     # ------------------------------------------------------------------
     # event loop body
@@ -599,25 +608,18 @@ class GpuManager(object):
     # ------------------------------------------------------------------
     # process management
     # ------------------------------------------------------------------
-    def _spawn(self, template, role, assign=None, slot=None):
-        cmd_r, cmd_w = os.pipe()
-        ev_r, ev_w = os.pipe()
+    @staticmethod
+    def _interpreter(template):
         argv = [template.python]
         if _bare_worker(template):
             # the torch-free HIP worker needs only this tree (on PYTHONPATH
             # below) and the stdlib: skipping site-packages' .pth
             # processing takes ~20 ms off every spawn
             argv.append('-S')
-        argv += ['-m', template.module,
-                 '--cmd-fd', str(cmd_r), '--ev-fd', str(ev_w),
-                 '--backend', template.backend]
-        if assign is not None:
-            argv += ['--assign', json.dumps(assign)]
-        elif slot is not None:
-            argv += ['--pin', json.dumps({
-                'gpu': slot.visible_id, 'slot': slot.index, 'cpus': slot.cpus,
-                'preinit': self.pool_mode,
-                'node_fence': self.node is not None})]
+        return argv
+
+    @staticmethod
+    def _environment(template):
         env = dict(os.environ)
         env.update({k: str(v) for k, v in template.env.items()})
         env['PYTHONUNBUFFERED'] = '1'
@@ -626,16 +628,87 @@ class GpuManager(object):
         env['PYTHONPATH'] = os.pathsep.join(
             [root] + [p for p in env.get('PYTHONPATH', '').split(os.pathsep)
                       if p])
+        return env
+
+    # env that decides what a worker imports: a zygote serves only the
+    # templates it preloaded for
+    _IMPORT_ENV = ('WORKER_ENGINE', 'WORKER_IMPORT_TORCH', 'KIOSK_NATIVE',
+                   'WORKER_PYTHON_SITE')
+
+    def _start_zygote(self):
+        tpl = self.pool_template
+        if not self.zygote_enabled or tpl is None or self.zygote is not None \
+                or tpl.module != 'kiosk_autoscaler_amd.worker.main':
+            return
+        from ..worker import zygote
+        if not zygote.become_subreaper():
+            logger.warning('PR_SET_CHILD_SUBREAPER refused: no zygote.')
+            return
+        argv = self._interpreter(tpl) + [
+            '-m', 'kiosk_autoscaler_amd.worker.zygote', '--backend',
+            tpl.backend]
+        self.zygote = zygote.ZygoteClient(argv, self._environment(tpl))
+        self.events.emit('zygote_spawn', pid=self.zygote.pid)
+
+    def _zygote_for(self, template):
+        z = self.zygote
+        tpl = self.pool_template
+        if z is None or tpl is None:
+            return None
+        if not z.alive():
+            logger.warning('Worker zygote %d exited; spawning directly.',
+                           z.pid)
+            z.close()
+            self.zygote = None
+            return None
+        if not z.poll_ready():
+            return None      # still importing: this spawn takes the slow path
+        if (template.module != tpl.module or
+                template.backend != tpl.backend or
+                _bare_worker(template) != _bare_worker(tpl) or
+                any(template.env.get(k) != tpl.env.get(k)
+                    for k in self._IMPORT_ENV)):
+            return None
+        return z
+
+    def _spawn(self, template, role, assign=None, slot=None):
+        cmd_r, cmd_w = os.pipe()
+        ev_r, ev_w = os.pipe()
+        args = ['--cmd-fd', str(cmd_r), '--ev-fd', str(ev_w),
+                '--backend', template.backend]
+        if assign is not None:
+            args += ['--assign', json.dumps(assign)]
+        elif slot is not None:
+            args += ['--pin', json.dumps({
+                'gpu': slot.visible_id, 'slot': slot.index, 'cpus': slot.cpus,
+                'preinit': self.pool_mode,
+                'node_fence': self.node is not None})]
+        env = self._environment(template)
+        popen = None
+        via = 'exec'
         try:
-            popen = subprocess.Popen(argv, env=env, pass_fds=(cmd_r, ev_w),
-                                     close_fds=True, start_new_session=True)
+            zygote = self._zygote_for(template)
+            if zygote is not None:
+                try:
+                    popen = zygote.fork(args, env, (cmd_r, ev_w))
+                    via = 'zygote'
+                except (OSError, ValueError) as err:
+                    logger.warning('zygote fork failed (%s); spawning '
+                                   'directly.', err)
+            if popen is None:
+                argv = self._interpreter(template) + ['-m', template.module]
+                popen = subprocess.Popen(argv + args, env=env,
+                                         pass_fds=(cmd_r, ev_w),
+                                         close_fds=True,
+                                         start_new_session=True)
         finally:
             os.close(cmd_r)
             os.close(ev_w)
         proc = _Process(popen, _Pipe(cmd_w, ev_r), role)
         proc.slot = slot.index if slot is not None else None
+        proc.via = via
         self.events.emit('process_spawn', role=role, pid=popen.pid,
-                         slot=proc.slot)
+                         slot=proc.slot, via=via)
         return proc
 
     def _refill_pool(self):

@@ -87,6 +87,24 @@ def _preimport(backend):
 _DEVICE_OPEN = {}
 
 
+def _warm_torch():
+    """A PyTorch plug-in's device start-up, paid before the assignment
+    needs it: torch's lazy CUDA init (its own context bookkeeping, caching
+    allocator) and one small bf16 GEMM, which creates the hipBLASLt handle
+    and loads a GEMM code object.  Only in a process that imported torch
+    (``WORKER_ENGINE``); returns stage stamps."""
+    if 'torch' not in sys.modules:
+        return {}
+    import torch
+    if not torch.cuda.is_available():
+        return {}
+    t0 = time.monotonic_ns()
+    a = torch.ones(256, 256, device='cuda', dtype=torch.bfloat16)
+    float((a @ a).float().sum())
+    torch.cuda.synchronize()
+    return {'torch_warm_start': t0, 'torch_warm_done': time.monotonic_ns()}
+
+
 def _open_device_async():
     from ..ops import native
     mod = native.load()
@@ -94,6 +112,7 @@ def _open_device_async():
     def run():
         try:
             _DEVICE_OPEN['stages'] = dict(mod.preinit_device(0))
+            _DEVICE_OPEN['stages'].update(_warm_torch())
         except Exception as err:  # pylint: disable=broad-except
             # the engine's own init reports the failure
             _DEVICE_OPEN['error'] = str(err)
@@ -311,6 +330,8 @@ def main(argv=None):
         try:
             mod = native.load()
             preinit = dict(mod.preinit_device(0))
+            # a PyTorch plug-in: torch's CUDA init + hipBLASLt handle too
+            preinit.update(_warm_torch())
             if not node and os.environ.get('FENCE', 'auto') in ('auto',
                                                                  'rccl'):
                 # RCCL's one-time init costs seconds: pay it while idle (with

@@ -1,0 +1,313 @@
+"""Worker zygote: spawn workers by ``fork()`` from a process that already
+imported everything a worker needs but never touched the GPU.
+
+A worker started from scratch pays the interpreter start and its imports
+before it can open the device: ~0.1 s for the torch-free HIP worker, but
+~1.5-2.2 s for a PyTorch plug-in engine (``import torch``), the dominant cost
+of its cold spawn (1.89 s).  The zygote pays them once, at
+manager start, and holds **no GPU** (no HIP call has been made: HIP reads
+``HIP_VISIBLE_DEVICES`` at its lazy init, so each forked worker still pins
+its own GPU).  A spawn is then ``fork()`` + the GPU work only.
+
+Protocol (manager <-> zygote, one ``AF_UNIX`` ``SOCK_SEQPACKET`` pair):
+
+* manager -> zygote: ``{"argv": [...], "env": {...}}`` with the worker's two
+  pipe ends (command read end, event write end) attached as ``SCM_RIGHTS``;
+* the zygote forks twice: the intermediate child exits at once, so the
+  worker is re-parented to the manager (``PR_SET_CHILD_SUBREAPER``) and the
+  manager reaps it like any child (:class:`ForkedChild`);
+* zygote -> manager: ``{"pid": <worker pid>}`` (or ``{"error": ...}``).
+
+The worker process then runs :func:`kiosk_autoscaler_amd.worker.main.main`
+with the same argv a ``subprocess`` spawn would have used.
+"""
+import json
+import os
+import signal
+import socket
+import sys
+import time
+
+PR_SET_CHILD_SUBREAPER = 36
+PR_SET_PDEATHSIG = 1
+MAX_MSG = 1 << 20
+
+
+def become_subreaper():
+    """Orphaned descendants (the zygote's workers) re-parent to this
+    process, so it can ``waitpid`` them.  False if the kernel refuses."""
+    try:
+        import ctypes
+        libc = ctypes.CDLL(None, use_errno=True)
+        return libc.prctl(PR_SET_CHILD_SUBREAPER, 1, 0, 0, 0) == 0
+    except (OSError, AttributeError):
+        return False
+
+
+class ForkedChild(object):
+    """``subprocess.Popen``-shaped handle of a worker the zygote forked and
+    this (subreaper) process adopted."""
+
+    def __init__(self, pid):
+        self.pid = pid
+        self.returncode = None
+
+    def poll(self):
+        if self.returncode is not None:
+            return self.returncode
+        try:
+            pid, status = os.waitpid(self.pid, os.WNOHANG)
+        except ChildProcessError:
+            # not (or no longer) our child: alive means still running
+            try:
+                os.kill(self.pid, 0)
+                return None
+            except ProcessLookupError:
+                self.returncode = 255
+                return self.returncode
+        if pid == 0:
+            return None
+        self.returncode = os.waitstatus_to_exitcode(status)
+        return self.returncode
+
+    def wait(self, timeout=None):
+        deadline = None if timeout is None else time.monotonic() + timeout
+        while self.poll() is None:
+            if deadline is not None and time.monotonic() > deadline:
+                import subprocess
+                raise subprocess.TimeoutExpired(['worker', str(self.pid)],
+                                                timeout)
+            time.sleep(0.005)
+        return self.returncode
+
+    def send_signal(self, sig):
+        if self.returncode is None:
+            try:
+                os.kill(self.pid, sig)
+            except ProcessLookupError:
+                pass
+
+    def kill(self):
+        self.send_signal(signal.SIGKILL)
+
+    def terminate(self):
+        self.send_signal(signal.SIGTERM)
+
+
+class ZygoteClient(object):
+    """Manager side: start the zygote, fork workers from it."""
+
+    def __init__(self, argv, env, timeout=10.0):
+        import subprocess
+        self.sock, child = socket.socketpair(socket.AF_UNIX,
+                                             socket.SOCK_SEQPACKET)
+        env = dict(env)
+        env['KIOSK_ZYGOTE_FD'] = str(child.fileno())
+        self.popen = subprocess.Popen(
+            list(argv) + ['--zygote-fd', str(child.fileno())], env=env,
+            pass_fds=(child.fileno(),), close_fds=True,
+            start_new_session=True)
+        child.close()
+        self.timeout = float(timeout)
+        self.ready = False
+        self.preload_s = None
+        self.forks = 0
+
+    @property
+    def pid(self):
+        return self.popen.pid
+
+    def alive(self):
+        return self.popen.poll() is None
+
+    def wait_ready(self, timeout=None):
+        """Block until the zygote finished its imports (True) or died."""
+        if self.ready:
+            return True
+        self.sock.settimeout(timeout if timeout is not None else self.timeout)
+        try:
+            data = self.sock.recv(MAX_MSG)
+        except (socket.timeout, OSError):
+            return False
+        if not data:
+            return False
+        message = json.loads(data)
+        self.ready = message.get('ready', False)
+        self.preload_s = message.get('preload_s')
+        return self.ready
+
+    def poll_ready(self):
+        """Non-blocking :meth:`wait_ready`."""
+        if self.ready:
+            return True
+        self.sock.setblocking(False)
+        try:
+            data = self.sock.recv(MAX_MSG)
+        except BlockingIOError:
+            return False
+        except OSError:
+            return False
+        finally:
+            self.sock.setblocking(True)
+        if not data:
+            return False
+        message = json.loads(data)
+        self.ready = message.get('ready', False)
+        self.preload_s = message.get('preload_s')
+        return self.ready
+
+    def fork(self, argv, env, fds):
+        """A worker process running ``worker.main.main(argv)`` with
+        ``env``; ``fds`` (its pipe ends) are passed, not inherited.
+        Returns a :class:`ForkedChild`."""
+        if not self.ready and not self.wait_ready():
+            raise OSError('zygote is not ready')
+        payload = json.dumps({'argv': list(argv), 'env': dict(env)}).encode()
+        self.sock.settimeout(self.timeout)
+        socket.send_fds(self.sock, [payload], list(fds))
+        reply = json.loads(self.sock.recv(MAX_MSG))
+        if 'pid' not in reply:
+            raise OSError('zygote fork failed: %s' % reply.get('error'))
+        self.forks += 1
+        return ForkedChild(int(reply['pid']))
+
+    def close(self):
+        try:
+            self.sock.close()
+        except OSError:
+            pass
+        if self.popen.poll() is None:
+            self.popen.terminate()
+            try:
+                self.popen.wait(timeout=5)
+            except Exception:  # pylint: disable=broad-except
+                self.popen.kill()
+
+
+# ---------------------------------------------------------------------------
+# zygote process
+# ---------------------------------------------------------------------------
+def _preload(backend):
+    """Everything a worker imports, without a single HIP call."""
+    from . import main as worker_main
+    worker_main._preload(backend)           # native module (+ torch)
+    worker_main._preimport(backend)         # runtime, events, models, plug-in
+    from ..parallel import nodefence  # noqa: F401
+    from ..redisq import RedisClient  # noqa: F401
+    import logging  # noqa: F401
+
+
+def _child(request, fds, sock):
+    """In the grandchild: become the worker described by ``request``."""
+    sock.close()
+    os.setsid()
+    cmd_r, ev_w = fds
+    keep = {0, 1, 2, cmd_r, ev_w}
+    for fd in range(3, 1024):
+        if fd not in keep:
+            try:
+                os.close(fd)
+            except OSError:
+                pass
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGCHLD):
+        signal.signal(sig, signal.SIG_DFL)
+    os.environ.clear()
+    os.environ.update(request['env'])
+    argv = list(request['argv'])
+    # the fds were renumbered by SCM_RIGHTS: point the worker at them
+    for flag, fd in (('--cmd-fd', cmd_r), ('--ev-fd', ev_w)):
+        if flag in argv:
+            argv[argv.index(flag) + 1] = str(fd)
+    sys.argv = ['kiosk-worker'] + argv
+    from . import main as worker_main
+    try:
+        code = worker_main.main(argv)
+    except SystemExit as stop:
+        code = stop.code if isinstance(stop.code, int) else 1
+    except BaseException:  # pylint: disable=broad-except
+        import traceback
+        traceback.print_exc()
+        code = 1
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(code or 0)
+
+
+def _serve(sock):
+    while True:
+        try:
+            payload, fds, _flags, _addr = socket.recv_fds(sock, MAX_MSG, 4)
+        except OSError:
+            return 0
+        if not payload:
+            return 0            # the manager went away
+        try:
+            request = json.loads(payload)
+            if len(fds) != 2:
+                raise ValueError('expected 2 fds, got %d' % len(fds))
+        except ValueError as err:
+            for fd in fds:
+                os.close(fd)
+            sock.send(json.dumps({'error': str(err)}).encode())
+            continue
+        r, w = os.pipe()
+        mid = os.fork()
+        if mid == 0:
+            os.close(r)
+            intermediate = os.getpid()
+            pid = os.fork()
+            if pid == 0:
+                os.close(w)
+                # wait for the intermediate to exit: the worker is then the
+                # manager's (subreaper) child and its death signal binds there
+                deadline = time.monotonic() + 5.0
+                while os.getppid() == intermediate and \
+                        time.monotonic() < deadline:
+                    time.sleep(0.0002)
+                _child(request, fds, sock)
+            os.write(w, str(pid).encode())
+            os._exit(0)
+        os.close(w)
+        for fd in fds:
+            os.close(fd)
+        data = b''
+        while True:
+            chunk = os.read(r, 64)
+            if not chunk:
+                break
+            data += chunk
+        os.close(r)
+        os.waitpid(mid, 0)
+        if data:
+            sock.send(json.dumps({'pid': int(data)}).encode())
+        else:
+            sock.send(json.dumps({'error': 'fork failed'}).encode())
+
+
+def main(argv=None):
+    import argparse
+    parser = argparse.ArgumentParser(description=__doc__)
+    parser.add_argument('--zygote-fd', type=int, required=True)
+    parser.add_argument('--backend', default='cpu')
+    args = parser.parse_args(argv)
+    sock = socket.socket(fileno=args.zygote_fd)
+    t0 = time.monotonic()
+    try:
+        _preload(args.backend)
+    except Exception as err:  # pylint: disable=broad-except
+        sock.send(json.dumps({'ready': False, 'error': str(err)}).encode())
+        return 3
+    # a worker must never outlive the manager, nor the zygote
+    try:
+        import ctypes
+        ctypes.CDLL(None).prctl(PR_SET_PDEATHSIG, int(signal.SIGTERM), 0, 0, 0)
+    except (OSError, AttributeError):
+        pass
+    signal.signal(signal.SIGCHLD, signal.SIG_DFL)
+    sock.send(json.dumps({'ready': True,
+                          'preload_s': time.monotonic() - t0}).encode())
+    return _serve(sock)
+
+
+if __name__ == '__main__':
+    sys.exit(main())

@@ -304,3 +304,45 @@ def test_scale_up_during_drain_cancels_it(stack):
     wait_for(lambda: client.hget('predict:job0', 'status') == 'done')
     assert client.hget('predict:job0', 'worker') == wid   # never left
     assert not any(e['ev'] == 'worker_exit' for e in events.records)
+
+
+def test_zygote_cold_spawn_reaped_like_a_child(stack):
+    """WORKER_ZYGOTE: with no warm pool every scale-up is a cold spawn; it
+    is forked from the pre-imported zygote (no interpreter start, no
+    imports), re-parented to the manager (subreaper), served keys, and its
+    exit -- clean or SIGKILL -- is reaped and handled like any child's."""
+    import signal
+    s, client, manager, scaler, events = stack(WARM_POOL='0')
+    assert manager.zygote is not None
+    wait_for(lambda: manager.zygote.poll_ready(), timeout=60)
+    enqueue(client, 2)
+    assert tick(scaler, s) == 1
+    wait_for(lambda: all(client.hget('predict:job%d' % i, 'status') == 'done'
+                         for i in range(2)), timeout=30)
+    spawns = [e for e in events.records if e['ev'] == 'process_spawn']
+    assert spawns and spawns[-1]['via'] == 'zygote'
+    worker = manager.status()['resources'][0]['workers'][0]
+    assert worker['pid'] == spawns[-1]['pid']
+    assert os.getppid() != worker['pid']
+    assert tick(scaler, s) == 0
+    wait_for(lambda: any(e['ev'] == 'worker_exit' and
+                         e['worker'] == worker['id'] for e in events.records),
+             timeout=30)
+    exit_ev = [e for e in events.records if e['ev'] == 'worker_exit' and
+               e['worker'] == worker['id']][0]
+    assert exit_ev['code'] == 0
+    # a forked worker killed mid-key: reaped (-9), its item requeued
+    client.hset('predict:slow', mapping={'status': 'new', 'rows': 8,
+                                         'service_ms': 3000})
+    client.lpush('predict', 'predict:slow')
+    assert tick(scaler, s) == 1
+    victim = wait_for(lambda: [w for w in manager.status()['resources'][0]
+                               ['workers'] if w['busy']], timeout=30)[0]
+    os.kill(victim['pid'], signal.SIGKILL)
+    wait_for(lambda: any(e['ev'] == 'worker_exit' and
+                         e['worker'] == victim['id'] and e['code'] == -9
+                         for e in events.records), timeout=30)
+    wait_for(lambda: any(e['ev'] == 'requeue' for e in events.records),
+             timeout=30)
+    wait_for(lambda: client.hget('predict:slow', 'status') == 'done',
+             timeout=60)
