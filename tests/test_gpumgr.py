@@ -524,3 +524,64 @@ def test_pci_mapping_verified_and_remapped(monkeypatch):
     assert 1 not in manager.standbys and proc1 in manager.retiring
     assert Proc.sent[-1] == {'cmd': 'exit'}
     assert isinstance(manager, gpumgr.GpuManager) and _Process
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('engine', ['native', 'torch'])
+def test_gpu_zygote_cold_spawn(resp_server, engine):
+    """MI355X, no warm pool: the worker is forked from the zygote (which
+    imported the worker -- and torch for the plug-in -- without touching the
+    GPU); the child pins its GPU, opens it, builds the engine and serves.
+    The READY time is printed (the PyTorch plug-in's cold spawn without
+    the zygote was 1.89 s)."""
+    import time
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict', 'RESOURCE_NAME': 'zyg', 'MAX_PODS': '1',
+           'WORKER_BACKEND': 'hip', 'WARM_POOL': '0', 'FENCE': 'none',
+           'REDIS_INTERVAL': '0', 'GPU_IDS': '0', 'MODEL_DIM': '1024',
+           'MODEL_HIDDEN': '4096', 'MODEL_LAYERS': '2', 'ROWS_PER_KEY': '256'}
+    spec = 'kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine'
+    if engine == 'torch':
+        os.environ['WORKER_ENGINE'] = spec
+    events = EventLog(source='test')
+    events.keep = True
+    try:
+        s = Settings(Config(environ=env, use_files=False))
+        client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                             decode_responses=True)
+        manager = gpumgr.build_manager(s, redis_client=client,
+                                       events=events).start()
+    finally:
+        os.environ.pop('WORKER_ENGINE', None)
+    try:
+        deadline = time.monotonic() + 120
+        while not manager.zygote.poll_ready():
+            assert time.monotonic() < deadline and manager.zygote.alive()
+            time.sleep(0.05)
+        for cycle in range(2):
+            item = 'predict:z%d' % cycle
+            client.hset(item, mapping={'status': 'new', 'rows': 256})
+            client.lpush('predict', item)
+            manager.patch_namespaced_deployment('zyg', 'default',
+                                                {'spec': {'replicas': 1}})
+            deadline = time.monotonic() + 120
+            while client.hget(item, 'status') != 'done':
+                assert time.monotonic() < deadline, client.hgetall(item)
+                time.sleep(0.05)
+            manager.patch_namespaced_deployment('zyg', 'default',
+                                                {'spec': {'replicas': 0}})
+            deadline = time.monotonic() + 60
+            while manager.status()['resources'][0]['workers']:
+                assert time.monotonic() < deadline
+                time.sleep(0.05)
+    finally:
+        manager.stop(timeout=20)
+    spawns = [e for e in events.records if e['ev'] == 'process_spawn']
+    ups = [e for e in events.records if e['ev'] == 'worker_up']
+    assert len(ups) == 2 and all(e['via'] == 'zygote' for e in spawns), spawns
+    print('zygote cold spawn (%s): assign -> READY %s s' % (
+        engine, [round(e['ready_s'], 3) for e in ups]))
+    assert all(e['ready_s'] < 10.0 for e in ups)
