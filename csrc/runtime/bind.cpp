@@ -154,6 +154,8 @@ PYBIND11_MODULE(_kiosk_hip, m) {
         return d;
       },
       py::arg("device") = 0);
+  m.def("release_kept_stream", &kiosk::release_kept_stream,
+        py::call_guard<py::gil_scoped_release>());
   m.def(
       "preload_modules",
       [](int device) {

@@ -47,17 +47,45 @@ hipStream_t take_kept_stream(int device) {
   return s;
 }
 
+// Destroys a kept stream on the device it was created on (a process may
+// preinit more than one device; the current device is restored).
+void destroy_on_device(hipStream_t s, int device) {
+  if (!s) return;
+  int current = -1;
+  (void)hipGetDevice(&current);
+  if (device >= 0 && device != current) (void)hipSetDevice(device);
+  (void)hipStreamDestroy(s);
+  if (device >= 0 && device != current && current >= 0) {
+    (void)hipSetDevice(current);
+  }
+}
+
 void keep_stream(hipStream_t s, int device) {
   hipStream_t old = nullptr;
+  int old_device = -1;
   {
     std::lock_guard<std::mutex> lock(g_kept_mu);
     old = g_kept_stream;
+    old_device = g_kept_device;
     g_kept_stream = s;
     g_kept_device = device;
   }
-  if (old) hipStreamDestroy(old);
+  destroy_on_device(old, old_device);
 }
 }  // namespace
+
+void release_kept_stream() {
+  hipStream_t s = nullptr;
+  int device = -1;
+  {
+    std::lock_guard<std::mutex> lock(g_kept_mu);
+    s = g_kept_stream;
+    device = g_kept_device;
+    g_kept_stream = nullptr;
+    g_kept_device = -1;
+  }
+  destroy_on_device(s, device);
+}
 
 std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   TraceRange range("kiosk.preinit");

@@ -20,6 +20,10 @@ long long monotonic_ns();
 // once on a tiny scratch buffer, then free it.  Leaves no HBM allocated
 // and nothing running; the later Engine ctor then skips ~150 ms of
 // runtime init + code-object loading.  Returns stage timestamps.
+// Destroys the stream preinit_device kept for the next Engine (if no Engine
+// took it): the standby's exit path, so teardown does not depend on process
+// exit.
+void release_kept_stream();
 std::vector<std::pair<std::string, long long>> preinit_device(int device);
 // `context` standby: HIP context + every kernel's code object, no launch (so
 // no hardware queue and no HBM beyond the code objects).

@@ -396,6 +396,12 @@ def main(argv=None):
                'cpus': assignment.get('cpus')}
         assignment = None
     _join_device_open()     # never exit under a running device open
+    if backend == 'hip':
+        try:
+            from ..ops import native
+            native.load().release_kept_stream()
+        except Exception:  # pylint: disable=broad-except
+            pass
     # The engine (HBM, streams, graphs) and the fence are released by now;
     # skip interpreter teardown (torch/HIP static destructors take ~0.5 s)
     # so the GPU slot frees promptly.
