@@ -155,6 +155,10 @@ EXTRA_DEFAULTS = (
     # s with no demand after which the standbys exit (0 = keep them): the
     # node then holds no GPU, the next scale-up is a cold spawn (~0.13 s)
     ('POOL_IDLE_RELEASE_S', float, 0.0),
+    # s a recycled standby keeps its engine (weights, arena, graphs; ~1.2
+    # GiB of the idle GPU's 2.6) without an assignment; then it frees it and
+    # keeps context, queue and node communicator (0 = keep forever)
+    ('ENGINE_IDLE_RELEASE_S', float, 60.0),
     ('WARM_START', bool, True),             # run the N1 warm-start kernel
     # auto (rccl with device standbys, shm otherwise; store on CPU) | rccl
     # | shm | store | gloo | none

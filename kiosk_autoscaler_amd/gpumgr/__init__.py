@@ -53,6 +53,7 @@ def worker_env(settings, keys_per_pod=None):
         'ROWS_PER_KEY': settings.ROWS_PER_KEY,
         'WARM_START': int(settings.WARM_START), 'FENCE': settings.FENCE,
         'FENCE_INIT_TIMEOUT': settings.FENCE_INIT_TIMEOUT,
+        'ENGINE_IDLE_RELEASE_S': settings.ENGINE_IDLE_RELEASE_S,
         'RESOURCE_NAMESPACE': settings.RESOURCE_NAMESPACE,
         'RESOURCE_NAME': settings.RESOURCE_NAME,
     }
@@ -69,7 +70,7 @@ def worker_env(settings, keys_per_pod=None):
                         'WORKER_IMPORT_TORCH', 'WORKER_ENGINE',
                         'WORKER_PYTHON_SITE', 'KIOSK_SHM_DIR',
                         'KIOSK_NATIVE', 'FAKE_RCCL_DIR', 'FAKE_RCCL_MODE',
-                        'ENGINE_IDLE_RELEASE_S', 'WORKER_MAX_RECYCLES'):
+                        'WORKER_MAX_RECYCLES'):
         if passthrough in os.environ:
             env[passthrough] = os.environ[passthrough]
     return env

@@ -168,7 +168,7 @@ class _Process(object):
 class Worker(object):
     __slots__ = ('id', 'resource', 'slot', 'proc', 'state', 'busy',
                  't_assigned', 't_ready', 't_exit', 'exit_code', 'from_pool',
-                 'stages', 'last_beat', 'kill_reason')
+                 'stages', 'last_beat', 'kill_reason', 'fenced_out')
 
     def __init__(self, wid, resource, slot, proc, from_pool):
         self.id = wid
@@ -185,13 +185,15 @@ class Worker(object):
         self.stages = {}
         self.last_beat = time.monotonic()   # last sign of progress
         self.kill_reason = None
+        self.fenced_out = False     # an agreed membership excluded it
 
     def summary(self):
         return {'id': self.id, 'gpu': self.slot.index, 'pid': self.proc.pid,
                 'state': self.state, 'busy': self.busy,
                 'from_pool': self.from_pool, 't_assigned': self.t_assigned,
                 't_ready': self.t_ready, 'stages': dict(self.stages),
-                'exit_code': self.exit_code, 'killed': self.kill_reason}
+                'exit_code': self.exit_code, 'killed': self.kill_reason,
+                'fenced_out': self.fenced_out}
 
 
 class Resource(object):
@@ -1059,6 +1061,10 @@ class GpuManager(object):
                 worker.last_beat = time.monotonic()
             elif kind == 'fenced':
                 self._on_fenced(worker.resource, message)
+            elif kind in ('fenced_out', 'fenced_in'):
+                worker.fenced_out = kind == 'fenced_out'
+                self.events.emit('worker_' + kind, worker=worker.id,
+                                 seq=message.get('seq'))
             elif kind == 'recycled':
                 self._on_recycled(worker, message)
             elif kind in ('standby', 'device'):

@@ -1010,3 +1010,37 @@ def test_forced_recycle_exit_is_shrunk_not_broken(resp_server, tmp_path,
     done = [e for e in events.records if e['ev'] == 'fence_done']
     assert len(done) >= 6 and all(e['transport'] == TRANSPORTS[transport][0]
                                   for e in done)
+
+
+@pytest.mark.slow
+def test_deep_idle_builds_one_generation_per_wake(resp_server, tmp_path):
+    """POOL_IDLE_RELEASE_S: the parked pool holds no process, so each wake
+    (a cold spawn forked from the zygote + the pool refill) needs a new
+    communicator -- exactly one per wake, not one per process that joins
+    (12 generations in 10 cycles)."""
+    s, client, events, manager, scaler = _node_stack(
+        resp_server, 'shm', tmp_path, MAX_PODS='2', WARM_POOL='2',
+        POOL_IDLE_RELEASE_S='0.5')
+    wakes = 3
+    try:
+        wait_for(lambda: manager.node.ready and manager.node.full,
+                 timeout=60)
+        for _ in range(wakes):
+            wait_for(lambda: manager.pool_parked, timeout=30)
+            manager.patch_namespaced_deployment('worker', 'default',
+                                                {'spec': {'replicas': 1}})
+            wait_for(lambda: _converged(manager, client) and
+                     len(_ready_ids(manager)) == 1, timeout=60)
+            manager.patch_namespaced_deployment('worker', 'default',
+                                                {'spec': {'replicas': 0}})
+            wait_for(lambda: _active(client)['members'] == [], timeout=30)
+    finally:
+        manager.stop(timeout=15)
+    kinds = [e['ev'] for e in events.records]
+    parks = kinds.count('pool_parked')
+    inits = [e for e in events.records if e['ev'] == 'node_comm_ready' and
+             e.get('mode') == 'init']
+    # boot + one per wake (the last park may or may not have happened)
+    assert len(inits) == wakes + 1, (len(inits), parks)
+    assert not any(e['failed'] for e in events.records
+                   if e['ev'] == 'node_comm_break')
