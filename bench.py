@@ -135,10 +135,12 @@ class Services(object):
         self.bdfs = bdfs
         if bdfs:
             # min of a few reads: memory a previous tenant of the GPU left
-            # may still be draining (one box read 231 GB used here)
+            # may still be draining (one box read 231 GB used here).  Every
+            # device is read: the manager may remap a slot's PCI address
+            # once its process reports what HIP sees (kiosk:slots)
             reads = []
             for _ in range(5):
-                reads.append(gpu_util.vram_snapshot(bdfs) or {})
+                reads.append(gpu_util.vram_snapshot() or {})
                 time.sleep(0.2)
             self.vram0 = {b: min(r[b] for r in reads if b in r)
                           for b in reads[-1]} or None
@@ -156,6 +158,15 @@ class Services(object):
                                  decode_responses=True)
         wait_for(lambda: self._ping(), 20, what='redis')
         self.start_scaler(self.n, pool=self.n, timeout=args.pool_timeout)
+        if bdfs:
+            verified = verified_bdfs(self.redis, self.n)
+            if verified and sorted(verified) != sorted(bdfs):
+                log('GPU mapping: the manager verified %s (KFD order gave '
+                    '%s)' % (verified, bdfs))
+            self.bdfs = bdfs = verified or bdfs
+            if self.vram0:
+                self.vram0 = {b: v for b, v in self.vram0.items()
+                              if b in set(bdfs)} or None
         if bdfs and self.vram0:
             reads = []
             for _ in range(3):
@@ -573,7 +584,8 @@ def main():
                 run_cycle(svc, gen, args, 0.5 * args.interval, 0.0,
                           'warmup %d' % w, budget)
                 warmups_done[0] += 1
-        sampler = start_util_sampler(args.gpus) if rank == 0 else None
+        sampler = (start_util_sampler(args.gpus, svc.bdfs) if rank == 0
+                   else None)
         barrier()
         sync()
         t0 = time.perf_counter()
@@ -792,11 +804,22 @@ def managed_bdfs(n_gpus):
     return None
 
 
-def start_util_sampler(n_gpus):
+def verified_bdfs(redis, n_gpus):
+    """The PCI addresses the manager verified through HIP for its slots
+    (``kiosk:slots``), or None until every slot is verified."""
+    try:
+        slots = json.loads(redis.get('kiosk:slots') or '[]')
+    except (ValueError, TypeError):
+        return None
+    found = [s['pci'] for s in slots if s.get('verified') and s.get('pci')]
+    return found if len(found) == n_gpus else None
+
+
+def start_util_sampler(n_gpus, bdfs=None):
     """amdsmi gfx-activity sampling over the managed GPUs (None on CPU)."""
     if os.environ.get('KIOSK_AMDSMI', '1') == '0':
         return None
-    sampler = gpu_util.UtilSampler(0.1, managed_bdfs(n_gpus))
+    sampler = gpu_util.UtilSampler(0.1, bdfs or managed_bdfs(n_gpus))
     sampler.start()
     return sampler
 

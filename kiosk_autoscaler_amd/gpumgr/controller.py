@@ -61,6 +61,7 @@ STARTING, READY, DRAINING, EXITED = 'starting', 'ready', 'draining', 'exited'
 ACTIVE_KEY = 'kiosk:active:{ns}:{name}'
 WORKER_KEY = 'kiosk:worker:{id}'
 POOL_KEY = 'kiosk:pool'
+SLOTS_KEY = 'kiosk:slots'
 STATE_KEY = 'kiosk:gpumgr:{ns}:{kind}:{name}'
 
 
@@ -785,6 +786,19 @@ class GpuManager(object):
         self._publish_pool()
         return proc
 
+    def _publish_slots(self):
+        """The slot table as verified so far (``kiosk:slots``): the bench
+        samples amdsmi on these PCI addresses, not on KFD order."""
+        if self.redis is None:
+            return
+        try:
+            self.redis.set(SLOTS_KEY, json.dumps([
+                {'index': s.index, 'visible': s.visible_id, 'pci': s.pci,
+                 'verified': bool(getattr(s, 'pci_verified', False)),
+                 'kind': s.kind} for s in self.slots]))
+        except Exception:  # pylint: disable=broad-except
+            pass
+
     def _publish_pool(self):
         if self.redis is None:
             return
@@ -851,9 +865,10 @@ class GpuManager(object):
         proc.pci = actual
         if expected == actual:
             if not getattr(slot, 'pci_verified', False):
+                slot.pci_verified = True
                 self.events.emit('gpu_mapping', slot=index, pci=actual,
                                  visible=slot.visible_id, verified=True)
-            slot.pci_verified = True
+                self._publish_slots()
             return True
         slot.pci = actual
         slot.numa_node, slot.cpus = local_cpus(actual)
@@ -865,6 +880,7 @@ class GpuManager(object):
         logger.error('GPU slot %d (HIP_VISIBLE_DEVICES=%s) is %s, not %s as '
                      'KFD order suggested: remapped (NUMA node %s).', index,
                      slot.visible_id, actual, expected, slot.numa_node)
+        self._publish_slots()
         if self.standbys.get(index) is proc and expected is not None:
             del self.standbys[index]
             proc.pipe.send({'cmd': 'exit'})
