@@ -347,3 +347,35 @@ def test_gpu_bench_contract(tmp_path):
     assert boot is None or 0 < boot < 8192, boot
     assert line['idle_node_hbm_mib'] is None or \
         line['idle_node_hbm_mib'] < 16384
+
+
+def test_pmc_summary_mfma_busy_over_active(tmp_path):
+    """tools/pmc_summary.py: SQ_VALU_MFMA_BUSY_CYCLES is SIMD-busy cycles
+    summed over the 1024 SIMDs; GRBM_GUI_ACTIVE sums 32 shader engines.
+    A kernel whose every SIMD is MFMA-busy for all its cycles reads 1.0,
+    and the kernel-trace duration gives the shader clock."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location(
+        'pmc_summary', os.path.join(root, 'tools', 'pmc_summary.py'))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    cycles = 400000.0
+    full = {'GRBM_GUI_ACTIVE': 32 * cycles,
+            'SQ_VALU_MFMA_BUSY_CYCLES': 1024 * cycles}
+    d = mod.derive(full, duration_ns=200000.0)
+    assert abs(d['mfma_busy_over_active'] - 1.0) < 1e-9
+    assert abs(d['shader_clock_ghz'] - 2.0) < 1e-9
+    half = dict(full, SQ_VALU_MFMA_BUSY_CYCLES=512 * cycles)
+    assert abs(mod.derive(half)['mfma_busy_over_active'] - 0.5) < 1e-9
+    # the CSVs of a rocprofv3 run: counters and kernel-trace durations
+    (tmp_path / 'a').mkdir()
+    (tmp_path / 'a' / 'fwd_counter_collection.csv').write_text(
+        'Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n'
+        '1,k,GRBM_GUI_ACTIVE,%d\n1,k,SQ_VALU_MFMA_BUSY_CYCLES,%d\n' % (
+            32 * cycles, 1024 * cycles))
+    (tmp_path / 'a' / 'fwd_kernel_stats.csv').write_text(
+        'Name,AverageNs\nk,200000\n')
+    data = mod.load([str(tmp_path / 'a')])
+    assert mod.durations([str(tmp_path / 'a')]) == {'k': 200000.0}
+    assert data['k']['GRBM_GUI_ACTIVE'] == 32 * cycles

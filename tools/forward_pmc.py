@@ -26,10 +26,31 @@ def main():
     parser.add_argument('--layers', type=int, default=4)
     parser.add_argument('--iters', type=int, default=5)
     parser.add_argument('--no-torch', action='store_true')
+    parser.add_argument('--calib-iters', type=int, default=200000,
+                        help='warm-start kernel iterations (4 back-to-back '
+                             'MFMAs each on every SIMD): the MFMA-busy '
+                             'calibration kernel (0 = skip)')
     args = parser.parse_args()
     import torch
     from kiosk_autoscaler_amd.ops import native
     mod = native.load()
+    if args.calib_iters:
+        # calibration: every SIMD issues back-to-back MFMAs, so
+        # SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x kernel cycles) should read ~1
+        # (tools/pmc_summary.py); the records' s_memtime / s_memrealtime
+        # give the shader clock under MFMA load
+        w = torch.zeros(1 << 20, dtype=torch.bfloat16, device='cuda')
+        rec = torch.zeros(256 * 8, dtype=torch.int32, device='cuda')
+        mod.warmstart_raw(w.data_ptr(), w.numel(), rec.data_ptr(), 256,
+                          args.calib_iters, 128 * 1024,
+                          torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        r = rec.view(256, 8).cpu().numpy().astype('int64') & 0xffffffff
+        real = ((r[:, 5] << 32) | r[:, 4]) - ((r[:, 3] << 32) | r[:, 2])
+        ghz = (r[:, 7] / (real / 100e6)) / 1e9
+        print('calib: %d MFMA/SIMD, shader clock %.3f GHz (min %.3f max '
+              '%.3f), %.1f us' % (4 * args.calib_iters, ghz.mean(), ghz.min(),
+                                  ghz.max(), real.mean() / 100.0), flush=True)
     engine = mod.Engine(0, args.dim, args.hidden, args.layers, args.rows, 3)
     try:
         engine.prepare(args.rows)

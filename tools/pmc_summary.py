@@ -3,9 +3,15 @@
 
 Usage: python tools/pmc_summary.py gpurun_out/pmc/a gpurun_out/pmc/b
 Prints one JSON line per kernel with the mean of each counter per dispatch
-and derived ratios: MFMA utilisation (SQ_VALU_MFMA_BUSY_CYCLES over
-GRBM_GUI_ACTIVE/8 x 1024 SIMDs), LDS bank-conflict share, and the
-wave-cycle split (parked / issue-stalled / issuing).
+and derived ratios: MFMA busy over active (SQ_VALU_MFMA_BUSY_CYCLES, the
+SIMD-cycles the matrix pipes were busy summed over the 1024 SIMDs, over
+1024 x the kernel's cycles = GRBM_GUI_ACTIVE / 32: that counter sums the 32
+shader engines, 8 XCDs x 4 -- calibrated with the warm-start kernel, whose
+every SIMD issues back-to-back MFMAs, profiles/r3_mfma_util/), the shader
+clock that implies when the kernel trace gives durations, LDS bank-conflict
+share, and the wave-cycle split (parked / issue-stalled / issuing).
+Round 2 divided GRBM_GUI_ACTIVE by 8 and read the MFMA counter as a work
+count; it is busy cycles (16 per v_mfma_f32_16x16x32_bf16).
 """
 import collections
 import csv
@@ -36,11 +42,34 @@ def load(dirs):
     return out
 
 
-def derive(c):
+SIMDS = 1024          # 256 CUs x 4
+GRBM_INSTANCES = 32   # GRBM_GUI_ACTIVE summed over 8 XCDs x 4 SEs
+
+
+def durations(dirs):
+    """Kernel name -> mean duration (ns) from the kernel-trace stats."""
+    out = {}
+    for d in dirs:
+        for path in glob.glob(os.path.join(d, '**', '*kernel_stats.csv'),
+                              recursive=True):
+            with open(path) as handle:
+                for row in csv.DictReader(handle):
+                    try:
+                        out[row['Name']] = float(row['AverageNs'])
+                    except (KeyError, ValueError):
+                        pass
+    return out
+
+
+def derive(c, duration_ns=None):
     d = {}
     if c.get('GRBM_GUI_ACTIVE') and 'SQ_VALU_MFMA_BUSY_CYCLES' in c:
-        d['mfma_util'] = c['SQ_VALU_MFMA_BUSY_CYCLES'] / (
-            c['GRBM_GUI_ACTIVE'] / 8.0 * 1024)
+        cycles = c['GRBM_GUI_ACTIVE'] / GRBM_INSTANCES
+        d['kernel_cycles'] = cycles
+        d['mfma_busy_over_active'] = c['SQ_VALU_MFMA_BUSY_CYCLES'] / (
+            SIMDS * cycles)
+        if duration_ns:
+            d['shader_clock_ghz'] = cycles / duration_ns
     if c.get('SQ_LDS_IDX_ACTIVE'):
         d['lds_conflict_share'] = c.get('SQ_LDS_BANK_CONFLICT', 0) / \
             c['SQ_LDS_IDX_ACTIVE']
@@ -54,12 +83,14 @@ def derive(c):
 
 def main():
     data = load(sys.argv[1:])
+    times = durations(sys.argv[1:])
     for name, counters in sorted(data.items()):
         short = name.replace('kiosk::(anonymous namespace)::', '')
         short = short.replace('void ', '').split('(')[0]
         row = {'kernel': short}
         row.update({k: round(v, 1) for k, v in sorted(counters.items())})
-        row.update({k: round(v, 4) for k, v in derive(counters).items()})
+        row.update({k: round(v, 4) for k, v in
+                    derive(counters, times.get(name)).items()})
         print(json.dumps(row))
 
 
