@@ -43,7 +43,7 @@ class NodeComm(object):
 
     def __init__(self, manager, init_timeout=12.0, fence_timeout=30.0,
                  fallback='shm', fallback_after=2, transport=None,
-                 shrink=True):
+                 shrink=True, shrink_grace=0.1):
         self.m = manager
         # after ``fallback_after`` consecutive failed generations the next
         # ones use the ``fallback`` transport (every rank switches in its
@@ -53,6 +53,12 @@ class NodeComm(object):
         self.fallback_after = max(1, int(fallback_after))
         self.transport_override = transport or None
         self.shrink_enabled = bool(shrink)
+        # losses are collected this long before one shrink excludes them
+        # all: workers drained by one scale-down retire within milliseconds
+        # of each other, and a loss while a shrink is connecting drops the
+        # generation
+        self.shrink_grace = float(shrink_grace)
+        self.loss_t = None
         self.init_timeout = float(init_timeout)
         self.fence_timeout = float(fence_timeout)
         self.gen = 0
@@ -76,7 +82,7 @@ class NodeComm(object):
     # ------------------------------------------------------------------
     @property
     def ready(self):
-        return self.state == READY
+        return self.state == READY and self.loss_t is None
 
     @property
     def full(self):
@@ -118,7 +124,11 @@ class NodeComm(object):
 
     def candidates(self):
         """``[(slot, proc)]`` over every managed slot, or ``None`` while one
-        of them has no live process with a node agent."""
+        of them has no live process with a node agent -- or while a worker
+        is still starting: a generation's RCCL init on a process that is
+        building its engine competes with it (a PyTorch engine started 1.9 s
+        after a deep-idle wake instead of 0.4 s), and the fence must stay
+        off the scale-up's critical path."""
         bound = self._bound()
         out = []
         for slot in self.m.slots:
@@ -126,6 +136,10 @@ class NodeComm(object):
             if not self._usable(proc) or proc in self.m.retiring:
                 return None
             out.append((slot.index, proc))
+        for resource in self.m.resources.values():
+            for worker in resource.workers.values():
+                if worker.state == 'starting':
+                    return None
         return out
 
     # ------------------------------------------------------------------
@@ -140,16 +154,23 @@ class NodeComm(object):
             if lost:
                 if (self.state == READY and self.shrink_enabled and
                         self.can_shrink and len(lost) < len(self.members)):
-                    self._shrink(lost, now)
+                    if self.loss_t is None:
+                        self.loss_t = now
+                    if now - self.loss_t >= self.shrink_grace:
+                        self.loss_t = None
+                        self._shrink(lost, now)
                 else:
+                    self.loss_t = None
                     self.break_('slot(s) %s lost their process' % [
                         self.members[r][0] for r in lost])
-            elif self.state in (INIT, SHRINK) and \
-                    now - self.t_start > self.init_timeout:
-                self.break_('generation %d.%d %s timed out after %.1f s' % (
-                    self.gen, self.sub, self.state, self.init_timeout),
-                    failed=True)
-        if self.state == READY and self.inflight is None and \
+            else:
+                self.loss_t = None
+                if self.state in (INIT, SHRINK) and \
+                        now - self.t_start > self.init_timeout:
+                    self.break_('generation %d.%d %s timed out after %.1f s'
+                                % (self.gen, self.sub, self.state,
+                                   self.init_timeout), failed=True)
+        if self.ready and self.inflight is None and \
                 len(self.members) < len(self.m.slots):
             members = self.candidates()
             if members:

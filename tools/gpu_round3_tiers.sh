@@ -5,6 +5,8 @@
 #        shm) + deep idle (POOL_IDLE_RELEASE_S=3)
 #   bash tools/gpu_round3_tiers.sh C -> torch plug-in: warm pool, context,
 #        cold spawn
+#   bash tools/gpu_round3_tiers.sh D -> deep idle, built-in and torch engine
+#        (node generation deferred until the woken worker is READY)
 set -o pipefail
 OUT=${OUT:-gpurun_out/r3_tiers}
 mkdir -p $OUT
@@ -32,4 +34,8 @@ elif [ "$1" = "C" ]; then
     run torch_context 260 --gpus 1 --steps 6 --warmup 1 --budget-s 230 --pool-mode context --cold-cycles 0 && \
   WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine POOL_IDLE_RELEASE_S=3 \
     run torch_deep_idle 260 --gpus 1 --steps 6 --warmup 1 --budget-s 230 --cold-cycles 0
+elif [ "$1" = "D" ]; then
+  POOL_IDLE_RELEASE_S=3 run deep_idle_v2 260 --gpus 1 --steps 10 --warmup 1 --budget-s 230 --cold-cycles 0 && \
+  WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine POOL_IDLE_RELEASE_S=3 \
+    run torch_deep_idle_v2 260 --gpus 1 --steps 6 --warmup 1 --budget-s 230 --cold-cycles 0
 fi
