@@ -326,6 +326,7 @@ class GpuManager(object):
         # imported the worker (and torch, for a plug-in) without the GPU
         self.zygote_enabled = bool(zygote)
         self.zygote = None
+        self._zygote_restart_at = 0.0
         self.mapping_fixes = 0   # slots remapped after a PCI check
         self.history = []   # exited workers, for accounting
         # persistent node-wide communicator: needs one long-lived process
@@ -601,6 +602,8 @@ class GpuManager(object):
                     self._on_worker_messages(owner)
             self._reap_all()
             self._watchdog()
+            if self.zygote_enabled and not self._check_zygote():
+                self._start_zygote()      # a dead zygote, after a pause
             if self.node is not None and not self._stopping:
                 self.node.step()
             for resource in self.resources.values():
@@ -641,11 +644,13 @@ class GpuManager(object):
     def _start_zygote(self):
         tpl = self.pool_template
         if not self.zygote_enabled or tpl is None or self.zygote is not None \
-                or tpl.module != 'kiosk_autoscaler_amd.worker.main':
+                or tpl.module != 'kiosk_autoscaler_amd.worker.main' or \
+                self._stopping or time.monotonic() < self._zygote_restart_at:
             return
         from ..worker import zygote
         if not zygote.become_subreaper():
             logger.warning('PR_SET_CHILD_SUBREAPER refused: no zygote.')
+            self.zygote_enabled = False
             return
         argv = self._interpreter(tpl) + [
             '-m', 'kiosk_autoscaler_amd.worker.zygote', '--backend',
@@ -653,16 +658,28 @@ class GpuManager(object):
         self.zygote = zygote.ZygoteClient(argv, self._environment(tpl))
         self.events.emit('zygote_spawn', pid=self.zygote.pid)
 
+    def _check_zygote(self):
+        """False (and the zygote forgotten, restarted after a pause) once
+        the zygote process has exited."""
+        z = self.zygote
+        if z is None:
+            return False
+        if z.alive():
+            return True
+        logger.warning('Worker zygote %d exited; spawning directly until it '
+                       'is restarted.', z.pid)
+        self.events.emit('zygote_exit', pid=z.pid, code=z.popen.returncode)
+        z.close()
+        self.zygote = None
+        self._zygote_restart_at = time.monotonic() + 10.0
+        return False
+
     def _zygote_for(self, template):
         z = self.zygote
         tpl = self.pool_template
         if z is None or tpl is None:
             return None
-        if not z.alive():
-            logger.warning('Worker zygote %d exited; spawning directly.',
-                           z.pid)
-            z.close()
-            self.zygote = None
+        if not self._check_zygote():
             return None
         if not z.poll_ready():
             return None      # still importing: this spawn takes the slow path

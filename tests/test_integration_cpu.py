@@ -346,3 +346,25 @@ def test_zygote_cold_spawn_reaped_like_a_child(stack):
              timeout=30)
     wait_for(lambda: client.hget('predict:slow', 'status') == 'done',
              timeout=60)
+
+
+def test_dead_zygote_is_restarted(stack):
+    """A zygote that dies costs the fast path only until it is restarted;
+    spawns meanwhile go through exec."""
+    s, client, manager, scaler, events = stack(WARM_POOL='0')
+    wait_for(lambda: manager.zygote.poll_ready(), timeout=60)
+    old = manager.zygote.pid
+    os.kill(old, signal.SIGKILL)
+    wait_for(lambda: manager.zygote is None or manager.zygote.pid != old,
+             timeout=10)
+    manager._zygote_restart_at = 0.0
+    wait_for(lambda: manager.zygote is not None and
+             manager.zygote.pid != old and manager.zygote.poll_ready(),
+             timeout=60)
+    assert any(e['ev'] == 'zygote_exit' for e in events.records)
+    enqueue(client, 1)
+    assert tick(scaler, s) == 1
+    wait_for(lambda: client.hget('predict:job0', 'status') == 'done',
+             timeout=30)
+    spawns = [e for e in events.records if e['ev'] == 'process_spawn']
+    assert spawns[-1]['via'] == 'zygote'
