@@ -1296,6 +1296,20 @@ class GpuManager(object):
         resource.fence_inflight = (epoch, members, time.monotonic())
         self.events.emit('fence_start', epoch=epoch, members=members)
 
+    def _node_fence_runnable(self):
+        """A resource has a membership change the node communicator can
+        fence right now (every member runs on one of its ranks)."""
+        for resource in self.resources.values():
+            if not resource.fence_wanted:
+                continue
+            members = [w for w in resource.ready()]
+            if sorted(w.id for w in members) == sorted(
+                    resource.fenced_members):
+                continue
+            if self.node.can_fence([w.proc for w in members]):
+                return True
+        return False
+
     def _maybe_node_fence(self, resource):
         """One 72-B all-reduce over the persistent communicator; waits
         (fence_wanted stays set) while a generation is being built or

@@ -171,7 +171,10 @@ class NodeComm(object):
                                 % (self.gen, self.sub, self.state,
                                    self.init_timeout), failed=True)
         if self.ready and self.inflight is None and \
-                len(self.members) < len(self.m.slots):
+                len(self.members) < len(self.m.slots) and \
+                not self.m._node_fence_runnable():
+            # (a fence the shrunk communicator can run goes first: the
+            # regrow's RCCL init would hold it for seconds)
             members = self.candidates()
             if members:
                 self._regrow(members, now)
