@@ -229,6 +229,9 @@ hipError_t launch_gemm_variant(const uint16_t* A, const uint16_t* B,
   if (variant == GEMM_256W4)
     return launch_gemm256(A, B, C, bias, R, M, N, K, epilogue, stream, 256,
                           4);
+  if (variant == GEMM_256W4P)
+    return launch_gemm256_persist(A, B, C, bias, R, M, N, K, epilogue,
+                                  stream);
   return launch_gemm(A, B, C, bias, R, M, N, K, epilogue, stream);
 }
 

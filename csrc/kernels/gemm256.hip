@@ -166,7 +166,14 @@ constexpr int waitcnt_vm(int vm) {
 // epilogue.  (A "ticket first" variant -- the first block publishes one
 // plane, the second keeps its accumulators and waits for it -- measured
 // slower than the reduce kernel and spilled: removed, profiles/r2_splitk_ab.)
-template <int EPI, int BN, int kWaves, int kFused = 0>
+// kPersist (4-wave only): a grid of one workgroup per CU walks the tiles
+// (tile += gridDim.x; the XCD remap keeps each XCD on its own tile range);
+// after a tile's main loop the next tile's first four DMA groups are issued
+// into the free ring units *before* this tile's epilogue, so they land while
+// the epilogue computes and stores.  The next main loop's opening
+// `vmcnt(16)` stays correct: waits count ops in issue order, and the
+// epilogue's stores are younger than the prefetch.
+template <int EPI, int BN, int kWaves, int kFused = 0, int kPersist = 0>
 __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
     uint16_t* __restrict__ C, const float* __restrict__ bias,
@@ -180,14 +187,21 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   B += static_cast<size_t>(split) * K;
   const int tiles_n = N / BN;
   const int tiles_m = (M + BM - 1) / BM;
-  const int wg = xcd_remap(static_cast<int>(blockIdx.x), tiles_m * tiles_n);
-  const int per_group = kGroupM * tiles_n;
-  const int group = wg / per_group;
-  const int first_m = group * kGroupM;
-  const int gsize = min(tiles_m - first_m, kGroupM);
-  const int in_group = wg - group * per_group;
-  const int m0 = (first_m + in_group % gsize) * BM;
-  const int n0 = (in_group / gsize) * BN;
+  const int ntiles = tiles_m * tiles_n;
+  // tile -> its origin: XCD-aware bijective remap, kGroupM-row grouping
+  auto origin = [&](int t, int& om, int& on) {
+    const int wg = xcd_remap(t, ntiles);
+    const int per_group = kGroupM * tiles_n;
+    const int group = wg / per_group;
+    const int first_m = group * kGroupM;
+    const int gsize = min(tiles_m - first_m, kGroupM);
+    const int in_group = wg - group * per_group;
+    om = (first_m + in_group % gsize) * BM;
+    on = (in_group / gsize) * BN;
+  };
+  int tile = static_cast<int>(blockIdx.x);
+  int m0 = 0, n0 = 0, m0_next = 0, n0_next = 0;
+  origin(tile, m0, n0);
 
   using G = Geo<BN, kWaves>;
   constexpr int TM = G::TM, TN = G::TN, kSlotBytes = G::kSlotBytes;
@@ -199,6 +213,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / G::kWavesN, wn = wave % G::kWavesN;
 
+  for (int it = 0;; ++it) {
   f32x4 acc[TM][TN];
   if constexpr (kWaves != 4) {
 #pragma unroll
@@ -308,7 +323,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   // half-steps-in-flight probe shows that is enough.  LDS rows are 128 B
   // with 16-B chunk c of row r at c ^ ((r >> 1) & 7): every ds_read_b128
   // lane group then covers 16 distinct bank slots.
-  auto mainloop_w4 = [&](int steps) {
+  auto mainloop_w4 = [&](int steps, bool prefetched) {
     constexpr int kUnit = BM * 128;
     int voff_a[8], voff_b[8];
 #pragma unroll
@@ -399,10 +414,12 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
         }
       }
     };
+    if (!prefetched) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+      for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int p = 0; p < 8; ++p) dma(g, p);
+        for (int p = 0; p < 8; ++p) dma(g, p);
+    }
     __builtin_amdgcn_s_waitcnt(waitcnt_vm(16));
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -457,7 +474,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   };
 
   if constexpr (kWaves == 4) {
-    mainloop_w4(K / 64);
+    mainloop_w4(K / 64, kPersist && it > 0);
   } else {
 #pragma unroll
     for (int h = 0; h < kSlots; ++h) stage(h);
@@ -482,6 +499,49 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) asm volatile("" : "+a"(acc[i][j]));
+  }
+  if constexpr (kPersist) {
+    // the next tile's groups 0..3 (units 0..3) under this tile's epilogue;
+    // every wave is past its last LDS read and the tail DMAs have drained
+    // (vmcnt(0) above), so no unit is still read or written
+    // branch-free (a branch here splits the 256 live accumulators'
+    // ranges and spills): past the last tile the prefetch re-reads this
+    // tile's first groups into units nobody reads; the kernel drains them
+    // before it exits
+    {
+      int next = tile + static_cast<int>(gridDim.x);
+      next = next < ntiles ? next : tile;
+      origin(next, m0_next, n0_next);
+      __builtin_amdgcn_s_barrier();
+      constexpr int kUnit = BM * 128;
+      const int steps = K / 64;
+      const auto rsrc_a = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint16_t*>(A), 0, 0x7fffffff, 0x00020000);
+      const auto rsrc_b = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint16_t*>(B), 0, 0x7fffffff, 0x00020000);
+      // group-major, as the main loop's prologue: groups 0-1 are the
+      // oldest 16 ops its opening vmcnt(16) waits for.  Offsets are
+      // computed per issue (no arrays live across the epilogue), and the
+      // block is fenced off from the epilogue's scheduling
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int t = min(g >> 1, steps - 1);
+        const int row0 = (g & 1) ? n0_next : m0_next;
+        const int rows = (g & 1) ? N : M;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+          const int r = (wave * 8 + p) * 8 + (lane >> 3);
+          const int c = (lane & 7) ^ ((r >> 1) & 7);
+          const int gr = row0 + r < rows ? row0 + r : rows - 1;
+          char* lds = smem + g * kUnit + (wave * 8 + p) * 1024;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              (g & 1) ? rsrc_b : rsrc_a, (lds_void_t*)lds, 16,
+              (gr * lda + c * 8) * 2, t * 128, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 
   // Epilogue.  Lane l holds row (l & 15), columns 4g..4g+3 (g = l >> 4) of
@@ -614,6 +674,19 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
       *reinterpret_cast<uint4*>(C + static_cast<size_t>(m) * N + col) = out;
     }
   }
+  if constexpr (!kPersist) {
+    break;
+  } else {
+    tile += static_cast<int>(gridDim.x);
+    if (tile >= ntiles) {
+      // the last prefetch must land before the workgroup's LDS is freed
+      __builtin_amdgcn_s_waitcnt(kWaitAll);
+      break;
+    }
+    m0 = m0_next;
+    n0 = n0_next;
+  }
+  }  // tile loop
 }
 
 template <int EPI, int BN, int W>
@@ -661,6 +734,27 @@ hipError_t launch256(const uint16_t* A, const uint16_t* B, uint16_t* C,
       return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// persistent 4-wave kernel: one workgroup per CU (its 160 KiB of LDS allow
+// no more), each walking ceil(tiles / CUs) tiles
+int g_cu_count = 256;
+
+template <int EPI>
+hipError_t configure_persist() {
+  return hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&gemm256_kernel<EPI, 256, 4, 0, 1>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256, 4>::kLdsBytes);
+}
+
+template <int EPI>
+void launch_persist_epi(const uint16_t* A, const uint16_t* B, uint16_t* C,
+                        const float* bias, const uint16_t* R, int M, int N,
+                        int K, int grid, hipStream_t stream) {
+  constexpr int lds = Geo<256, 4>::kLdsBytes;
+  hipLaunchKernelGGL((gemm256_kernel<EPI, 256, 4, 0, 1>), dim3(grid),
+                     dim3(256), lds, stream, A, B, C, bias, R, M, N, K, K,
+                     nullptr, nullptr);
 }
 
 template <int EPI, int kMode>
@@ -789,7 +883,15 @@ hipError_t launch_reduce(const float* P, int splits, int M, int N,
 }  // namespace
 
 hipError_t gemm256_prepare() {
+  int device = 0, cus = 0;
+  if (hipGetDevice(&device) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+                            device) == hipSuccess && cus > 0)
+    g_cu_count = cus;
   hipError_t err = configure256_all<256, 8>();
+  if (err == hipSuccess) err = configure_persist<EPI_NONE>();
+  if (err == hipSuccess) err = configure_persist<EPI_BIAS_GELU>();
+  if (err == hipSuccess) err = configure_persist<EPI_BIAS_RESIDUAL>();
   if (err == hipSuccess) err = configure256_all<128, 8>();
   if (err == hipSuccess) err = configure256_all<256, 4>();
   if (err == hipSuccess) err = configure_fused4<EPI_NONE>();
@@ -826,6 +928,31 @@ hipError_t launch_gemm256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                              stream);
   return launch256<256, 8>(A, B, C, bias, R, M, N, K, K, 1, epilogue,
                            stream);
+}
+
+hipError_t launch_gemm256_persist(const uint16_t* A, const uint16_t* B,
+                                  uint16_t* C, const float* bias,
+                                  const uint16_t* R, int M, int N, int K,
+                                  int epilogue, hipStream_t stream) {
+  if (!gemm256w4_shape_ok(M, N, K)) return hipErrorInvalidValue;
+  const int tiles = ((M + BM - 1) / BM) * (N / 256);
+  const int grid = tiles < g_cu_count ? tiles : g_cu_count;
+  switch (epilogue) {
+    case EPI_NONE:
+      launch_persist_epi<EPI_NONE>(A, B, C, bias, R, M, N, K, grid, stream);
+      break;
+    case EPI_BIAS_GELU:
+      launch_persist_epi<EPI_BIAS_GELU>(A, B, C, bias, R, M, N, K, grid,
+                                        stream);
+      break;
+    case EPI_BIAS_RESIDUAL:
+      launch_persist_epi<EPI_BIAS_RESIDUAL>(A, B, C, bias, R, M, N, K, grid,
+                                            stream);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 int gemm256_splits(int M, int N, int K) {

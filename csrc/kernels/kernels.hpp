@@ -43,10 +43,12 @@ hipError_t warmstart_prepare();
 // ring when that fills the chip, else 128x128), 1 = 128x128 two-barrier,
 // 2 = 256x256 LDS ring, 3 = 256x128 LDS ring, 4 = split-K 256x256 (fp32
 // partials in `workspace` + one fused reduce/epilogue kernel), 5 = 256x256
-// ring with 4 waves of 128x128 outputs (accumulators in AGPRs).
+// ring with 4 waves of 128x128 outputs (accumulators in AGPRs), 6 = the
+// same as a persistent grid (one workgroup per CU walks the tiles; the next
+// tile's first DMA groups overlap the epilogue).
 enum GemmVariant {
   GEMM_AUTO = 0, GEMM_128 = 1, GEMM_256 = 2, GEMM_256x128 = 3,
-  GEMM_256_SPLITK = 4, GEMM_256W4 = 5
+  GEMM_256_SPLITK = 4, GEMM_256W4 = 5, GEMM_256W4P = 6
 };
 hipError_t launch_gemm_variant(const uint16_t* A, const uint16_t* B,
                                uint16_t* C, const float* bias,
@@ -65,6 +67,10 @@ hipError_t launch_gemm256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                           const float* bias, const uint16_t* R, int M, int N,
                           int K, int epilogue, hipStream_t stream,
                           int bn = 256, int waves = 8);
+hipError_t launch_gemm256_persist(const uint16_t* A, const uint16_t* B,
+                                  uint16_t* C, const float* bias,
+                                  const uint16_t* R, int M, int N, int K,
+                                  int epilogue, hipStream_t stream);
 int gemm256_splits(int M, int N, int K);
 size_t gemm256_splitk_workspace(int M, int N, int K);
 // split-K on the 4-wave kernel: combine in-launch by each tile's last

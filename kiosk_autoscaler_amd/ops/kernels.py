@@ -25,7 +25,7 @@ def _check_bf16(t, name):
 
 
 VARIANTS = {'auto': 0, '128': 1, '256': 2, '256x128': 3, '256splitk': 4,
-            '256w4': 5}
+            '256w4': 5, '256w4p': 6}
 
 
 def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
@@ -38,8 +38,10 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
     ring when that does, else 128x128; split-K 256x256 where the grid alone
     would leave CUs idle), ``'128'``, ``'256'``, ``'256x128'`` or
     ``'256splitk'`` (fp32 partials in a temporary workspace + one fused
-    reduce/epilogue kernel) or ``'256w4'`` (256x256 ring, 4 waves of
-    128x128 outputs)."""
+    reduce/epilogue kernel), ``'256w4'`` (256x256 ring, 4 waves of
+    128x128 outputs) or ``'256w4p'`` (the same as a persistent grid: one
+    workgroup per CU walks the tiles, the next tile's first loads overlap
+    the epilogue)."""
     import torch
     mod = native.load()
     _check_bf16(a, 'a')
@@ -53,9 +55,9 @@ def gemm(a, b, bias=None, residual=None, epilogue='none', out=None,
             raise ValueError('split-K does not apply to M=%d N=%d K=%d '
                              '(the 256x256 grid already fills the chip, or '
                              'K is too short)' % (M, N, K))
-    elif variant in ('256', '256x128', '256w4'):
+    elif variant in ('256', '256x128', '256w4', '256w4p'):
         bn = 128 if variant == '256x128' else 256
-        kq = 64 if variant == '256w4' else 32
+        kq = 64 if variant in ('256w4', '256w4p') else 32
         if M < 1 or N % bn or K % kq or K < kq:
             raise ValueError('the 256x%d kernel needs N %% %d == 0 and '
                              'K %% %d == 0 (M=%d N=%d K=%d)'

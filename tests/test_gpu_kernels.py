@@ -253,7 +253,7 @@ def test_preload_modules_stamps(mod):
                                    (520, 384, 160), (777, 768, 192),
                                    (256, 512, 128)])
 @pytest.mark.parametrize('epilogue', ['none', 'gelu', 'residual'])
-@pytest.mark.parametrize('variant', ['256', '256x128', '256w4'])
+@pytest.mark.parametrize('variant', ['256', '256x128', '256w4', '256w4p'])
 def test_gemm256_ring_kernel(mod, M, N, K, epilogue, variant):
     """The 256x256 / 256x128 LDS-ring kernels against the fp32 reference
     (odd half counts exercise the clamped tail staging); a shape a variant
@@ -264,8 +264,8 @@ def test_gemm256_ring_kernel(mod, M, N, K, epilogue, variant):
     b = rand_bf16(N, K, scale=0.1, seed=12)
     bias = torch.randn(N, device='cuda')
     res = rand_bf16(M, N, seed=13)
-    if (variant in ('256', '256w4') and N % 256) or \
-            (variant == '256w4' and K % 64):
+    if (variant in ('256', '256w4', '256w4p') and N % 256) or \
+            (variant in ('256w4', '256w4p') and K % 64):
         with pytest.raises(ValueError, match='needs N'):
             kernels.gemm(a, b, bias=bias, residual=res, epilogue=epilogue,
                          variant=variant)
@@ -282,6 +282,36 @@ def test_gemm256_ring_kernel(mod, M, N, K, epilogue, variant):
     torch.testing.assert_close(c.float(), ref, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize('M,N,K', [(4000, 4608, 192), (2048, 16384, 256),
+                                   (8192, 8192, 128)])
+@pytest.mark.parametrize('epilogue', ['none', 'gelu', 'residual'])
+def test_gemm256_persistent_walks_many_tiles(mod, M, N, K, epilogue):
+    """The persistent 4-wave grid (one workgroup per CU) at shapes with more
+    tiles than CUs -- 288, 512 and 1024 tiles, a ragged last row of tiles --
+    so workgroups run 2-4 tiles and every tile after the first starts on
+    loads prefetched under the previous tile's epilogue."""
+    from kiosk_autoscaler_amd.ops import kernels
+    a = rand_bf16(M, K, seed=21)
+    b = rand_bf16(N, K, scale=0.1, seed=22)
+    bias = torch.randn(N, device='cuda')
+    res = rand_bf16(M, N, seed=23)
+    ref = a.float() @ b.float().t()
+    if epilogue != 'none':
+        ref = ref + bias
+    if epilogue == 'gelu':
+        ref = gelu_tanh(ref)
+    if epilogue == 'residual':
+        ref = ref + res.float()
+    c = kernels.gemm(a, b, bias=bias, residual=res, epilogue=epilogue,
+                     variant='256w4p')
+    torch.testing.assert_close(c.float(), ref, atol=3e-2, rtol=2e-2)
+    # bit-identical to the non-persistent 4-wave kernel (same tiles, same
+    # K order)
+    c4 = kernels.gemm(a, b, bias=bias, residual=res, epilogue=epilogue,
+                      variant='256w4')
+    assert torch.equal(c, c4)
+
+
 def test_gemm256_identity(mod):
     from kiosk_autoscaler_amd.ops import kernels
     M = K = 512
@@ -296,8 +326,8 @@ def test_gemm256_identity(mod):
     a = torch.eye(M, K, device='cuda', dtype=torch.bfloat16)
     b = (torch.arange(N * K, device='cuda', dtype=torch.float32)
          .reshape(N, K) % 241 - 120).to(torch.bfloat16)
-    for variant in ('256', '256x128', '256w4'):
-        if variant == '256w4' and N % 256:
+    for variant in ('256', '256x128', '256w4', '256w4p'):
+        if variant in ('256w4', '256w4p') and N % 256:
             continue
         c = kernels.gemm(a, b, variant=variant)
         assert torch.equal(c, b.t().contiguous()[:M]), variant

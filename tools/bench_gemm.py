@@ -22,6 +22,9 @@ def main():
     parser.add_argument('--rounds', type=int, default=5)
     parser.add_argument('--shapes', default='2048x16384x4096,2048x4096x16384,'
                         '8192x16384x4096,4096x4096x4096')
+    parser.add_argument('--only', default='',
+                        help='comma-separated function names to time '
+                             '(default: all)')
     args = parser.parse_args()
     for spec in args.shapes.split(','):
         M, N, K = (int(v) for v in spec.split('x'))
@@ -41,6 +44,13 @@ def main():
 
         def ours_256w4():
             kernels.gemm(a, b, out=out, variant='256w4')
+
+        def ours_256w4p():
+            kernels.gemm(a, b, out=out, variant='256w4p')
+
+        def ours_256w4p_gelu():
+            kernels.gemm(a, b, bias=bias, epilogue='gelu', out=out,
+                         variant='256w4p')
 
         def ours_256_gelu():
             kernels.gemm(a, b, bias=bias, epilogue='gelu', out=out,
@@ -89,12 +99,17 @@ def main():
             fns['native256w4'] = ours_256w4
             fns['native256_gelu'] = ours_256_gelu
             fns['native256w4_gelu'] = ours_256w4_gelu
+            fns['native256w4p'] = ours_256w4p
+            fns['native256w4p_gelu'] = ours_256w4p_gelu
         fns['native256x128'] = ours_256x128
         if mod.gemm_workspace_bytes(M, N, K):
             fns['native256splitk'] = ours_splitk
             fns['native256splitk_fused'] = ours_splitk_fused
             fns['native256splitk_reduce'] = ours_splitk_reduce
 
+        if args.only:
+            keep = set(args.only.split(','))
+            fns = {k: v for k, v in fns.items() if k in keep}
         results = {k: [] for k in fns}
         for fn in fns.values():
             fn()
