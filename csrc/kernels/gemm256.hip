@@ -209,11 +209,19 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   constexpr int kWaitHalf1 = waitcnt_vm(3 * kLoadsPerHalf);
   constexpr int kWaitHalf2 = waitcnt_vm(2 * kLoadsPerHalf);
   constexpr int kWaitAll = waitcnt_vm(0);
-  const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / G::kWavesN, wn = wave % G::kWavesN;
-
   for (int it = 0;; ++it) {
+  // per tile, the lane-derived offsets are recomputed from an opaque lane
+  // id (mbcnt, not threadIdx): hoisted out of the persistent tile loop
+  // they would stay live across it and spill (no-op for one-tile grids)
+  int lane_id = static_cast<int>(threadIdx.x & 63);
+  if constexpr (kPersist) {
+    lane_id = static_cast<int>(
+        __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
+    asm volatile("" : "+v"(lane_id));
+  }
+  const int lane = lane_id;
   f32x4 acc[TM][TN];
   if constexpr (kWaves != 4) {
 #pragma unroll
@@ -524,6 +532,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
       // computed per issue (no arrays live across the epilogue), and the
       // block is fenced off from the epilogue's scheduling
       __builtin_amdgcn_sched_barrier(0);
+      int plane = static_cast<int>(
+          __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
+      asm volatile("" : "+v"(plane));   // derived here, not before the loop
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int t = min(g >> 1, steps - 1);
@@ -531,8 +542,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
         const int rows = (g & 1) ? N : M;
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
-          const int r = (wave * 8 + p) * 8 + (lane >> 3);
-          const int c = (lane & 7) ^ ((r >> 1) & 7);
+          const int r = (wave * 8 + p) * 8 + (plane >> 3);
+          const int c = (plane & 7) ^ ((r >> 1) & 7);
           const int gr = row0 + r < rows ? row0 + r : rows - 1;
           char* lds = smem + g * kUnit + (wave * 8 + p) * 1024;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(

@@ -22,7 +22,7 @@ def test_four_wave_gemm_asm_contract():
                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                           text=True, timeout=600)
     assert proc.returncode == 0, proc.stdout[-3000:]
-    assert 'checked 7 4-wave kernels: ok' in proc.stdout
+    assert 'checked 10 4-wave kernels: ok' in proc.stdout
 
 
 def test_checker_flags_violations():

@@ -547,7 +547,10 @@ def _death_mid_allreduce(manager, client, events):
     wait_for(lambda: _converged(manager, client) and
              len(_ready_ids(manager)) == 4, timeout=30)
     frozen = wait_for(lambda: manager.standbys.get(7), timeout=20)
-    wait_for(lambda: frozen.node_ok and manager.node.full, timeout=30)
+    wait_for(lambda: frozen.node_ok and manager.node.full and
+             manager.node.inflight is None, timeout=30)
+    with manager.lock:
+        assert any(p is frozen for _, p in manager.node.members)
     gens = manager.node.generations
     os.kill(frozen.pid, signal.SIGSTOP)
     try:
@@ -558,8 +561,9 @@ def _death_mid_allreduce(manager, client, events):
         wait_for(lambda: manager.node.inflight is not None, timeout=10)
         time.sleep(0.3)                     # the survivors are blocked now
         assert manager.node.inflight is not None
-        assert not [e for e in events.records[mark:]
-                    if e['ev'] == 'fence_done']
+        early = [e for e in events.records[mark:] if e['ev'] == 'fence_done']
+        assert not early, [(e['members'], e['n'], e.get('gen'), e.get('seq'))
+                           for e in early] + [manager.node.summary()]
     finally:
         os.kill(frozen.pid, signal.SIGKILL)
         os.kill(frozen.pid, signal.SIGCONT)

@@ -4,9 +4,11 @@
 hipcc pads no wait states after an inline-asm MFMA (cdna_hip_programming.md
 §5.7), so in every ``gemm256_kernel<*, 256, 4, *>`` the accumulators (AGPRs)
 may be touched only by MFMAs until the ``s_nop`` drain that ends the k-loop,
-and no scratch (spill) access may appear anywhere.  This script compiles
-csrc/kernels/gemm256.hip to gfx950 assembly and fails if either rule is
-broken.
+and no scratch (spill) access may appear anywhere -- except, in the
+persistent variant (``kPersist`` = 1: a loop over tiles around it all), a
+spill outside the k-loop (a reload or two per tile, never per MFMA).  This
+script compiles csrc/kernels/gemm256.hip to gfx950 assembly and fails if
+either rule is broken.
 
     python tools/check_asm_mfma.py
 """
@@ -32,8 +34,8 @@ def check(asm_text):
         end = asm_text.index('.Lfunc_end', start)
         body = [l.strip() for l in asm_text[start:end].split('\n')]
         insts = [l for l in body if l and not l.startswith(('.', ';'))]
-        if any(l.startswith('scratch_') for l in insts):
-            problems.append('%s: scratch (spill) access' % name)
+        persistent = re.search(r'ELi256ELi4ELi\dELi1EE', name) is not None
+        scratch = [i for i, l in enumerate(insts) if l.startswith('scratch_')]
         # last MFMA before the drain: everything between must not touch AGPRs
         drain = [i for i, l in enumerate(insts) if l.startswith('s_nop 7')]
         if not drain:
@@ -45,6 +47,12 @@ def check(asm_text):
         if last_mfma is None:
             problems.append('%s: no MFMA before the drain' % name)
             continue
+        first_mfma = min(i for i, l in enumerate(insts)
+                         if l.startswith('v_mfma'))
+        hot = [i for i in scratch if first_mfma <= i <= last_mfma]
+        if hot or (scratch and not persistent):
+            problems.append('%s: scratch (spill) access%s' % (
+                name, ' in the k-loop' if hot else ''))
         for l in insts[last_mfma + 1:first_drain]:
             if AGPR.search(l.split(';')[0]) and not l.startswith('v_mfma'):
                 problems.append('%s: AGPR touched before the drain: %s'
