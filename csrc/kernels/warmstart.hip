@@ -20,6 +20,17 @@
 namespace kiosk {
 namespace {
 
+// The accumulators pinned to AGPRs by inline asm (as gemm256.hip does): with
+// the builtin, hipcc rotated the four accumulators through VGPR copies every
+// iteration and the loop kept the matrix pipe only 38 % busy
+// (SQ_VALU_MFMA_BUSY_CYCLES over SIMD-cycles, profiles/r3_mfma_util/).
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& a,
+                                         const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+               : "+a"(acc)
+               : "v"(a), "v"(b));
+}
+
 __global__ __launch_bounds__(256) void warmstart_kernel(
     const uint16_t* __restrict__ w, size_t n, uint32_t* __restrict__ record,
     int iters, int lds_bytes) {
@@ -60,11 +71,14 @@ __global__ __launch_bounds__(256) void warmstart_kernel(
   const bf16x8 b = __builtin_bit_cast(bf16x8, rb);
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
   for (int i = 0; i < iters; ++i) {
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, acc1, 0, 0, 0);
-    acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, a, acc2, 0, 0, 0);
-    acc3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, b, acc3, 0, 0, 0);
+    mfma_acc(acc0, a, b);
+    mfma_acc(acc1, b, a);
+    mfma_acc(acc2, a, a);
+    mfma_acc(acc3, b, b);
   }
+  // no wait states follow an asm MFMA: drain before the AGPRs are read
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  asm volatile("" : "+a"(acc0), "+a"(acc1), "+a"(acc2), "+a"(acc3));
   float sum = acc0[0] + acc1[1] + acc2[2] + acc3[3];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);

@@ -351,7 +351,8 @@ def test_gpu_bench_contract(tmp_path):
 
 def test_pmc_summary_mfma_busy_over_active(tmp_path):
     """tools/pmc_summary.py: SQ_VALU_MFMA_BUSY_CYCLES is SIMD-busy cycles
-    summed over the 1024 SIMDs; GRBM_GUI_ACTIVE sums 32 shader engines.
+    summed over the 1024 SIMDs; GRBM_GUI_ACTIVE sums the 8 XCDs; a counter
+    collected in two passes is averaged, not summed.
     A kernel whose every SIMD is MFMA-busy for all its cycles reads 1.0,
     and the kernel-trace duration gives the shader clock."""
     import importlib.util
@@ -361,7 +362,7 @@ def test_pmc_summary_mfma_busy_over_active(tmp_path):
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     cycles = 400000.0
-    full = {'GRBM_GUI_ACTIVE': 32 * cycles,
+    full = {'GRBM_GUI_ACTIVE': 8 * cycles,
             'SQ_VALU_MFMA_BUSY_CYCLES': 1024 * cycles}
     d = mod.derive(full, duration_ns=200000.0)
     assert abs(d['mfma_busy_over_active'] - 1.0) < 1e-9
@@ -369,13 +370,17 @@ def test_pmc_summary_mfma_busy_over_active(tmp_path):
     half = dict(full, SQ_VALU_MFMA_BUSY_CYCLES=512 * cycles)
     assert abs(mod.derive(half)['mfma_busy_over_active'] - 0.5) < 1e-9
     # the CSVs of a rocprofv3 run: counters and kernel-trace durations
-    (tmp_path / 'a').mkdir()
-    (tmp_path / 'a' / 'fwd_counter_collection.csv').write_text(
-        'Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n'
-        '1,k,GRBM_GUI_ACTIVE,%d\n1,k,SQ_VALU_MFMA_BUSY_CYCLES,%d\n' % (
-            32 * cycles, 1024 * cycles))
+    for sub, counter in (('a', 'SQ_VALU_MFMA_BUSY_CYCLES'),
+                         ('b', 'SQ_WAIT_ANY')):
+        (tmp_path / sub).mkdir()
+        (tmp_path / sub / 'fwd_counter_collection.csv').write_text(
+            'Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n'
+            '1,k,GRBM_GUI_ACTIVE,%d\n1,k,%s,%d\n' % (
+                8 * cycles, counter, 1024 * cycles))
     (tmp_path / 'a' / 'fwd_kernel_stats.csv').write_text(
         'Name,AverageNs\nk,200000\n')
-    data = mod.load([str(tmp_path / 'a')])
-    assert mod.durations([str(tmp_path / 'a')]) == {'k': 200000.0}
-    assert data['k']['GRBM_GUI_ACTIVE'] == 32 * cycles
+    dirs = [str(tmp_path / 'a'), str(tmp_path / 'b')]
+    data = mod.load(dirs)
+    assert mod.durations(dirs) == {'k': 200000.0}
+    assert data['k']['GRBM_GUI_ACTIVE'] == 8 * cycles    # not 16x
+    assert abs(mod.derive(data['k'])['mfma_busy_over_active'] - 1.0) < 1e-9

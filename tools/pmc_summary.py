@@ -4,14 +4,13 @@
 Usage: python tools/pmc_summary.py gpurun_out/pmc/a gpurun_out/pmc/b
 Prints one JSON line per kernel with the mean of each counter per dispatch
 and derived ratios: MFMA busy over active (SQ_VALU_MFMA_BUSY_CYCLES, the
-SIMD-cycles the matrix pipes were busy summed over the 1024 SIMDs, over
-1024 x the kernel's cycles = GRBM_GUI_ACTIVE / 32: that counter sums the 32
-shader engines, 8 XCDs x 4 -- calibrated with the warm-start kernel, whose
-every SIMD issues back-to-back MFMAs, profiles/r3_mfma_util/), the shader
-clock that implies when the kernel trace gives durations, LDS bank-conflict
-share, and the wave-cycle split (parked / issue-stalled / issuing).
-Round 2 divided GRBM_GUI_ACTIVE by 8 and read the MFMA counter as a work
-count; it is busy cycles (16 per v_mfma_f32_16x16x32_bf16).
+SIMD-cycles the matrix pipes were busy -- 16 per v_mfma_f32_16x16x32_bf16,
+its issue interval -- summed over the 1024 SIMDs, over 1024 x the kernel's
+cycles = GRBM_GUI_ACTIVE / 8, the counter summing the 8 XCDs: checked with
+the warm-start kernel, whose own s_memtime / s_memrealtime stamps give the
+shader clock, profiles/r3_mfma_util/), the shader clock that implies when
+the kernel trace gives durations, LDS bank-conflict share, and the
+wave-cycle split (parked / issue-stalled / issuing).
 """
 import collections
 import csv
@@ -21,29 +20,41 @@ import os
 import sys
 
 
-def load(dirs):
+def load_pass(d):
+    """kernel -> counter -> mean per dispatch, for one rocprofv3 run."""
     sums = collections.defaultdict(lambda: collections.defaultdict(float))
     counts = collections.defaultdict(lambda: collections.defaultdict(set))
+    for path in glob.glob(os.path.join(d, '**', '*counter_collection*.csv'),
+                          recursive=True):
+        with open(path) as handle:
+            for row in csv.DictReader(handle):
+                name = row.get('Kernel_Name', '')
+                counter = row.get('Counter_Name', '')
+                value = float(row.get('Counter_Value', 0) or 0)
+                dispatch = row.get('Dispatch_Id', '')
+                sums[name][counter] += value
+                counts[name][counter].add(dispatch)
+    return {name: {c: v / max(1, len(counts[name][c]))
+                   for c, v in by_counter.items()}
+            for name, by_counter in sums.items()}
+
+
+def load(dirs):
+    """Per kernel, each counter averaged over the passes that collected it.
+    (Round 2 summed a counter collected in several passes -- GRBM_GUI_ACTIVE
+    rides along in most -- over dispatch ids that repeat from pass to pass,
+    inflating it by the number of passes.)"""
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for d in dirs:
-        for path in glob.glob(os.path.join(d, '**', '*counter_collection*.csv'),
-                              recursive=True):
-            with open(path) as handle:
-                for row in csv.DictReader(handle):
-                    name = row.get('Kernel_Name', '')
-                    counter = row.get('Counter_Name', '')
-                    value = float(row.get('Counter_Value', 0) or 0)
-                    dispatch = row.get('Dispatch_Id', '')
-                    sums[name][counter] += value
-                    counts[name][counter].add(dispatch)
-    out = {}
-    for name, by_counter in sums.items():
-        out[name] = {c: v / max(1, len(counts[name][c]))
-                     for c, v in by_counter.items()}
-    return out
+        for name, counters in load_pass(d).items():
+            for c, v in counters.items():
+                acc[name][c].append(v)
+    return {name: {c: sum(v) / len(v) for c, v in by_counter.items()}
+            for name, by_counter in acc.items()}
 
 
 SIMDS = 1024          # 256 CUs x 4
-GRBM_INSTANCES = 32   # GRBM_GUI_ACTIVE summed over 8 XCDs x 4 SEs
+GRBM_INSTANCES = 8    # GRBM_GUI_ACTIVE summed over the 8 XCDs
 
 
 def durations(dirs):
