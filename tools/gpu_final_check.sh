@@ -1,7 +1,7 @@
 # Round-end rehearsal on one MI355X: the GPU test suite, smoke(), and the
 # driver's exact bench command; each step bounded, stop at the first failure.
 set -o pipefail
-OUT=gpurun_out/final
+OUT=${OUT:-gpurun_out/final}
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 170 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }
 tail -2 $OUT/gpu_tests.log
