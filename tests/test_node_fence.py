@@ -1048,3 +1048,55 @@ def test_deep_idle_builds_one_generation_per_wake(resp_server, tmp_path):
     assert len(inits) == wakes + 1, (len(inits), parks)
     assert not any(e['failed'] for e in events.records
                    if e['ev'] == 'node_comm_break')
+
+
+@pytest.mark.gpu
+def test_gpu_shrink_and_regrow_with_real_workers(resp_server):
+    """MI355X, two slots on the one GPU with context standbys (node
+    communicator over shm): kill slot 1's standby -9; the survivor shrinks
+    it out and keeps fencing (a scale-up on slot 0 is fenced by the
+    1-rank shrunk communicator), then slot 1's fresh standby joins the
+    next full generation -- with real HIP worker processes."""
+    from kiosk_autoscaler_amd import gpumgr
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict', 'RESOURCE_NAME': 'shr', 'MAX_PODS': '2',
+           'WORKER_BACKEND': 'hip', 'WARM_POOL': '2', 'FENCE': 'auto',
+           'WARM_POOL_MODE': 'context', 'REDIS_INTERVAL': '0',
+           'GPU_IDS': '0,0', 'MODEL_DIM': '1024', 'MODEL_HIDDEN': '4096',
+           'MODEL_LAYERS': '2', 'ROWS_PER_KEY': '256'}
+    s = Settings(Config(environ=env, use_files=False))
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    events = EventLog(source='test')
+    events.keep = True
+    manager = gpumgr.build_manager(s, redis_client=client,
+                                   events=events).start()
+
+    def active():
+        return _active_of(client, 'shr')
+    try:
+        wait_for(lambda: manager.node.ready and manager.node.full,
+                 timeout=120)
+        victim = manager.standbys[1]
+        os.kill(victim.pid, signal.SIGKILL)
+        wait_for(lambda: manager.node.shrinks == 1 and manager.node.ready,
+                 timeout=60)
+        manager.patch_namespaced_deployment('shr', 'default',
+                                            {'spec': {'replicas': 1}})
+        wait_for(lambda: active() and len(active()['members']) == 1,
+                 timeout=120)
+        wait_for(lambda: manager.node.generations == 2 and
+                 manager.node.full, timeout=120)
+        manager.patch_namespaced_deployment('shr', 'default',
+                                            {'spec': {'replicas': 0}})
+        wait_for(lambda: active()['members'] == [], timeout=60)
+    finally:
+        manager.stop(timeout=20)
+    done = [e for e in events.records if e['ev'] == 'fence_done']
+    assert done and all(e['transport'] == 'shm' for e in done)
+    assert any(e['n'] == 1 and e['mode'] == 'shrink' for e in done) or \
+        any(e['n'] == 2 for e in done)
+    assert not any(e['ev'] == 'node_comm_break' for e in events.records)
