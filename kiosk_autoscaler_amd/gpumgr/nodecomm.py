@@ -43,7 +43,7 @@ class NodeComm(object):
 
     def __init__(self, manager, init_timeout=12.0, fence_timeout=30.0,
                  fallback='shm', fallback_after=2, transport=None,
-                 shrink=True, shrink_grace=0.1):
+                 shrink=True, shrink_grace=0.1, hang_grace=2.0):
         self.m = manager
         # after ``fallback_after`` consecutive failed generations the next
         # ones use the ``fallback`` transport (every rank switches in its
@@ -59,6 +59,15 @@ class NodeComm(object):
         # generation
         self.shrink_grace = float(shrink_grace)
         self.loss_t = None
+        # a failed connect / collective: every live rank reports it within
+        # ~its own timeout; ranks still silent `hang_grace` after the first
+        # report (or after the manager's own timeout) are hung -- a frozen
+        # process, a wedged device -- and are killed, so the next
+        # generation does not wait on them forever (a fence
+        # timeout marks a rank dead)
+        self.hang_grace = float(hang_grace)
+        self.verdict = None      # {'kind', 'reported', 't0', 'detail', 'seq'}
+        self.hung_kills = 0
         self.init_timeout = float(init_timeout)
         self.fence_timeout = float(fence_timeout)
         self.gen = 0
@@ -101,6 +110,7 @@ class NodeComm(object):
                 'fallback': self.fallback_used, 'failures': self.failures,
                 'failed_total': self.failed_total,
                 'generations': self.generations, 'shrinks': self.shrinks,
+                'hung_kills': self.hung_kills,
                 'last_error': self.last_error}
 
     def _bound(self):
@@ -165,11 +175,18 @@ class NodeComm(object):
                         self.members[r][0] for r in lost])
             else:
                 self.loss_t = None
-                if self.state in (INIT, SHRINK) and \
+                if self.state in (INIT, SHRINK) and self.verdict is None and \
                         now - self.t_start > self.init_timeout:
-                    self.break_('generation %d.%d %s timed out after %.1f s'
-                                % (self.gen, self.sub, self.state,
-                                   self.init_timeout), failed=True)
+                    self._open_verdict('init', set(self.ready_ranks), now,
+                                       'generation %d.%d %s timed out after '
+                                       '%.1f s' % (self.gen, self.sub,
+                                                   self.state,
+                                                   self.init_timeout))
+        if self.verdict is not None:
+            v = self.verdict
+            if len(v['reported']) >= len(self.members) or \
+                    now - v['t0'] >= self.hang_grace:
+                self._conclude(now)
         if self.ready and self.inflight is None and \
                 len(self.members) < len(self.m.slots) and \
                 not self.m._node_fence_runnable():
@@ -182,12 +199,49 @@ class NodeComm(object):
             members = self.candidates()
             if members:
                 self._start(members, now)
-        if self.inflight is not None and \
+        if self.inflight is not None and self.verdict is None and \
                 now - self.inflight['t'] > self.fence_timeout:
             seq = self.inflight['seq']
             for _, proc in self.members:
                 proc.pipe.send({'cmd': 'fence_abort', 'seq': seq})
-            self.break_('fence seq %d timed out' % seq, failed=True)
+            self._open_verdict('fence', set(), now - self.hang_grace,
+                               'fence seq %d timed out' % seq, seq=seq)
+            self._conclude(now)
+
+    def _open_verdict(self, kind, reported, now, detail, seq=None):
+        self.verdict = {'kind': kind, 'reported': set(reported), 't0': now,
+                        'detail': detail, 'seq': seq}
+
+    def _conclude(self, now):
+        """A failed generation / shrink / fence: kill the ranks that never
+        answered while others did, then drop the generation (a failure the
+        dead ranks explain is not counted toward the fallback)."""
+        v, self.verdict = self.verdict, None
+        silent = [r for r in range(len(self.members))
+                  if r not in v['reported']]
+        killed = []
+        if silent and len(silent) < len(self.members):
+            for r in silent:
+                index, proc = self.members[r]
+                if self._alive(proc):
+                    killed.append(index)
+                    self.hung_kills += 1
+                    self.m.events.emit('node_rank_hung', gen=self.gen,
+                                       slot=index, pid=proc.pid,
+                                       kind=v['kind'], detail=v['detail'])
+                    logger.error('Node communicator generation %d: slot %d '
+                                 '(pid %d) did not answer (%s); killing it.',
+                                 self.gen, index, proc.pid, v['detail'])
+                    try:
+                        proc.popen.kill()
+                    except OSError:
+                        pass
+        if v['kind'] == 'fence' and self.inflight is not None:
+            self.inflight['resource'].fence_wanted = True
+            self.inflight = None
+        reason = v['detail'] + (' (hung slot(s) %s killed)' % killed
+                                if killed else '')
+        self.break_(reason, failed=not killed)
 
     def _start(self, members, now):
         self.gen += 1
@@ -260,6 +314,7 @@ class NodeComm(object):
         is re-run on the next one)."""
         if self.state == NONE:
             return
+        self.verdict = None
         for _, proc in self.members:
             if self._alive(proc):
                 proc.pipe.send({'cmd': 'comm_abort', 'gen': self.gen})
@@ -314,13 +369,22 @@ class NodeComm(object):
                 return
             if not message.get('ok'):
                 what = 'shrink' if self.state == SHRINK else 'connect'
-                # a failed shrink is not a failed generation: the next full
-                # one starts once the lost slot has a process again
-                self.break_('rank %s failed to %s: %s' % (
-                    message.get('rank'), what, message.get('detail')),
-                    failed=self.state == INIT)
+                detail = 'rank %s failed to %s: %s' % (
+                    message.get('rank'), what, message.get('detail'))
+                if self.state == SHRINK:
+                    # a failed shrink is not a failed generation: the next
+                    # full one starts once the lost slot has a process again
+                    self.break_(detail, failed=False)
+                    return
+                if self.verdict is None:
+                    self._open_verdict('init', set(self.ready_ranks),
+                                       time.monotonic(), detail)
+                self.verdict['reported'].add(message.get('rank'))
                 return
             self.ready_ranks[message.get('rank')] = message
+            if self.verdict is not None:
+                self.verdict['reported'].add(message.get('rank'))
+                return
             if len(self.ready_ranks) == len(self.members):
                 shrunk = self.state == SHRINK
                 self.state = READY
@@ -346,18 +410,26 @@ class NodeComm(object):
             inflight = self.inflight
             if inflight is None or message.get('seq') != inflight['seq']:
                 return
-            self.inflight = None
             resource = inflight['resource']
             if not message.get('ok'):
-                resource.fence_wanted = True
                 if message.get('interrupted'):
-                    return          # a peer died: the shrink re-runs it
-                logger.warning('Node fence seq %s failed: %s',
-                               inflight['seq'], message.get('detail'))
-                self.m._fence_failed_node(resource, message)
-                self.break_('fence failed on rank %s' % message.get('rank'),
-                            failed=True)
+                    # a peer died: the shrink re-runs it
+                    self.inflight = None
+                    resource.fence_wanted = True
+                    return
+                if self.verdict is None:
+                    logger.warning('Node fence seq %s failed: %s',
+                                   inflight['seq'], message.get('detail'))
+                    self.m._fence_failed_node(resource, message)
+                    self._open_verdict(
+                        'fence', set(), time.monotonic(),
+                        'fence seq %s failed on rank %s: %s' % (
+                            inflight['seq'], message.get('rank'),
+                            message.get('detail')), seq=inflight['seq'])
+                self.verdict['reported'].add(message.get('rank'))
                 return
+            self.inflight = None
+            self.verdict = None
             self.m._fence_completed(resource, inflight['epoch'],
                                     inflight['members'], inflight['t'],
                                     message)

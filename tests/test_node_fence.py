@@ -236,6 +236,9 @@ class _FakeProc(object):
     def poll(self):
         return None
 
+    def kill(self):
+        pass
+
     def send(self, message):
         self.sent.append(message)
 
@@ -269,8 +272,13 @@ def test_node_comm_falls_back_after_failed_generations():
         init = procs[1].sent[-1]
         assert init['cmd'] == 'comm_init' and init['gen'] == gen
         assert 'transport' not in init
-        node.on_message(procs[1], {'ev': 'comm_ready', 'gen': gen, 'rank': 1,
-                                   'ok': False, 'detail': 'rccl refused'})
+        # every rank reports the failed connect: no rank is silent (hung),
+        # so the generation counts as failed
+        for rank in (1, 0):
+            node.on_message(procs[rank], {'ev': 'comm_ready', 'gen': gen,
+                                          'rank': rank, 'ok': False,
+                                          'detail': 'rccl refused'})
+        node.step()
         node.retry_at = 0.0
     assert [e['ev'] for e in manager.emitted].count('node_comm_fallback') == 1
     node.step()
@@ -287,9 +295,60 @@ def test_node_comm_falls_back_after_failed_generations():
     node.step()
     node.on_message(manager.standbys[0], {'ev': 'comm_ready', 'gen': 1,
                                           'rank': 0, 'ok': False})
+    node.step()
     node.retry_at = 0.0
     node.step()
     assert 'transport' not in manager.standbys[0].sent[-1]
+
+
+def test_node_comm_kills_a_rank_that_never_answers():
+    """SURVEY §5.3 (a fence timeout marks a rank dead): ranks 0 and 1
+    report a failed connect, rank 2 stays silent past the grace -- it is
+    hung (frozen process, wedged device) and is killed so the next
+    generation does not wait on it; the generation is not counted as a
+    transport failure (no fallback)."""
+    from kiosk_autoscaler_amd.gpumgr.nodecomm import NodeComm
+    manager = _FakeManager(3)
+    killed = []
+    for proc in manager.standbys.values():
+        proc.kill = (lambda p=proc: killed.append(p.pid))
+    node = NodeComm(manager, fallback='shm', fallback_after=1,
+                    hang_grace=0.05)
+    node.step()
+    for rank in (0, 1):
+        node.on_message(manager.standbys[rank], {
+            'ev': 'comm_ready', 'gen': 1, 'rank': rank, 'ok': False,
+            'detail': 'ncclCommInitRank timed out'})
+    node.step()
+    assert node.state == 'init' and not killed     # within the grace
+    time.sleep(0.06)
+    node.step()
+    assert killed == [102] and node.hung_kills == 1
+    hung = [e for e in manager.emitted if e['ev'] == 'node_rank_hung']
+    assert hung[0]['slot'] == 2 and hung[0]['kind'] == 'init'
+    assert node.failures == 0 and node.fallback_used is None
+    # a fence: rank 0 reports its all-reduce timed out, ranks 1-2 silent
+    # past the manager's timeout -> nobody answered but one: 1 and 2 killed
+    node.state = 'ready'
+    node.members = [(i, manager.standbys[i]) for i in range(3)]
+    killed[:] = []
+
+    class _Res(object):
+        fence_wanted = False
+        epoch = 0
+        namespace = 'ns'
+        name = 'r'
+        workers = {}
+    res = _Res()
+    node.inflight = {'resource': res, 'epoch': 1, 'seq': 7, 'members': [],
+                     't': time.monotonic()}
+    manager._fence_failed_node = lambda r, m: None
+    node.on_message(manager.standbys[0], {'ev': 'fenced', 'seq': 7,
+                                          'ok': False, 'rank': 0,
+                                          'detail': 'timed out'})
+    time.sleep(0.06)
+    node.step()
+    assert sorted(killed) == [101, 102] and res.fence_wanted
 
 
 def test_store_node_transport_three_ranks(redis_client):
