@@ -1159,3 +1159,40 @@ def test_gpu_shrink_and_regrow_with_real_workers(resp_server):
     assert any(e['n'] == 1 and e['mode'] == 'shrink' for e in done) or \
         any(e['n'] == 2 for e in done)
     assert not any(e['ev'] == 'node_comm_break' for e in events.records)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize('transport', ['shm', 'rccl-fake'])
+def test_frozen_rank_is_killed_and_membership_recovers(resp_server, tmp_path,
+                                                       transport):
+    """A standby frozen (SIGSTOP) before a fence: the live ranks' all-reduce
+    times out (FENCE_INIT_TIMEOUT), they report it, the frozen rank never
+    does -> the manager kills it (`node_rank_hung`), the slot gets a fresh
+    standby, the next generation is built and the READY set is fenced --
+    instead of every later generation waiting on the frozen rank."""
+    s, client, events, manager, scaler = _node_stack(
+        resp_server, transport, tmp_path, MAX_PODS='3', WARM_POOL='3',
+        FENCE_INIT_TIMEOUT='1.5')
+    manager.node.hang_grace = 1.0
+    try:
+        wait_for(lambda: manager.node.ready and manager.node.full,
+                 timeout=60)
+        frozen = manager.standbys[2]
+        os.kill(frozen.pid, signal.SIGSTOP)
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 1}})
+        hung = wait_for(lambda: [e for e in events.records
+                                 if e['ev'] == 'node_rank_hung'], timeout=30)
+        assert hung[0]['pid'] == frozen.pid and hung[0]['slot'] == 2
+        wait_for(lambda: frozen.popen.poll() is not None, timeout=10)
+        wait_for(lambda: _converged(manager, client) and
+                 len(_ready_ids(manager)) == 1, timeout=60)
+        assert manager.node.full and manager.node.fallback_used is None
+    finally:
+        try:
+            os.kill(frozen.pid, signal.SIGCONT)
+        except OSError:
+            pass
+        manager.stop(timeout=15)
+    breaks = [e for e in events.records if e['ev'] == 'node_comm_break']
+    assert breaks and not any(b['failed'] for b in breaks)
