@@ -40,7 +40,6 @@ namespace {
 constexpr int BM = 256, BKH = 32;
 constexpr int kRowBytes = BKH * 2;                 // 64 B per row per half
 constexpr int kSlots = 4;
-constexpr int kGroupM = 4;
 
 // Per-BN geometry.  LDS slot = A[256][32] + B[BN][32]; an operand half is
 // rows/16 DMA pieces of 16 rows x 64 B spread over the 8 waves.
@@ -178,7 +177,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
     uint16_t* __restrict__ C, const float* __restrict__ bias,
     const uint16_t* __restrict__ R, int M, int N, int K, int lda,
-    float* __restrict__ P, int* __restrict__ cnt) {
+    float* __restrict__ P, int* __restrict__ cnt, int group_m) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // split-K: blockIdx.y picks a K/gridDim.y slice (K is the slice length,
   // lda the full row stride); EPI_PARTIAL writes fp32 partials per slice
@@ -188,13 +187,15 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   const int tiles_n = N / BN;
   const int tiles_m = (M + BM - 1) / BM;
   const int ntiles = tiles_m * tiles_n;
-  // tile -> its origin: XCD-aware bijective remap, kGroupM-row grouping
+  // tile -> its origin: XCD-aware bijective remap, group_m-row grouping
+  // (consecutive tiles of an XCD walk group_m tile rows down one tile column
+  // before the next column: the B column is re-read from that XCD's L2)
   auto origin = [&](int t, int& om, int& on) {
     const int wg = xcd_remap(t, ntiles);
-    const int per_group = kGroupM * tiles_n;
+    const int per_group = group_m * tiles_n;
     const int group = wg / per_group;
-    const int first_m = group * kGroupM;
-    const int gsize = min(tiles_m - first_m, kGroupM);
+    const int first_m = group * group_m;
+    const int gsize = min(tiles_m - first_m, group_m);
     const int in_group = wg - group * per_group;
     om = (first_m + in_group % gsize) * BM;
     on = (in_group / gsize) * BN;
@@ -700,6 +701,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   }  // tile loop
 }
 
+// tile rows per group of the 256-row kernels' tile order (gemm_set_group_m)
+int g_group_m = 4;
+
 template <int EPI, int BN, int W>
 hipError_t configure256() {
   return hipFuncSetAttribute(
@@ -727,19 +731,19 @@ hipError_t launch256(const uint16_t* A, const uint16_t* B, uint16_t* C,
   switch (epilogue) {
     case EPI_NONE:
       hipLaunchKernelGGL((gemm256_kernel<EPI_NONE, BN, W>), grid, block, lds,
-                         stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr);
+                         stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr, g_group_m);
       break;
     case EPI_BIAS_GELU:
       hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_GELU, BN, W>), grid, block,
-                         lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr);
+                         lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr, g_group_m);
       break;
     case EPI_BIAS_RESIDUAL:
       hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_RESIDUAL, BN, W>), grid,
-                         block, lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr);
+                         block, lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr, g_group_m);
       break;
     case EPI_PARTIAL:
       hipLaunchKernelGGL((gemm256_kernel<EPI_PARTIAL, BN, W>), grid, block,
-                         lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr);
+                         lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr, g_group_m);
       break;
     default:
       return hipErrorInvalidValue;
@@ -765,7 +769,7 @@ void launch_persist_epi(const uint16_t* A, const uint16_t* B, uint16_t* C,
   constexpr int lds = Geo<256, 4>::kLdsBytes;
   hipLaunchKernelGGL((gemm256_kernel<EPI, 256, 4, 0, 1>), dim3(grid),
                      dim3(256), lds, stream, A, B, C, bias, R, M, N, K, K,
-                     nullptr, nullptr);
+                     nullptr, nullptr, g_group_m);
 }
 
 template <int EPI, int kMode>
@@ -777,7 +781,7 @@ hipError_t launch_fused4(const uint16_t* A, const uint16_t* B, uint16_t* C,
   constexpr int lds = Geo<256, 4>::kLdsBytes;
   hipLaunchKernelGGL((gemm256_kernel<EPI, 256, 4, kMode>),
                      dim3(blocks, splits), dim3(256), lds, stream, A, B, C,
-                     bias, R, M, N, K, lda, P, cnt);
+                     bias, R, M, N, K, lda, P, cnt, g_group_m);
   return hipGetLastError();
 }
 
@@ -982,6 +986,9 @@ int gemm256_splits(int M, int N, int K) {
 // last arriver re-reads both planes (6 % slower than 0 at 2048x4096x16384,
 // profiles/r1_gemm/gemm_w4_splitk_fused_ab.jsonl).
 int g_splitk_fused = 0;
+
+void gemm_set_group_m(int rows) { g_group_m = rows < 1 ? 1 : rows; }
+int gemm_group_m() { return g_group_m; }
 
 void gemm_set_splitk_fused(int mode) { g_splitk_fused = mode ? 1 : 0; }
 int gemm_splitk_fused() { return g_splitk_fused; }

@@ -77,6 +77,9 @@ size_t gemm256_splitk_workspace(int M, int N, int K);
 // slice, or (default, faster here) partial planes + the reduce kernel
 void gemm_set_splitk_fused(int mode);   // 0 reduce kernel, 1 in-launch
 int gemm_splitk_fused();
+// tile rows per group in the 256-row kernels' tile order (default 4)
+void gemm_set_group_m(int rows);
+int gemm_group_m();
 hipError_t launch_gemm256_splitk(const uint16_t* A, const uint16_t* B,
                                  uint16_t* C, const float* bias,
                                  const uint16_t* R, int M, int N, int K,

@@ -65,6 +65,9 @@ PYBIND11_MODULE(_kiosk_hip, m) {
         py::arg("mode"),
         "4-wave split-K combine: 0 = partial planes + reduce kernel, "
         "1 = in-launch by the last slice (both planes)");
+  m.def("gemm_set_group_m", &kiosk::gemm_set_group_m,
+        "tile rows per group of the 256-row GEMM tile order (A/B knob)");
+  m.def("gemm_group_m", &kiosk::gemm_group_m);
   m.def("gemm_splitk_fused", &kiosk::gemm_splitk_fused);
   m.attr("sum_blocks") = kiosk::kSumBlocks;
 

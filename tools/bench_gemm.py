@@ -25,7 +25,13 @@ def main():
     parser.add_argument('--only', default='',
                         help='comma-separated function names to time '
                              '(default: all)')
+    parser.add_argument('--group-m', default='',
+                        help='comma-separated tile-row group sizes of the '
+                             '256-row kernels: each adds <name>_gm<G> arms '
+                             'of the 4-wave kernels (A/B in one process)')
     args = parser.parse_args()
+    group_ms = [int(g) for g in args.group_m.split(',') if g]
+    default_gm = mod.gemm_group_m()
     for spec in args.shapes.split(','):
         M, N, K = (int(v) for v in spec.split('x'))
         a = (torch.rand(M, K, device='cuda') * 2 - 1).to(torch.bfloat16)
@@ -107,6 +113,14 @@ def main():
             fns['native256splitk_fused'] = ours_splitk_fused
             fns['native256splitk_reduce'] = ours_splitk_reduce
 
+        for gm in group_ms:
+            for base in ('native256w4', 'native256w4_gelu'):
+                if base in fns:
+                    def arm(fn=fns[base], gm=gm):
+                        mod.gemm_set_group_m(gm)
+                        fn()
+                        mod.gemm_set_group_m(default_gm)
+                    fns['%s_gm%d' % (base, gm)] = arm
         if args.only:
             keep = set(args.only.split(','))
             fns = {k: v for k, v in fns.items() if k in keep}
