@@ -312,6 +312,31 @@ def test_gemm256_persistent_walks_many_tiles(mod, M, N, K, epilogue):
     assert torch.equal(c, c4)
 
 
+@pytest.mark.parametrize('M,N,K', [(1280, 2304, 512), (2048, 4096, 256)])
+def test_gemm256_group_m_only_reorders_tiles(mod, M, N, K):
+    """The tile-row group size (gemm_set_group_m) changes which tiles run
+    together, never a tile's result: every group size -- including a ragged
+    last group (5 tile rows) -- is bit-identical to the default, for the
+    one-tile and the persistent 4-wave grids."""
+    from kiosk_autoscaler_amd.ops import kernels
+    a = rand_bf16(M, K, seed=31)
+    b = rand_bf16(N, K, scale=0.1, seed=32)
+    bias = torch.randn(N, device='cuda')
+    default = mod.gemm_group_m()
+    ref = kernels.gemm(a, b, bias=bias, epilogue='gelu', variant='256w4')
+    try:
+        for gm in (1, 2, 3, 8, 64):
+            mod.gemm_set_group_m(gm)
+            assert mod.gemm_group_m() == gm
+            for variant in ('256w4', '256w4p'):
+                c = kernels.gemm(a, b, bias=bias, epilogue='gelu',
+                                 variant=variant)
+                assert torch.equal(c, ref), (gm, variant)
+    finally:
+        mod.gemm_set_group_m(default)
+    assert mod.gemm_group_m() == default
+
+
 def test_gemm256_identity(mod):
     from kiosk_autoscaler_amd.ops import kernels
     M = K = 512
