@@ -6,6 +6,7 @@
 #   bash tools/gpu_round2_variants.sh D   -> INTERVAL=0.1 (reference loop, fast cadence)
 #   bash tools/gpu_round2_variants.sh E   -> POOL_IDLE_RELEASE_S=3 (no GPU held when idle)
 #   bash tools/gpu_round2_variants.sh F   -> WARM_POOL_MODE=context (no HBM held)
+#   bash tools/gpu_round2_variants.sh G   -> configs 3/5 shapes: strict, 2 queues, jobs KPP=4
 set -o pipefail
 OUT=${OUT:-gpurun_out/r2_variants}
 mkdir -p $OUT
@@ -24,6 +25,11 @@ if [ "$1" = "A" ]; then
   run strict 200 --gpus 1 --steps 10 --warmup 1 --policy strict --budget-s 180 && \
   run two_queues 200 --gpus 1 --steps 10 --warmup 1 --queues predict,track --budget-s 180 && \
   run idle_interval_0.1 200 --gpus 1 --steps 10 --warmup 1 --idle-interval 0.1 --budget-s 180
+elif [ "$1" = "G" ]; then
+  run strict 200 --gpus 1 --steps 10 --warmup 1 --policy strict --budget-s 180 && \
+  run two_queues 200 --gpus 1 --steps 10 --warmup 1 --queues predict,track --budget-s 180 && \
+  run job_kpp4_strict 260 --gpus 1 --steps 6 --warmup 1 --resource-type job --kpp 4 --on 8 --lam-per-gpu 1.0 --policy strict --budget-s 240 && \
+  run job_kpp4_reference 260 --gpus 1 --steps 6 --warmup 1 --resource-type job --kpp 4 --on 8 --lam-per-gpu 1.0 --budget-s 240 --drain-timeout 20
 elif [ "$1" = "D" ]; then
   # the reference's own loop at INTERVAL=0.1: only viable with a ~1 ms
   # actuator (with a pod start the same policy thrashes: see the
