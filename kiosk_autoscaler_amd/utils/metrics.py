@@ -8,9 +8,12 @@ the manager daemon can serve ``/metrics``:
   depth and in-flight keys per queue, desired / current workers, tick
   duration, scale events, assignment -> READY latency, worker exits by
   outcome, requeued items, watchdog kills, fence epochs and their duration,
-  node-communicator generations / breaks / init time, free-HBM sizing;
+  node-communicator generations / shrinks / breaks / fallbacks / hung-rank
+  kills and their init times, process spawns (zygote fork or exec),
+  free-HBM sizing;
 * at scrape time from the GPU manager: workers per state, standbys
-  (booted / booting), GPU slots.
+  (booted / booting), GPU slots, READY vs fenced (available) replicas per
+  resource, the node communicator's state and rank count.
 
 ``prometheus_client`` is imported only when the exporter is enabled.
 """
@@ -60,8 +63,22 @@ class PrometheusExporter(object):
                                        buckets=LATENCY_BUCKETS)
         self.comm_builds = Counter('kiosk_node_comm_generations',
                                    'node communicators built (pool boot, '
-                                   'then one per slot-process death)',
+                                   'regrows, rebuilds after a break)',
                                    registry=r)
+        self.comm_shrinks = Counter('kiosk_node_comm_shrinks', 'lost ranks '
+                                    'shrunk out of the node communicator',
+                                    registry=r)
+        self.comm_shrink_seconds = Histogram(
+            'kiosk_node_comm_shrink_seconds', 'slowest survivor of a shrink',
+            registry=r, buckets=LATENCY_BUCKETS)
+        self.comm_fallbacks = Counter('kiosk_node_comm_fallbacks', 'switches '
+                                      'to the fallback transport',
+                                      ['transport'], registry=r)
+        self.hung_kills = Counter('kiosk_node_rank_hung_kills', 'ranks '
+                                  'killed for not answering a failed '
+                                  'connect / fence', registry=r)
+        self.spawns = Counter('kiosk_process_spawns', 'worker / standby '
+                              'processes started', ['via'], registry=r)
         self.comm_breaks = Counter('kiosk_node_comm_breaks', 'node '
                                    'communicator generations dropped',
                                    ['failed'], registry=r)
@@ -123,9 +140,19 @@ class PrometheusExporter(object):
             if record.get('wall_s') is not None:
                 self.fence_seconds.observe(record['wall_s'])
         elif ev == 'node_comm_ready':
-            self.comm_builds.inc()
-            self.comm_init_seconds.observe(
-                float(record.get('init_ms') or 0.0) / 1e3)
+            seconds = float(record.get('init_ms') or 0.0) / 1e3
+            if record.get('mode') == 'shrink':
+                self.comm_shrinks.inc()
+                self.comm_shrink_seconds.observe(seconds)
+            else:
+                self.comm_builds.inc()
+                self.comm_init_seconds.observe(seconds)
+        elif ev == 'node_comm_fallback':
+            self.comm_fallbacks.labels(str(record.get('transport'))).inc()
+        elif ev == 'node_rank_hung':
+            self.hung_kills.inc()
+        elif ev == 'process_spawn':
+            self.spawns.labels(str(record.get('via') or 'exec')).inc()
         elif ev == 'node_comm_break':
             self.comm_breaks.labels(
                 str(bool(record.get('failed'))).lower()).inc()
@@ -165,6 +192,30 @@ class _ManagerCollector(object):
         yield standbys
         yield GaugeMetricFamily('kiosk_gpu_slots', 'GPU slots managed',
                                 value=len(status.get('slots', [])))
+        replicas = GaugeMetricFamily(
+            'kiosk_replicas', 'per resource: READY workers vs the READY '
+            'workers of the last fenced membership (available)',
+            labels=['resource', 'kind'])
+        for res in status.get('resources', []):
+            st = res.get('status') or {}
+            name = res['metadata']['name']
+            replicas.add_metric([name, 'ready'],
+                                st.get('ready_replicas') or 0)
+            replicas.add_metric([name, 'available'],
+                                st.get('available_replicas') or 0)
+        yield replicas
+        node = status.get('node_comm')
+        if node:
+            yield GaugeMetricFamily('kiosk_node_comm_ranks', 'ranks of the '
+                                    'current node communicator',
+                                    value=node.get('ranks') or 0)
+            state = GaugeMetricFamily('kiosk_node_comm_state', 'node '
+                                      'communicator state (1 = current)',
+                                      labels=['state'])
+            for name in ('none', 'init', 'ready', 'shrink'):
+                state.add_metric([name], 1 if node.get('state') == name
+                                 else 0)
+            yield state
 
 
 def attach(events, port, manager=None, addr='0.0.0.0'):

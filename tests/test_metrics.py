@@ -31,13 +31,25 @@ def test_exporter_counts_events_and_serves_http():
     events.emit('worker_exit', code=-9, killed='no progress')
     events.emit('requeue', items=2)
     events.emit('fence_done', transport='rccl', wall_s=0.05)
-    events.emit('node_comm_ready', gen=1, n=8, init_ms=1900.0)
+    events.emit('node_comm_ready', gen=1, n=8, init_ms=1900.0, mode='init')
+    events.emit('node_comm_ready', gen=1, sub=1, n=7, init_ms=3.0,
+                mode='shrink')
     events.emit('node_comm_break', gen=1, failed=False)
+    events.emit('node_comm_fallback', gen=2, transport='shm')
+    events.emit('node_rank_hung', gen=2, slot=3, pid=1)
+    events.emit('process_spawn', pid=1, via='zygote')
+    events.emit('process_spawn', pid=2)
     events.emit('hbm_sizing', gpu=0, hbm_free=2.8e11, keys_per_pod=4)
     text = generate_latest(exporter.registry).decode()
     for line in ('kiosk_node_comm_generations_total 1.0',
                  'kiosk_node_comm_breaks_total{failed="false"} 1.0',
                  'kiosk_node_comm_init_seconds_count 1.0',
+                 'kiosk_node_comm_shrinks_total 1.0',
+                 'kiosk_node_comm_shrink_seconds_count 1.0',
+                 'kiosk_node_comm_fallbacks_total{transport="shm"} 1.0',
+                 'kiosk_node_rank_hung_kills_total 1.0',
+                 'kiosk_process_spawns_total{via="zygote"} 1.0',
+                 'kiosk_process_spawns_total{via="exec"} 1.0',
                  'kiosk_hbm_free_bytes{gpu="0"} 2.8e+11',
                  'kiosk_keys_per_pod_effective{gpu="0"} 4.0'):
         assert line in text, line
@@ -51,7 +63,9 @@ def test_exporter_counts_events_and_serves_http():
                  'kiosk_requeued_items_total 2.0',
                  'kiosk_fence_epochs_total{transport="rccl"} 1.0',
                  'kiosk_gpu_slots 3.0',
-                 'kiosk_workers{resource="w",state="ready"} 0.0'):
+                 'kiosk_workers{resource="w",state="ready"} 0.0',
+                 'kiosk_replicas{kind="ready",resource="w"} 0.0',
+                 'kiosk_replicas{kind="available",resource="w"} 0.0'):
         assert line in text, line
     if exporter.port:
         body = urllib.request.urlopen(
