@@ -511,6 +511,15 @@ class GpuManager(object):
     # ------------------------------------------------------------------
     def start(self):
         if self._thread is None:
+            if self.node is not None:
+                # shared-memory segments of generations whose ranks all died
+                # before joining (a crashed earlier manager's node)
+                from ..parallel.nodefence import sweep_stale_shm
+                stale = sweep_stale_shm(
+                    older_than=max(300.0, 5 * self.node.init_timeout))
+                if stale:
+                    logger.warning('Removed %d stale node-communicator '
+                                   'segment(s): %s', len(stale), stale)
             with self.lock:
                 self._start_zygote()
                 self._refill_pool()

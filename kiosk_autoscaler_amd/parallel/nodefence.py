@@ -221,6 +221,34 @@ class ShmNodeTransport(object):
             comm.close()
 
 
+def sweep_stale_shm(dirs=None, older_than=300.0, now=None):
+    """Remove ``kiosk-shm-*`` segments left behind by generations whose
+    ranks all died before joining (a joined generation unlinks its file at
+    once, so nothing live is older than its ``FENCE_INIT_TIMEOUT``).  The
+    manager calls it at start; returns the paths removed."""
+    now = time.time() if now is None else now
+    if dirs is None:
+        dirs = (os.environ.get('KIOSK_SHM_DIR') or '/dev/shm', '/tmp')
+    removed = []
+    for directory in dirs:
+        try:
+            names = os.listdir(directory)
+        except OSError:
+            continue
+        for name in names:
+            if not name.startswith('kiosk-shm-'):
+                continue
+            path = os.path.join(directory, name)
+            try:
+                if now - os.stat(path).st_mtime < older_than:
+                    continue
+                os.unlink(path)
+                removed.append(path)
+            except OSError:
+                pass
+    return removed
+
+
 class GlooNodeTransport(object):
     """One persistent gloo group per generation over a FileStore (CPU)."""
 

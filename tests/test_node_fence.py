@@ -1196,3 +1196,23 @@ def test_frozen_rank_is_killed_and_membership_recovers(resp_server, tmp_path,
         manager.stop(timeout=15)
     breaks = [e for e in events.records if e['ev'] == 'node_comm_break']
     assert breaks and not any(b['failed'] for b in breaks)
+
+
+def test_sweep_stale_shm_segments(tmp_path):
+    """Segments a dead generation left behind (never joined, so never
+    unlinked) are removed once older than the bound; fresh ones and other
+    files stay."""
+    from kiosk_autoscaler_amd.parallel.nodefence import sweep_stale_shm
+    old = tmp_path / 'kiosk-shm-123-0-deadbeefdeadbeef'
+    old_child = tmp_path / 'kiosk-shm-123-0-deadbeefdeadbeef.s1'
+    fresh = tmp_path / 'kiosk-shm-456-1-0123456789abcdef'
+    other = tmp_path / 'unrelated'
+    for path in (old, old_child, fresh, other):
+        path.write_bytes(b'x')
+    t = time.time()
+    for path in (old, old_child, other):
+        os.utime(path, (t - 1000, t - 1000))
+    removed = sweep_stale_shm([str(tmp_path), str(tmp_path / 'missing')],
+                              older_than=300.0, now=t)
+    assert sorted(removed) == sorted([str(old), str(old_child)])
+    assert fresh.exists() and other.exists() and not old.exists()
