@@ -151,6 +151,23 @@ __device__ __forceinline__ void mfma_drain() {
 #ifndef KIOSK_W4_SPREAD
 #define KIOSK_W4_SPREAD 1
 #endif
+// Stagger the four waves' DMA issue slots against each other: without it
+// all four issue their pieces at the same MFMA indices right after the
+// barrier and queue on the CU's one texture-address path.  2 (default):
+// waves 2 and 3 issue KIOSK_W4_STAGGER_OFF MFMAs later -- +2.0 % on the
+// bias+GELU up-projection, +1.2 % on the split-K down-projection, +0.4-0.6 %
+// at 8192^3 (profiles/r3_stagger/, 5 interleaved rounds); 4 = waves 0..3
+// at offsets 0, 1, 3, 4 (slower); 0 = off.  The persistent kernel keeps one
+// schedule (two copies of its loop spill).
+#ifndef KIOSK_W4_STAGGER
+#define KIOSK_W4_STAGGER 2
+#endif
+#ifndef KIOSK_W4_STAGGER_OFF
+#define KIOSK_W4_STAGGER_OFF 3     // MFMAs the later half of the waves lags
+#endif
+#ifndef KIOSK_W4_STAGGER_SEL
+#define KIOSK_W4_STAGGER_SEL 1     // 0: odd waves lag; 1: waves 2, 3 lag
+#endif
 // Counted waits go through the builtin (not inline asm) so hipcc's waitcnt
 // pass sees them and adds no conservative lgkmcnt(0) of its own.  gfx9
 // encoding: vmcnt[3:0] | expcnt[6:4] (7 = no wait) | lgkmcnt[11:8] |
@@ -332,7 +349,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   // half-steps-in-flight probe shows that is enough.  LDS rows are 128 B
   // with 16-B chunk c of row r at c ^ ((r >> 1) & 7): every ds_read_b128
   // lane group then covers 16 distinct bank slots.
-  auto mainloop_w4 = [&](int steps, bool prefetched) {
+  auto mainloop_w4 = [&](auto phase, int steps, bool prefetched) {
+    // this wave's DMA slot offset within a half-step (KIOSK_W4_STAGGER)
+    constexpr int kOff = decltype(phase)::value;
     constexpr int kUnit = BM * 128;
     int voff_a[8], voff_b[8];
 #pragma unroll
@@ -417,7 +436,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
           // MFMAs (~256 cycles) to return before the next half-step's
           // lgkmcnt(0) + barrier
           if constexpr (!(KIOSK_GEMM_ABLATE & 1))
-            if (u % 6 == 0 && u < 48) dma(h + 4, u / 6);
+            if (u >= kOff && (u - kOff) % 6 == 0 && (u - kOff) < 48)
+              dma(h + 4, (u - kOff) / 6);
           if constexpr (!(KIOSK_GEMM_ABLATE & 2))
             if (u % 3 == 1 && u < 48) read(HH(), tn, u / 3, wb_next, xa_next);
         }
@@ -483,7 +503,31 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
   };
 
   if constexpr (kWaves == 4) {
-    mainloop_w4(K / 64, kPersist && it > 0);
+    using P0 = std::integral_constant<int, 0>;
+    if constexpr (KIOSK_W4_STAGGER == 2 && !kPersist) {
+      if (KIOSK_W4_STAGGER_SEL ? (wave >> 1) & 1 : wave & 1)
+        mainloop_w4(std::integral_constant<int, KIOSK_W4_STAGGER_OFF>(),
+                    K / 64, kPersist && it > 0);
+      else
+        mainloop_w4(P0(), K / 64, kPersist && it > 0);
+    } else if constexpr (KIOSK_W4_STAGGER == 4 && !kPersist) {
+      switch (wave & 3) {
+        case 0: mainloop_w4(P0(), K / 64, kPersist && it > 0); break;
+        case 1:
+          mainloop_w4(std::integral_constant<int, 1>(), K / 64,
+                      kPersist && it > 0);
+          break;
+        case 2:
+          mainloop_w4(std::integral_constant<int, 3>(), K / 64,
+                      kPersist && it > 0);
+          break;
+        default:
+          mainloop_w4(std::integral_constant<int, 4>(), K / 64,
+                      kPersist && it > 0);
+      }
+    } else {
+      mainloop_w4(P0(), K / 64, kPersist && it > 0);
+    }
   } else {
 #pragma unroll
     for (int h = 0; h < kSlots; ++h) stage(h);

@@ -27,6 +27,11 @@ int main(int argc, char** argv) {
   const int N = argc > 2 ? atoi(argv[2]) : 8192;
   const int K = argc > 3 ? atoi(argv[3]) : 8192;
   const int waves = argc > 4 ? atoi(argv[4]) : 4;
+  // epilogue (0 none, 1 bias+GELU, 2 bias+residual) and split-K slices
+  // (>= 2: the 4-wave partial kernel + the reduce, as the worker's
+  // down-projection runs)
+  const int epi = argc > 5 ? atoi(argv[5]) : 0;
+  const int splits = argc > 6 ? atoi(argv[6]) : 1;
   const int iters = 20;
   std::vector<uint16_t> h(static_cast<size_t>(std::max(M, N)) * K);
   uint32_t x = 12345;
@@ -45,6 +50,16 @@ int main(int argc, char** argv) {
                   hipMemcpyHostToDevice));
   CHECK(hipMemcpy(B, h.data(), static_cast<size_t>(N) * K * 2,
                   hipMemcpyHostToDevice));
+  float* bias = nullptr;
+  uint16_t* R = nullptr;
+  float* ws = nullptr;
+  const size_t ws_bytes =
+      splits > 1 ? static_cast<size_t>(splits) * M * N * 4 + 65536 : 0;
+  CHECK(hipMalloc(&bias, static_cast<size_t>(N) * 4));
+  CHECK(hipMemset(bias, 0, static_cast<size_t>(N) * 4));
+  CHECK(hipMalloc(&R, static_cast<size_t>(M) * N * 2));
+  CHECK(hipMemset(R, 0, static_cast<size_t>(M) * N * 2));
+  if (ws_bytes) CHECK(hipMalloc(&ws, ws_bytes));
   CHECK(kiosk::gemm256_prepare());
   hipEvent_t t0, t1;
   CHECK(hipEventCreate(&t0));
@@ -53,8 +68,11 @@ int main(int argc, char** argv) {
   for (int r = 0; r < 7; ++r) {
     CHECK(hipEventRecord(t0, 0));
     for (int i = 0; i < iters; ++i)
-      CHECK(kiosk::launch_gemm256(A, B, C, nullptr, nullptr, M, N, K,
-                                  kiosk::EPI_NONE, 0, 256, waves));
+      CHECK(splits > 1
+                ? kiosk::launch_gemm256_splitk(A, B, C, bias, R, M, N, K, epi,
+                                               splits, ws, ws_bytes, 0)
+                : kiosk::launch_gemm256(A, B, C, bias, R, M, N, K, epi, 0,
+                                        256, waves));
     CHECK(hipEventRecord(t1, 0));
     CHECK(hipEventSynchronize(t1));
     float ms;
@@ -62,9 +80,9 @@ int main(int argc, char** argv) {
     ms /= iters;
     if (r > 0 && ms < best) best = ms;
   }
-  printf("{\"ablate\": %d, \"waves\": %d, \"shape\": [%d, %d, %d], "
-         "\"ms\": %.4f, \"tflops\": %.1f}\n",
-         KIOSK_GEMM_ABLATE, waves, M, N, K, best,
+  printf("{\"ablate\": %d, \"waves\": %d, \"epi\": %d, \"splits\": %d, "
+         "\"shape\": [%d, %d, %d], \"ms\": %.4f, \"tflops\": %.1f}\n",
+         KIOSK_GEMM_ABLATE, waves, epi, splits, M, N, K, best,
          2.0 * M * N * K / (best * 1e-3) / 1e12);
   return 0;
 }
