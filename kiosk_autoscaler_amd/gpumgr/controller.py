@@ -332,10 +332,14 @@ class GpuManager(object):
         # persistent node-wide communicator: needs one long-lived process
         # per slot (a standby for every GPU, recycled workers); otherwise
         # every epoch bootstraps its own communicator (round-1 mode).  In
-        # every pool mode: standbys that hold no GPU (context / import, and
-        # the cold spawns after a deep-idle park) run it over the native
-        # shared-memory transport instead of RCCL, which would need a
-        # hardware queue and ~0.8 GiB of HBM per GPU (profiles/r2_hbm_hold)
+        # every pool mode: standbys that hold no GPU (context / import) run
+        # it over the native shared-memory transport instead of RCCL, which
+        # would need a hardware queue and ~0.8 GiB of HBM per GPU
+        # (profiles/r2_hbm_hold); so does a pool that parks (deep idle),
+        # whose every wake is a new set of processes -- a new RCCL
+        # communicator per wake cost 2.1 s on average (5.7 s max) at one
+        # rank (profiles/r3_tiers/deep_idle_v2.json), the shared-memory one
+        # a millisecond
         self.fence_comm = fence_comm
         self.node = None
         if (fence and fence_comm == 'node' and self.recycle and
@@ -343,7 +347,7 @@ class GpuManager(object):
                 self.pool_size >= len(self.slots)):
             transport = fence_transport
             if transport is None and pool_template.backend == 'hip' and \
-                    pool_mode != 'device':
+                    (pool_mode != 'device' or self.pool_idle_release_s > 0):
                 transport = 'shm'
             self.node = NodeComm(self, fence_timeout=min(fence_timeout, 30.0),
                                  init_timeout=fence_init_timeout,

@@ -585,3 +585,22 @@ def test_gpu_zygote_cold_spawn(resp_server, engine):
     print('zygote cold spawn (%s): assign -> READY %s s' % (
         engine, [round(e['ready_s'], 3) for e in ups]))
     assert all(e['ready_s'] < 10.0 for e in ups)
+
+
+@pytest.mark.parametrize('mode,park,expected', [
+    ('device', 0.0, None),      # long-lived GPU standbys: RCCL (FENCE)
+    ('device', 3.0, 'shm'),     # deep idle: new processes every wake
+    ('context', 0.0, 'shm'),    # standbys without a GPU queue / HBM
+    ('import', 0.0, 'shm'),
+])
+def test_node_transport_follows_pool_mode(mode, park, expected):
+    """The node communicator runs over RCCL only where its ranks are
+    long-lived GPU processes; a pool that parks (every wake a new set of
+    processes, a new multi-second RCCL init each) or whose standbys hold no
+    GPU queue fences over the native shared-memory transport."""
+    slots = [gpus.GpuSlot(i, str(i)) for i in range(2)]
+    tpl = gpumgr.WorkerTemplate(queues=['q'], backend='hip')
+    manager = gpumgr.GpuManager(slots, pool_size=2, pool_template=tpl,
+                                pool_mode=mode, pool_idle_release_s=park)
+    assert manager.node is not None
+    assert manager.node.transport_override == expected
