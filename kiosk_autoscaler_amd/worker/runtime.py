@@ -135,7 +135,24 @@ class QueueConsumer(object):
     def queues_empty(self):
         return all(self.redis.llen(q) == 0 for q in self.queues)
 
-    def complete(self, pkey):
+    def complete(self, pkey, item=None, mapping=None):
+        """Drop the in-flight key; with ``mapping``, write the job's result
+        hash in the same MULTI/EXEC, so no observer (the tally, a test) sees
+        a job ``done`` whose processing key still counts as work -- and one
+        round trip instead of two.  A connection error falls back to the
+        retrying single commands (both are idempotent)."""
+        if mapping is None:
+            self.redis.delete(pkey)
+            return
+        try:
+            pipe = self.redis.pipeline(transaction=True)
+            pipe.hset(item, mapping=mapping)
+            pipe.delete(pkey)
+            pipe.execute()
+            return
+        except (AttributeError, redis_errors.ConnectionError):
+            pass
+        self.redis.hset(item, mapping=mapping)
         self.redis.delete(pkey)
 
 
@@ -456,6 +473,7 @@ class WorkerRuntime(object):
                   outputs=None):
         cfg = self.config
         for index, (queue, item, pkey, params, fields) in enumerate(jobs):
+            mapping = None
             if fields:      # results go into the job hash (kiosk convention)
                 mapping = {
                     'status': 'done', 'worker': cfg.worker_id,
@@ -467,8 +485,7 @@ class WorkerRuntime(object):
                 else:
                     mapping.update({str(k): str(v) for k, v in
                                     outputs[index].items()})
-                self.redis.hset(item, mapping=mapping)
-            consumer.complete(pkey)
+            consumer.complete(pkey, item, mapping)
             self.keys_done += 1
             self._emit_event('key_done', item=item, queue=queue, t_ns=t_done,
                              gpu=cfg.slot, compute_ms=result['ms'],

@@ -83,7 +83,11 @@ def test_scale_up_process_scale_down(stack):
     assert client.llen('predict') == 0
     assert not list(client.scan_iter(match='processing-predict:*'))
     view = manager.list_namespaced_deployment('default').items[0]
-    assert view.spec.replicas == 1 and view.status.available_replicas == 1
+    assert view.spec.replicas == 1
+    # available = fenced; the first key is served ungated, so under load
+    # the keys can finish before the fence does
+    wait_for(lambda: manager.list_namespaced_deployment('default')
+             .items[0].status.available_replicas == 1)
     workers = [r for r in manager.status()['resources']][0]['workers']
     assert workers[0]['from_pool'] is True
     # fence for the 1-member set completes and is published

@@ -511,7 +511,10 @@ def test_eight_workers_churn_and_death(resp_server, transport, tmp_path):
         return scaler.scale('default', 'deployment', 'worker', 0, 8, 1)
 
     def all_done(items):
-        return all(client.hget(i, 'status') == 'done' for i in items)
+        # a worker marks the hash done before it DELs its processing key:
+        # the next tick must not see that key as work
+        return (all(client.hget(i, 'status') == 'done' for i in items) and
+                not list(client.scan_iter(match='processing-*')))
 
     try:
         assert manager.node is not None

@@ -133,7 +133,9 @@ def test_plugin_through_the_manager_with_recycling(resp_server):
             client.hset(item, mapping={'status': 'new', 'payload': text})
             client.lpush('predict', item)
             assert scaler.scale('default', 'deployment', 'plug', 0, 1, 1) == 1
-            until(lambda: client.hget(item, 'status') == 'done')
+            # done is written before the processing key is DELeted
+            until(lambda: client.hget(item, 'status') == 'done' and
+                  not list(client.scan_iter(match='processing-*')))
             assert client.hget(item, 'output') == 'rev:' + text[::-1]
             assert scaler.scale('default', 'deployment', 'plug', 0, 1, 1) == 0
             until(lambda: not [w for r in manager.resources.values()
