@@ -663,6 +663,13 @@ def base_line(args, episodes, elapsed):
             'idle_interval_s': args.idle_interval,
             'warm_pool_mode': args.pool_mode,
             'worker_recycle': not args.no_recycle,
+            # deep idle (standbys exit after this many idle seconds; 0 =
+            # kept) and the arrival wake's queue-read period
+            'pool_idle_release_s': float(os.environ.get(
+                'POOL_IDLE_RELEASE_S') or 0.0),
+            'pool_wake_poll_s': (float(os.environ.get('POOL_WAKE_POLL_S')
+                                       or 0.05) if os.environ.get(
+                                           'POOL_IDLE_RELEASE_S') else None),
         },
         'steps_requested': args.steps,
     }
@@ -755,6 +762,15 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         'queue_wait_mean_s': _r(summary['queue_wait_mean_s']),
         'keys_done': summary['keys_done'], 'keys': summary['keys'],
         'stranded_cycles': sum(1 for ep in episodes if ep['stranded']),
+        # deep idle: times the pool was released, and refilled by a key's
+        # arrival ahead of the scale-up tick (POOL_WAKE_POLL_S)
+        'pool_parks': sum(1 for e in events if e.get('ev') == 'pool_parked'),
+        'pool_arrival_wakes': sum(1 for e in events
+                                  if e.get('ev') == 'pool_resumed' and
+                                  e.get('reason') == 'arrival'),
+        'cold_spawned_workers': sum(1 for e in events
+                                    if e.get('ev') == 'worker_assigned' and
+                                    e.get('from_pool') is False),
         'cold_spawn_latency_s': _r((cold or {}).get('latency_s')),
         'cold_spawn_actuation_s': _r((cold or {}).get('actuation_s')),
         'event_busy_wall_pct': _r(100.0 * summary['gpu_busy_s'] /

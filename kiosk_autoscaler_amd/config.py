@@ -155,6 +155,10 @@ EXTRA_DEFAULTS = (
     # s with no demand after which the standbys exit (0 = keep them): the
     # node then holds no GPU, the next scale-up is a cold spawn (~0.13 s)
     ('POOL_IDLE_RELEASE_S', float, 0.0),
+    # with POOL_IDLE_RELEASE_S: s between queue-length reads while no worker
+    # runs; a new key refills a parked pool before the scale-up tick (the
+    # decision still waits for the tick; 0 = wake at the scale-up only)
+    ('POOL_WAKE_POLL_S', float, 0.05),
     # s a recycled standby keeps its engine (weights, arena, graphs; ~1.2
     # GiB of the idle GPU's 2.6) without an assignment; then it frees it and
     # keeps context, queue and node communicator (0 = keep forever)

@@ -127,7 +127,11 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
                          fence_fallback=settings.FENCE_FALLBACK,
                          fence_fallback_after=settings.FENCE_FALLBACK_AFTER,
                          fence_init_timeout=settings.FENCE_INIT_TIMEOUT,
-                         zygote=settings.WORKER_ZYGOTE)
+                         zygote=settings.WORKER_ZYGOTE,
+                         pool_wake_poll_s=settings.POOL_WAKE_POLL_S,
+                         # the tick that scales for an arrival comes within
+                         # INTERVAL (+ the tick itself) of it
+                         pool_wake_hold_s=1.5 * float(settings.INTERVAL) + 1.0)
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

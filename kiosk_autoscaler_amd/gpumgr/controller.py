@@ -279,6 +279,18 @@ class GpuManager(object):
         recycle: a cleanly drained worker (or a finished job worker) frees
             its HBM and becomes its GPU's standby again, keeping the HIP
             context -- no process re-boot before the next scale-up there.
+        pool_idle_release_s: deep idle -- with no demand for this long the
+            standbys exit and the node holds no GPU (0 = never).
+        pool_wake_poll_s: while the pool is parked (or idling toward it),
+            read the managed queues' lengths this often; a new arrival
+            refills the pool at once instead of at the scale-up tick.  The
+            scaling decision is untouched (it stays with the INTERVAL tick):
+            the standbys only get the rest of the tick phase -- INTERVAL / 2
+            on average -- to open their devices, so the scale-up finds them
+            booted (0 = off).
+        pool_wake_hold_s: an arrival-woken pool is kept at least this long
+            (the autoscaler's tick period and a margin: the tick that scales
+            for the key must find it), whatever ``pool_idle_release_s``.
     """
 
     def __init__(self, slots, redis_client=None, pool_size=0,
@@ -289,7 +301,7 @@ class GpuManager(object):
                  fence_comm='node', pool_idle_release_s=0.0,
                  fence_fallback='shm', fence_fallback_after=2,
                  fence_init_timeout=12.0, fence_transport=None,
-                 zygote=False):
+                 zygote=False, pool_wake_poll_s=0.0, pool_wake_hold_s=0.0):
         self.slots = list(slots)
         self.redis = redis_client
         self.pool_size = max(0, int(pool_size))
@@ -309,6 +321,15 @@ class GpuManager(object):
         self.pool_idle_release_s = float(pool_idle_release_s or 0.0)
         self.pool_parked = False
         self._last_demand = time.monotonic()
+        self.pool_wake_poll_s = float(pool_wake_poll_s or 0.0)
+        self.pool_wake_hold_s = float(pool_wake_hold_s or 0.0)
+        self._wake_until = 0.0
+        self._next_arrival_check = 0.0
+        # queue -> length at the last check; reset to empty when demand
+        # ends (a scale to zero implies empty queues, stranded keys aside),
+        # so a key landing before the first check still counts as arrived
+        self._queued = {}
+        self.arrival_wakes = 0
         self.resources = collections.OrderedDict()
         self.standbys = collections.OrderedDict()   # slot index -> _Process
         self.lock = threading.RLock()
@@ -712,10 +733,14 @@ class GpuManager(object):
         if assign is not None:
             args += ['--assign', json.dumps(assign)]
         elif slot is not None:
-            args += ['--pin', json.dumps({
-                'gpu': slot.visible_id, 'slot': slot.index, 'cpus': slot.cpus,
-                'preinit': self.pool_mode,
-                'node_fence': self.node is not None})]
+            pin = {'gpu': slot.visible_id, 'slot': slot.index,
+                   'cpus': slot.cpus, 'preinit': self.pool_mode,
+                   'node_fence': self.node is not None}
+            if role == 'standby' and time.monotonic() < self._wake_until:
+                # woken by an arrival: the scale-up for it is due within a
+                # tick, so build the engine now rather than at the assignment
+                pin['prebuild'] = self._prebuild_spec(template)
+            args += ['--pin', json.dumps(pin)]
         env = self._environment(template)
         popen = None
         via = 'exec'
@@ -780,13 +805,25 @@ class GpuManager(object):
                      for r in self.resources.values())
         if demand:
             self._last_demand = now
+            self._queued = {}
             if self.pool_parked:
                 self.pool_parked = False
                 self.events.emit('pool_resumed')
                 logger.info('Demand returned: refilling the warm pool.')
             return False
+        if self.pool_idle_release_s > 0 and self._arrived(now):
+            self._last_demand = now
+            self._wake_until = now + self.pool_wake_hold_s
+            if self.pool_parked:
+                self.pool_parked = False
+                self.arrival_wakes += 1
+                self.events.emit('pool_resumed', reason='arrival')
+                logger.info('Keys arrived: refilling the warm pool ahead of '
+                            'the scale-up tick.')
+            return False
         if (self.pool_idle_release_s <= 0 or self.pool_parked or
-                now - self._last_demand < self.pool_idle_release_s):
+                now - self._last_demand < self.pool_idle_release_s or
+                now < self._wake_until):
             return False
         self.pool_parked = True
         released = 0
@@ -801,6 +838,43 @@ class GpuManager(object):
         logger.info('No demand for %.0f s: released %d standby process(es).',
                     now - self._last_demand, released)
         return True
+
+    def _prebuild_spec(self, template):
+        """What an arrival-woken standby builds its engine for: the shape
+        (kind, keys per pod) of the resource its template serves."""
+        for resource in self.resources.values():
+            if resource.template.module == template.module:
+                return {'kind': resource.kind,
+                        'keys_per_pod': resource.template.keys_per_pod}
+        return {'kind': 'deployment', 'keys_per_pod': template.keys_per_pod}
+
+    def _arrived(self, now):
+        """True when a managed queue grew since the last check (read every
+        ``pool_wake_poll_s`` while no worker is declared or live).  Growth,
+        not length: keys a policy strands below KEYS_PER_POD do not hold
+        the pool, new ones wake it.  One pipelined LLEN per queue."""
+        if self.pool_wake_poll_s <= 0 or self.redis is None or \
+                now < self._next_arrival_check:
+            return False
+        self._next_arrival_check = now + self.pool_wake_poll_s
+        queues = sorted(set(q for r in self.resources.values()
+                            for q in r.template.queues))
+        if not queues:
+            return False
+        try:
+            pipe = self.redis.pipeline(transaction=False)
+            for queue in queues:
+                pipe.llen(queue)
+            lengths = dict(zip(queues, (int(n or 0) for n in pipe.execute())))
+        except Exception as err:  # pylint: disable=broad-except
+            logger.debug('arrival check failed: %s', err)
+            return False
+        before, self._queued = self._queued, lengths
+        grown = [q for q in queues if lengths[q] > before.get(q, 0)]
+        if grown:
+            self.events.emit('arrival', queues=grown,
+                             parked=self.pool_parked)
+        return bool(grown)
 
     def _take_standby(self, template, slot):
         """The standby pinned to ``slot`` (booted or still booting: it
@@ -862,6 +936,12 @@ class GpuManager(object):
             return
         if message.get('ev') == 'device':
             self._check_device(proc, message.get('pci'))
+            return
+        if message.get('ev') == 'prebuilt':
+            self.events.emit('standby_prebuilt', pid=proc.pid, slot=proc.slot,
+                             ms=message.get('ms'),
+                             hbm_bytes=message.get('hbm_bytes'),
+                             error=message.get('error'))
             return
         if message.get('ev') == 'standby':
             proc.booted = True

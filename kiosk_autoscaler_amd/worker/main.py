@@ -206,6 +206,32 @@ def _cached_engine(backend, cfg, stage):
     return engine
 
 
+def _prebuild_engine(backend, pin, channel):
+    """A standby the manager woke for a key's arrival builds its engine
+    (weights, arena, forward graph, pass time) before the assignment: the
+    scale-up then finds it cached, as a recycled standby's, and READY is the
+    warm-start kernel alone.  Best effort: a failure leaves the build to
+    the assignment."""
+    from .runtime import WorkerConfig
+    spec = pin.get('prebuild') or {}
+    t0 = time.monotonic_ns()
+    try:
+        cfg = WorkerConfig(os.environ, {
+            'worker_id': 'standby', 'kind': spec.get('kind', 'deployment'),
+            'slot': pin.get('slot', 0), 'gpu': pin.get('gpu', ''),
+            'template': {'keys_per_pod': spec.get('keys_per_pod')}})
+        engine = _cached_engine(backend, cfg, None)
+        if os.environ.get('WARM_START', '1').lower() not in (
+                '0', 'false', 'no', 'off'):
+            engine.warmstart()
+        channel.emit('prebuilt', ms=(time.monotonic_ns() - t0) / 1e6,
+                     hbm_bytes=_cached_engine_bytes())
+    except Exception as err:  # pylint: disable=broad-except
+        _drop_cached_engines()
+        channel.emit('prebuilt', ms=(time.monotonic_ns() - t0) / 1e6,
+                     error='%s: %s' % (type(err).__name__, err))
+
+
 def _release_engine(engine):
     """End of an assignment: a cached engine stays resident (freed when the
     process exits, a different model needs the HBM, or the standby has
@@ -365,6 +391,8 @@ def main(argv=None):
     node_agent = None
     if node:
         node_agent = _start_node_agent(channel, backend, early.get('slot', 0))
+    if pin is not None and pin.get('prebuild') and not args.assign:
+        _prebuild_engine(backend, pin, channel)
     assignment = parse_assignment(args.assign) if args.assign else None
     recycles = 0
     max_recycles = int(os.environ.get('WORKER_MAX_RECYCLES', 64))

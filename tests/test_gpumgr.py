@@ -434,7 +434,8 @@ def test_pool_parks_after_idle_and_refills_on_demand(resp_server):
     env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
            'QUEUES': 'predict', 'RESOURCE_NAME': 'park', 'MAX_PODS': '1',
            'WORKER_BACKEND': 'cpu', 'WARM_POOL': '1', 'FENCE': 'none',
-           'REDIS_INTERVAL': '0', 'POOL_IDLE_RELEASE_S': '0.3'}
+           'REDIS_INTERVAL': '0', 'POOL_IDLE_RELEASE_S': '0.3',
+           'POOL_WAKE_POLL_S': '0'}     # wake at the scale-up only
     s = Settings(Config(environ=env, use_files=False))
     assert s.POOL_IDLE_RELEASE_S == 0.3
     client = StrictRedis(host=resp_server.host, port=resp_server.port,
@@ -475,6 +476,82 @@ def test_pool_parks_after_idle_and_refills_on_demand(resp_server):
         until(lambda: len(manager.standbys) == 1)
         # ... and parked again after the next idle period
         until(lambda: kinds().count('pool_parked') == 2)
+    finally:
+        manager.stop()
+
+
+def test_parked_pool_wakes_on_arrival_before_the_tick(resp_server):
+    """``POOL_WAKE_POLL_S``: a key landing on a parked node refills the
+    pool at once -- no scale decision is taken (declared stays 0 until the
+    tick) -- so the scale-up finds a booted standby; keys a policy strands
+    do not hold the pool: it parks again, and only new arrivals wake it."""
+    import time
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict,track', 'RESOURCE_NAME': 'wake',
+           'MAX_PODS': '1', 'WORKER_BACKEND': 'cpu', 'WARM_POOL': '1',
+           'FENCE': 'none', 'REDIS_INTERVAL': '0',
+           'POOL_IDLE_RELEASE_S': '0.3', 'POOL_WAKE_POLL_S': '0.02',
+           # an arrival holds the pool 1.5 x INTERVAL + 1 s = 1.3 s
+           'INTERVAL': '0.2'}
+    s = Settings(Config(environ=env, use_files=False))
+    assert s.POOL_WAKE_POLL_S == 0.02
+    assert gpumgr.build_manager(s).pool_wake_hold_s == 1.3
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    events = EventLog(source='test')
+    events.keep = True
+    manager = gpumgr.build_manager(s, redis_client=client,
+                                   events=events).start()
+
+    def until(predicate, timeout=30):
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            if predicate():
+                return
+            time.sleep(0.02)
+        raise AssertionError('timed out')
+
+    def count(kind):
+        return sum(1 for e in events.records if e['ev'] == kind)
+
+    def booted():
+        return bool(manager.standbys) and all(
+            p.booted for p in manager.standbys.values())
+    try:
+        until(lambda: count('pool_parked') == 1 and not manager.standbys)
+        # a key on the second queue: the pool refills with nothing declared
+        client.hset('track:k', mapping={'status': 'new'})
+        client.lpush('track', 'track:k')
+        until(booted)
+        woke = [e for e in events.records if e['ev'] == 'pool_resumed']
+        assert woke and woke[-1]['reason'] == 'arrival'
+        # the woken standby built its engine before any assignment
+        built = [e for e in events.records if e['ev'] == 'standby_prebuilt']
+        assert built and built[-1]['error'] is None
+        assert manager.arrival_wakes == 1
+        view = manager.list_namespaced_deployment('default').items[0]
+        assert view.spec.replicas == 0            # the decision is the tick's
+        # the tick's scale-up takes the booted standby
+        manager.patch_namespaced_deployment('wake', 'default',
+                                            {'spec': {'replicas': 1}})
+        until(lambda: client.hget('track:k', 'status') == 'done')
+        spawned = [e for e in events.records if e['ev'] == 'worker_assigned']
+        assert spawned[-1]['from_pool'] is True
+        manager.patch_namespaced_deployment('wake', 'default',
+                                            {'spec': {'replicas': 0}})
+        until(lambda: count('pool_parked') == 2 and not manager.standbys)
+        # a stranded key (never scaled for): one wake, then it parks again
+        # and stays parked while the queue does not grow
+        client.lpush('predict', 'predict:stranded')
+        until(lambda: manager.arrival_wakes == 2)
+        until(lambda: count('pool_parked') == 3 and not manager.standbys)
+        time.sleep(0.5)
+        assert manager.arrival_wakes == 2 and manager.pool_parked
+        client.lpush('predict', 'predict:new')
+        until(lambda: manager.arrival_wakes == 3)
     finally:
         manager.stop()
 

@@ -7,6 +7,9 @@
 #        cold spawn
 #   bash tools/gpu_round3_tiers.sh D -> deep idle, built-in and torch engine
 #        (node generation deferred until the woken worker is READY)
+#   bash tools/gpu_round3_tiers.sh E -> deep idle woken by arrivals
+#        (POOL_WAKE_POLL_S): release after 3 s and after 1 s, built-in and
+#        torch engine
 set -o pipefail
 OUT=${OUT:-gpurun_out/r3_tiers}
 mkdir -p $OUT
@@ -38,4 +41,9 @@ elif [ "$1" = "D" ]; then
   POOL_IDLE_RELEASE_S=3 run deep_idle_v2 260 --gpus 1 --steps 10 --warmup 1 --budget-s 230 --cold-cycles 0 && \
   WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine POOL_IDLE_RELEASE_S=3 \
     run torch_deep_idle_v2 260 --gpus 1 --steps 6 --warmup 1 --budget-s 230 --cold-cycles 0
+elif [ "$1" = "E" ]; then
+  POOL_IDLE_RELEASE_S=3 run deep_idle_wake_3s 260 --gpus 1 --steps 10 --warmup 1 --budget-s 230 --cold-cycles 0 && \
+  POOL_IDLE_RELEASE_S=1 run deep_idle_wake_1s 260 --gpus 1 --steps 10 --warmup 1 --budget-s 230 --cold-cycles 0 && \
+  WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine POOL_IDLE_RELEASE_S=1 \
+    run torch_deep_idle_wake_1s 260 --gpus 1 --steps 6 --warmup 1 --budget-s 230 --cold-cycles 0
 fi
