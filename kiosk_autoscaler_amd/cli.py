@@ -119,10 +119,17 @@ def run_loop(scaler, settings, max_ticks=None, sleep=time.sleep,
             # at most IDLE_INTERVAL instead of INTERVAL (not the reference's
             # semantics; reported separately in the benchmarks)
             interval = idle
+        # an embedded manager wakes a parked pool just ahead of the tick
+        # that will scale for a new key (POOL_WAKE_LEAD_S)
+        note = getattr(scaler.actuator, 'note_next_tick', None)
         if settings.FIXED_RATE:
             next_tick += interval
+            if callable(note):
+                note(time.monotonic() + max(0.0, next_tick - clock()))
             sleep(max(0.0, next_tick - clock()))
         else:
+            if callable(note):
+                note(time.monotonic() + interval)
             sleep(interval)
     return ticks
 

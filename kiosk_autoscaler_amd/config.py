@@ -159,6 +159,10 @@ EXTRA_DEFAULTS = (
     # runs; a new key refills a parked pool before the scale-up tick (the
     # decision still waits for the tick; 0 = wake at the scale-up only)
     ('POOL_WAKE_POLL_S', float, 0.05),
+    # ... and wakes this long before the tick that will scale for the key
+    # (embedded manager: the loop tells it when that is), so the woken
+    # standbys hold the GPU for the lead, not the whole tick phase
+    ('POOL_WAKE_LEAD_S', float, 0.75),
     # s a recycled standby keeps its engine (weights, arena, graphs; ~1.2
     # GiB of the idle GPU's 2.6) without an assignment; then it frees it and
     # keeps context, queue and node communicator (0 = keep forever)

@@ -131,7 +131,8 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
                          pool_wake_poll_s=settings.POOL_WAKE_POLL_S,
                          # the tick that scales for an arrival comes within
                          # INTERVAL (+ the tick itself) of it
-                         pool_wake_hold_s=1.5 * float(settings.INTERVAL) + 1.0)
+                         pool_wake_hold_s=1.5 * float(settings.INTERVAL) + 1.0,
+                         pool_wake_lead_s=settings.POOL_WAKE_LEAD_S)
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

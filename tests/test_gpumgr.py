@@ -556,6 +556,64 @@ def test_parked_pool_wakes_on_arrival_before_the_tick(resp_server):
         manager.stop()
 
 
+def test_arrival_wake_waits_for_the_lead_before_the_tick(resp_server):
+    """``POOL_WAKE_LEAD_S``: told when the next tick is, the manager wakes
+    a parked pool that long before it, not at the arrival; without a known
+    tick (or inside the lead) it wakes at once."""
+    import time
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict', 'RESOURCE_NAME': 'lead', 'MAX_PODS': '1',
+           'WORKER_BACKEND': 'cpu', 'WARM_POOL': '1', 'FENCE': 'none',
+           'REDIS_INTERVAL': '0', 'POOL_IDLE_RELEASE_S': '0.2',
+           'POOL_WAKE_POLL_S': '0.02', 'POOL_WAKE_LEAD_S': '0.4',
+           'INTERVAL': '0.2'}
+    s = Settings(Config(environ=env, use_files=False))
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    events = EventLog(source='test')
+    events.keep = True
+    manager = gpumgr.build_manager(s, redis_client=client,
+                                   events=events).start()
+    assert manager.pool_wake_lead_s == 0.4
+
+    def until(predicate, timeout=30):
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            if predicate():
+                return
+            time.sleep(0.01)
+        raise AssertionError('timed out')
+
+    def resumed():
+        return [e['t'] for e in events.records if e['ev'] == 'pool_resumed']
+    try:
+        until(lambda: manager.pool_parked and not manager.standbys)
+        tick = time.monotonic() + 1.5
+        manager.note_next_tick(tick)
+        t_push = time.monotonic()
+        client.lpush('predict', 'predict:a')
+        until(lambda: manager.arrival_wakes == 1)
+        woke = time.monotonic()
+        assert woke >= tick - 0.4 - 0.05, (woke - t_push)
+        assert woke < tick                # ahead of the tick
+        until(lambda: manager.standbys)
+        # the tick passes without a scale-up (the key is taken by hand): the
+        # pool parks again after the hold, then a key whose tick is already
+        # inside the lead wakes it at once
+        client.delete('predict')
+        until(lambda: manager.pool_parked and not manager.standbys)
+        manager.note_next_tick(time.monotonic() + 0.2)
+        t_push = time.monotonic()
+        client.lpush('predict', 'predict:b')
+        until(lambda: manager.arrival_wakes == 2)
+        assert time.monotonic() - t_push < 0.3
+    finally:
+        manager.stop()
+
+
 def test_pci_mapping_verified_and_remapped(monkeypatch):
     """a process reports the PCI address HIP sees for its pinned
     ordinal; a match verifies the slot, a mismatch remaps the slot to the

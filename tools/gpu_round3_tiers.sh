@@ -10,6 +10,9 @@
 #   bash tools/gpu_round3_tiers.sh E -> deep idle woken by arrivals
 #        (POOL_WAKE_POLL_S): release after 3 s and after 1 s, built-in and
 #        torch engine
+#   bash tools/gpu_round3_tiers.sh F -> deep idle woken POOL_WAKE_LEAD_S
+#        before the tick, released 0.5 s after the scale-down: the driver's
+#        command (20 + 5 steps), then the torch plug-in
 set -o pipefail
 OUT=${OUT:-gpurun_out/r3_tiers}
 mkdir -p $OUT
@@ -46,4 +49,8 @@ elif [ "$1" = "E" ]; then
   POOL_IDLE_RELEASE_S=1 run deep_idle_wake_1s 260 --gpus 1 --steps 10 --warmup 1 --budget-s 230 --cold-cycles 0 && \
   WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine POOL_IDLE_RELEASE_S=1 \
     run torch_deep_idle_wake_1s 260 --gpus 1 --steps 6 --warmup 1 --budget-s 230 --cold-cycles 0
+elif [ "$1" = "F" ]; then
+  POOL_IDLE_RELEASE_S=0.5 run deep_idle_lead 330 --gpus 1 --steps 20 --warmup 5 && \
+  WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine POOL_IDLE_RELEASE_S=0.5 \
+    run torch_deep_idle_lead 260 --gpus 1 --steps 8 --warmup 1 --budget-s 230 --cold-cycles 0
 fi
