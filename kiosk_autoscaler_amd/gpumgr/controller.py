@@ -160,6 +160,7 @@ class _Process(object):
         self.recycles = 0
         self.node_ok = False    # runs a node-communicator agent
         self.hbm_free = None    # free HBM bytes the standby measured
+        self.woken = False      # spawned by an arrival wake (prebuilds)
 
     @property
     def pid(self):
@@ -333,6 +334,9 @@ class GpuManager(object):
         self._wake_until = 0.0
         self.pool_wake_lead_s = float(pool_wake_lead_s or 0.0)
         self._next_tick = None    # monotonic instant of the next tick
+        # spawn -> booted+prebuilt of recent arrival-woken standbys: the
+        # lead adapts to it (1.5 x the slowest + 50 ms, capped by the knob)
+        self._wake_boots = collections.deque(maxlen=8)
         self._wake_at = None      # a deferred arrival wake
         self._next_arrival_check = 0.0
         # queue -> length at the last check; reset to empty when demand
@@ -740,15 +744,17 @@ class GpuManager(object):
         ev_r, ev_w = os.pipe()
         args = ['--cmd-fd', str(cmd_r), '--ev-fd', str(ev_w),
                 '--backend', template.backend]
+        # a standby spawned by an arrival wake: the scale-up for the key is
+        # due within a tick, so it builds the engine now, not at the assign
+        woken = (assign is None and slot is not None and role == 'standby'
+                 and time.monotonic() < self._wake_until)
         if assign is not None:
             args += ['--assign', json.dumps(assign)]
         elif slot is not None:
             pin = {'gpu': slot.visible_id, 'slot': slot.index,
                    'cpus': slot.cpus, 'preinit': self.pool_mode,
                    'node_fence': self.node is not None}
-            if role == 'standby' and time.monotonic() < self._wake_until:
-                # woken by an arrival: the scale-up for it is due within a
-                # tick, so build the engine now rather than at the assignment
+            if woken:
                 pin['prebuild'] = self._prebuild_spec(template)
             args += ['--pin', json.dumps(pin)]
         env = self._environment(template)
@@ -773,6 +779,7 @@ class GpuManager(object):
             os.close(cmd_r)
             os.close(ev_w)
         proc = _Process(popen, _Pipe(cmd_w, ev_r), role)
+        proc.woken = woken
         proc.slot = slot.index if slot is not None else None
         proc.via = via
         self.events.emit('process_spawn', role=role, pid=popen.pid,
@@ -825,10 +832,11 @@ class GpuManager(object):
             return False
         if self.pool_idle_release_s > 0 and self._arrived(now):
             wake_at = now
-            if self.pool_parked and self.pool_wake_lead_s > 0 and \
+            lead = self.wake_lead()
+            if self.pool_parked and lead > 0 and \
                     self._next_tick is not None and \
-                    self._next_tick - now > self.pool_wake_lead_s:
-                wake_at = self._next_tick - self.pool_wake_lead_s
+                    self._next_tick - now > lead:
+                wake_at = self._next_tick - lead
             if self._wake_at is None or wake_at < self._wake_at:
                 self._wake_at = wake_at
         if self._wake_at is not None and now >= self._wake_at:
@@ -864,11 +872,22 @@ class GpuManager(object):
         """The autoscaler loop's next tick instant (``time.monotonic``
         seconds): a deferred arrival wake is timed against it."""
         self._next_tick = float(t_monotonic)
-        if self._wake_at is not None and self.pool_wake_lead_s > 0:
+        lead = self.wake_lead()
+        if self._wake_at is not None and lead > 0:
             # the tick came earlier than planned for (IDLE_INTERVAL)
-            self._wake_at = min(self._wake_at,
-                                self._next_tick - self.pool_wake_lead_s)
+            self._wake_at = min(self._wake_at, self._next_tick - lead)
         self._wake()
+
+    def wake_lead(self):
+        """Seconds before the next tick an arrival wakes a parked pool:
+        ``pool_wake_lead_s`` until woken standbys have been timed, then
+        1.5 x the slowest of the last 8 spawn -> booted+prebuilt times plus
+        50 ms, never above ``pool_wake_lead_s`` (built-in worker: ~0.2 s ->
+        ~0.35 s; PyTorch plug-in: ~0.55 s -> the cap)."""
+        cap = self.pool_wake_lead_s
+        if cap <= 0 or not self._wake_boots:
+            return cap
+        return min(cap, 1.5 * max(self._wake_boots) + 0.05)
 
     def _prebuild_spec(self, template):
         """What an arrival-woken standby builds its engine for: the shape
@@ -975,6 +994,10 @@ class GpuManager(object):
                              error=message.get('error'))
             return
         if message.get('ev') == 'standby':
+            if proc.woken and not proc.booted:
+                # spawn -> booted and prebuilt: what the wake lead must cover
+                self._wake_boots.append(
+                    (time.monotonic_ns() - proc.t_spawn) / 1e9)
             proc.booted = True
             proc.hbm_free = message.get('hbm_free')
             if message.get('pci'):

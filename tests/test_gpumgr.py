@@ -610,6 +610,11 @@ def test_arrival_wake_waits_for_the_lead_before_the_tick(resp_server):
         client.lpush('predict', 'predict:b')
         until(lambda: manager.arrival_wakes == 2)
         assert time.monotonic() - t_push < 0.3
+        # the lead adapts to the woken standbys' measured boot (CPU: well
+        # under the 0.4 s cap)
+        until(lambda: len(manager._wake_boots) == 2)
+        assert manager.wake_lead() == min(
+            0.4, 1.5 * max(manager._wake_boots) + 0.05)
     finally:
         manager.stop()
 
