@@ -90,6 +90,14 @@ class PrometheusExporter(object):
                               registry=r)
         self.kpp = Gauge('kiosk_keys_per_pod_effective', 'KEYS_PER_POD '
                          'after free-HBM sizing', ['gpu'], registry=r)
+        self.pool_parks = Counter('kiosk_pool_parks', 'deep idle: standby '
+                                  'pool released', registry=r)
+        self.pool_wakes = Counter('kiosk_pool_wakes', 'parked pool refilled',
+                                  ['reason'], registry=r)
+        self.prebuild_seconds = Histogram(
+            'kiosk_standby_prebuild_seconds', 'arrival-woken standby: engine '
+            'prebuilt before the assignment', registry=r,
+            buckets=LATENCY_BUCKETS)
         if manager is not None:
             r.register(_ManagerCollector(manager))
         self.port = None
@@ -156,6 +164,12 @@ class PrometheusExporter(object):
         elif ev == 'node_comm_break':
             self.comm_breaks.labels(
                 str(bool(record.get('failed'))).lower()).inc()
+        elif ev == 'pool_parked':
+            self.pool_parks.inc()
+        elif ev == 'pool_resumed':
+            self.pool_wakes.labels(str(record.get('reason') or 'demand')).inc()
+        elif ev == 'standby_prebuilt' and not record.get('error'):
+            self.prebuild_seconds.observe(float(record.get('ms') or 0.0) / 1e3)
         elif ev == 'hbm_sizing':
             gpu = str(record.get('gpu'))
             self.hbm_free.labels(gpu).set(record.get('hbm_free') or 0)

@@ -40,6 +40,10 @@ def test_exporter_counts_events_and_serves_http():
     events.emit('process_spawn', pid=1, via='zygote')
     events.emit('process_spawn', pid=2)
     events.emit('hbm_sizing', gpu=0, hbm_free=2.8e11, keys_per_pod=4)
+    events.emit('pool_parked', standbys=1, idle_s=0.5)
+    events.emit('pool_resumed', reason='arrival')
+    events.emit('pool_resumed')
+    events.emit('standby_prebuilt', ms=11.0, error=None)
     text = generate_latest(exporter.registry).decode()
     for line in ('kiosk_node_comm_generations_total 1.0',
                  'kiosk_node_comm_breaks_total{failed="false"} 1.0',
@@ -51,7 +55,11 @@ def test_exporter_counts_events_and_serves_http():
                  'kiosk_process_spawns_total{via="zygote"} 1.0',
                  'kiosk_process_spawns_total{via="exec"} 1.0',
                  'kiosk_hbm_free_bytes{gpu="0"} 2.8e+11',
-                 'kiosk_keys_per_pod_effective{gpu="0"} 4.0'):
+                 'kiosk_keys_per_pod_effective{gpu="0"} 4.0',
+                 'kiosk_pool_parks_total 1.0',
+                 'kiosk_pool_wakes_total{reason="arrival"} 1.0',
+                 'kiosk_pool_wakes_total{reason="demand"} 1.0',
+                 'kiosk_standby_prebuild_seconds_count 1.0'):
         assert line in text, line
     for line in ('kiosk_queue_keys{queue="q"} 4.0',
                  'kiosk_in_progress_keys{queue="q"} 1.0',
