@@ -575,7 +575,12 @@ class GpuManager(object):
 
     def _loop(self):
         while not self._stop.is_set():
-            self.poll(0.05)
+            timeout = 0.05
+            wake_at = self._wake_at
+            if wake_at is not None:
+                # a deferred arrival wake is due: do not sleep past it
+                timeout = min(timeout, max(0.001, wake_at - time.monotonic()))
+            self.poll(timeout)
 
     def stop(self, timeout=10.0):
         """Drain every worker, stop standbys, join the loop."""
@@ -846,7 +851,11 @@ class GpuManager(object):
             if self.pool_parked:
                 self.pool_parked = False
                 self.arrival_wakes += 1
-                self.events.emit('pool_resumed', reason='arrival')
+                self.events.emit('pool_resumed', reason='arrival',
+                                 lead_s=round(self.wake_lead(), 4),
+                                 tick_in_s=(round(self._next_tick - now, 4)
+                                            if self._next_tick is not None
+                                            else None))
                 logger.info('Keys arrived: refilling the warm pool ahead of '
                             'the scale-up tick.')
             return False
@@ -882,12 +891,14 @@ class GpuManager(object):
         """Seconds before the next tick an arrival wakes a parked pool:
         ``pool_wake_lead_s`` until woken standbys have been timed, then
         1.5 x the slowest of the last 8 spawn -> booted+prebuilt times plus
-        50 ms, never above ``pool_wake_lead_s`` (built-in worker: ~0.2 s ->
-        ~0.35 s; PyTorch plug-in: ~0.55 s -> the cap)."""
+        50 ms and the arrival poll, at least 0.2 s, never above
+        ``pool_wake_lead_s`` (built-in worker: ~0.1-0.2 s -> 0.25-0.4 s;
+        PyTorch plug-in: ~0.55 s -> the cap)."""
         cap = self.pool_wake_lead_s
         if cap <= 0 or not self._wake_boots:
             return cap
-        return min(cap, 1.5 * max(self._wake_boots) + 0.05)
+        return min(cap, max(0.2, 1.5 * max(self._wake_boots) + 0.05 +
+                            self.pool_wake_poll_s))
 
     def _prebuild_spec(self, template):
         """What an arrival-woken standby builds its engine for: the shape
@@ -996,6 +1007,8 @@ class GpuManager(object):
         if message.get('ev') == 'standby':
             if proc.woken and not proc.booted:
                 # spawn -> booted and prebuilt: what the wake lead must cover
+                # (once: a recycled worker reports 'standby' again later)
+                proc.woken = False
                 self._wake_boots.append(
                     (time.monotonic_ns() - proc.t_spawn) / 1e9)
             proc.booted = True
