@@ -119,6 +119,29 @@ def test_idle_interval_fast_path():
     assert sleeps == [0.25, 0.25, 5]
 
 
+def test_run_loop_tells_the_manager_the_next_tick():
+    """The embedded manager times its arrival wake against the loop's next
+    tick (POOL_WAKE_LEAD_S): after every tick the loop reports when the next
+    one starts -- now + the sleep it is about to take."""
+    import time
+    scaler = mock.Mock()
+    scaler.last_decision = 0
+    told = []
+    scaler.actuator.note_next_tick.side_effect = told.append
+    sleeps = []
+    before = time.monotonic()
+    cli.run_loop(scaler, _settings(INTERVAL=5, IDLE_INTERVAL=0.25),
+                 max_ticks=3, sleep=sleeps.append, clock=lambda: 0.0)
+    after = time.monotonic()
+    assert sleeps == [0.25, 0.25] and len(told) == 2
+    for t in told:
+        assert before + 0.25 <= t <= after + 0.25
+    # an actuator without the hook (the unix: daemon client) is left alone
+    scaler.actuator = object()
+    cli.run_loop(scaler, _settings(INTERVAL=5), max_ticks=2,
+                 sleep=lambda dt: None, clock=lambda: 0.0)
+
+
 def test_max_pods_clamped_to_gpu_slots(resp_server):
     from kiosk_autoscaler_amd.redisq import StrictRedis
     s = _settings(MAX_PODS=5, GPU_IDS='0,1', WORKER_BACKEND='cpu',
