@@ -168,6 +168,14 @@ __device__ __forceinline__ void mfma_drain() {
 #ifndef KIOSK_W4_STAGGER_SEL
 #define KIOSK_W4_STAGGER_SEL 1     // 0: odd waves lag; 1: waves 2, 3 lag
 #endif
+// Experiment (tools/gemm_ablate.hip A/B, off in the product): stage the
+// k-loop's operand pieces through VGPRs -- buffer_load_dwordx4 into
+// registers in half-step h, ds_write_b128 into the ring in half-step h + 1 --
+// instead of LDS-DMA, whose issue holds the wave ~60 cycles among MFMAs.
+#ifndef KIOSK_W4_REGSTAGE
+#define KIOSK_W4_REGSTAGE 0
+#endif
+
 // Counted waits go through the builtin (not inline asm) so hipcc's waitcnt
 // pass sees them and adds no conservative lgkmcnt(0) of its own.  gfx9
 // encoding: vmcnt[3:0] | expcnt[6:4] (7 = no wait) | lgkmcnt[11:8] |
@@ -379,6 +387,24 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)lds, 16,
                                                  voff_a[p], t * 128, 0, 0);
     };
+    // KIOSK_W4_REGSTAGE: piece p of the group in flight, in registers;
+    // written to its ring unit three groups before its first read
+    // (2: two register buffers by group parity, so a load has two
+    // half-steps to land before its write instead of one)
+    typedef __attribute__((ext_vector_type(4))) int i32x4;
+    constexpr int kBufs = KIOSK_W4_REGSTAGE == 2 ? 2 : 1;
+    i32x4 stage[kBufs * 8];
+    auto gload = [&](int g, int p, int buf) {
+      const int t = min(g >> 1, steps - 1);
+      stage[buf * 8 + p] = __builtin_amdgcn_raw_buffer_load_b128(
+          (g & 1) ? rsrc_b : rsrc_a, (g & 1) ? voff_b[p] : voff_a[p],
+          t * 128, 0);
+    };
+    const int lane16 = (threadIdx.x & 63) * 16;
+    auto swrite = [&](int g, int p, int buf) {
+      char* lds = smem + (g % 5) * kUnit + (wave * 8 + p) * 1024 + lane16;
+      *reinterpret_cast<i32x4*>(lds) = stage[buf * 8 + p];
+    };
     // fragment r of half h: r < TN -> B tile r, else A tile r - TN
     const int fr = lane & 15;
     const int lane_a = (wm * 128 + fr) * 128, lane_b = (wn * 128 + fr) * 128;
@@ -412,7 +438,10 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
       constexpr bool kOdd = decltype(odd)::value;
       const int h = 2 * t + kOdd;
       __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(kOdd ? 8 : 16));
+      // regstage: the previous half-step's ds_writes (lgkmcnt 0) must land;
+      // the loads in flight are waited for by each write (compiler vmcnt)
+      __builtin_amdgcn_s_waitcnt(
+          waitcnt_vm(KIOSK_W4_REGSTAGE ? 63 : (kOdd ? 8 : 16)));
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       // half h + 1: step t (h even, second half) or t + 1 (h odd, first)
@@ -436,8 +465,19 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
           // MFMAs (~256 cycles) to return before the next half-step's
           // lgkmcnt(0) + barrier
           if constexpr (!(KIOSK_GEMM_ABLATE & 1))
-            if (u >= kOff && (u - kOff) % 6 == 0 && (u - kOff) < 48)
-              dma(h + 4, (u - kOff) / 6);
+            if (u >= kOff && (u - kOff) % 6 == 0 && (u - kOff) < 48) {
+              if constexpr (KIOSK_W4_REGSTAGE == 1) {
+                swrite(h + 3, (u - kOff) / 6, 0);
+                gload(h + 4, (u - kOff) / 6, 0);
+              } else if constexpr (KIOSK_W4_REGSTAGE == 2) {
+                // group h + 3 leaves buffer (h + 3) % 2, group h + 5 refills it
+                constexpr int kBuf = kOdd ? 0 : 1;
+                swrite(h + 3, (u - kOff) / 6, kBuf);
+                gload(h + 5, (u - kOff) / 6, kBuf);
+              } else {
+                dma(h + 4, (u - kOff) / 6);
+              }
+            }
           if constexpr (!(KIOSK_GEMM_ABLATE & 2))
             if (u % 3 == 1 && u < 48) read(HH(), tn, u / 3, wb_next, xa_next);
         }
@@ -445,9 +485,18 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
     };
     if (!prefetched) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
+      for (int g = 0; g < (KIOSK_W4_REGSTAGE ? 3 : 4); ++g)
 #pragma unroll
         for (int p = 0; p < 8; ++p) dma(g, p);
+    }
+    if constexpr (KIOSK_W4_REGSTAGE) {
+      // group 3 (and 4) go through the registers (written in half-step 0, 1)
+#pragma unroll
+      for (int p = 0; p < 8; ++p) gload(3, p, kBufs == 2 ? 1 : 0);
+      if constexpr (kBufs == 2) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) gload(4, p, 0);
+      }
     }
     __builtin_amdgcn_s_waitcnt(waitcnt_vm(16));
     __builtin_amdgcn_s_barrier();
