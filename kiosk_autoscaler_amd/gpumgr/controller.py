@@ -818,9 +818,10 @@ class GpuManager(object):
         """Deep idle (``POOL_IDLE_RELEASE_S``): with no declared or live
         worker for that long, retire every standby -- the node then holds
         no GPU, like the reference at zero replicas -- and keep the pool
-        empty until demand returns; the first scale-up after it is a cold
-        spawn and the pool refills behind it.  True if standbys were
-        retired."""
+        empty until demand returns: a key's arrival (``pool_wake_poll_s``,
+        woken ``wake_lead()`` before the next tick) or, without it, the
+        scale-up itself, which is then a cold spawn with the pool refilling
+        behind it.  True if standbys were retired."""
         now = time.monotonic()
         demand = any(r.declared > 0 or any(w.state != EXITED
                                            for w in r.workers.values())
@@ -879,12 +880,14 @@ class GpuManager(object):
 
     def note_next_tick(self, t_monotonic):
         """The autoscaler loop's next tick instant (``time.monotonic``
-        seconds): a deferred arrival wake is timed against it."""
-        self._next_tick = float(t_monotonic)
-        lead = self.wake_lead()
-        if self._wake_at is not None and lead > 0:
-            # the tick came earlier than planned for (IDLE_INTERVAL)
-            self._wake_at = min(self._wake_at, self._next_tick - lead)
+        seconds): a deferred arrival wake is timed against it.  Called from
+        the loop's thread: under the manager lock."""
+        with self.lock:
+            self._next_tick = float(t_monotonic)
+            lead = self.wake_lead()
+            if self._wake_at is not None and lead > 0:
+                # the tick came earlier than planned for (IDLE_INTERVAL)
+                self._wake_at = min(self._wake_at, self._next_tick - lead)
         self._wake()
 
     def wake_lead(self):
