@@ -13,6 +13,8 @@
 #   bash tools/gpu_round3_tiers.sh F -> deep idle woken POOL_WAKE_LEAD_S
 #        before the tick, released 0.5 s after the scale-down: the driver's
 #        command (20 + 5 steps), then the torch plug-in
+#   bash tools/gpu_round3_tiers.sh G -> config-4 shape (60 s Poisson bursts,
+#        60 s off), resident pool vs arrival-woken deep idle
 set -o pipefail
 OUT=${OUT:-gpurun_out/r3_tiers}
 mkdir -p $OUT
@@ -53,4 +55,7 @@ elif [ "$1" = "F" ]; then
   POOL_IDLE_RELEASE_S=0.5 run deep_idle_lead 330 --gpus 1 --steps 20 --warmup 5 && \
   WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine POOL_IDLE_RELEASE_S=0.5 \
     run torch_deep_idle_lead 260 --gpus 1 --steps 8 --warmup 1 --budget-s 230 --cold-cycles 0
+elif [ "$1" = "G" ]; then
+  run config4_resident 420 --gpus 1 --steps 2 --warmup 0 --on 60 --off 60 --budget-s 400 --cold-cycles 0 && \
+  POOL_IDLE_RELEASE_S=0.5 run config4_deep_idle_wake 420 --gpus 1 --steps 2 --warmup 0 --on 60 --off 60 --budget-s 400 --cold-cycles 0
 fi
