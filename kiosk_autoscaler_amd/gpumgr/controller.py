@@ -540,6 +540,12 @@ class GpuManager(object):
                              for index, p in self.standbys.items()],
                 'node_comm': (self.node.summary() if self.node is not None
                               else None),
+                # deep idle: parked pool, arrival wakes, current wake lead
+                'pool': {'parked': self.pool_parked,
+                         'arrival_wakes': self.arrival_wakes,
+                         'wake_lead_s': (self.wake_lead()
+                                         if self.pool_idle_release_s > 0
+                                         else None)},
                 'resources': [dict(r.view().to_dict(), workers=[
                     w.summary() for w in r.workers.values()])
                     for r in self.resources.values()],

@@ -206,6 +206,15 @@ class _ManagerCollector(object):
         yield standbys
         yield GaugeMetricFamily('kiosk_gpu_slots', 'GPU slots managed',
                                 value=len(status.get('slots', [])))
+        pool = status.get('pool') or {}
+        yield GaugeMetricFamily('kiosk_pool_parked', 'deep idle: the standby '
+                                'pool is released (1) or resident (0)',
+                                value=1 if pool.get('parked') else 0)
+        if pool.get('wake_lead_s') is not None:
+            yield GaugeMetricFamily('kiosk_pool_wake_lead_seconds', 'how '
+                                    'long before the next tick an arrival '
+                                    'wakes the parked pool',
+                                    value=pool['wake_lead_s'])
         replicas = GaugeMetricFamily(
             'kiosk_replicas', 'per resource: READY workers vs the READY '
             'workers of the last fenced membership (available)',

@@ -71,6 +71,7 @@ def test_exporter_counts_events_and_serves_http():
                  'kiosk_requeued_items_total 2.0',
                  'kiosk_fence_epochs_total{transport="rccl"} 1.0',
                  'kiosk_gpu_slots 3.0',
+                 'kiosk_pool_parked 0.0',
                  'kiosk_workers{resource="w",state="ready"} 0.0',
                  'kiosk_replicas{kind="ready",resource="w"} 0.0',
                  'kiosk_replicas{kind="available",resource="w"} 0.0'):
