@@ -886,10 +886,17 @@ class GpuManager(object):
 
     def note_next_tick(self, t_monotonic):
         """The autoscaler loop's next tick instant (``time.monotonic``
-        seconds): a deferred arrival wake is timed against it.  Called from
-        the loop's thread: under the manager lock."""
+        seconds, system-wide, so a ``unix:`` daemon's clients report it
+        too): a deferred arrival wake is timed against it.  With several
+        autoscalers on one manager the earliest upcoming tick wins (a
+        report replaces a tick that is due or past).  Called from the
+        loop's thread: under the manager lock."""
+        t_monotonic = float(t_monotonic)
         with self.lock:
-            self._next_tick = float(t_monotonic)
+            current = self._next_tick
+            if current is None or current <= time.monotonic() + 0.05 or \
+                    t_monotonic < current:
+                self._next_tick = t_monotonic
             lead = self.wake_lead()
             if self._wake_at is not None and lead > 0:
                 # the tick came earlier than planned for (IDLE_INTERVAL)

@@ -10,7 +10,8 @@ a restarted reference autoscaler finds its Deployment still running.
 Requests: ``{"op": "list", "kind": ..., "namespace": ...}``,
 ``{"op": "patch", "kind", "name", "namespace", "body"}``,
 ``{"op": "register", "kind", "namespace", "name", "template"}``,
-``{"op": "status"}``.  Replies: ``{"ok": true, ...}`` or
+``{"op": "status"}``, ``{"op": "tick", "t": <monotonic s>}`` (the
+client's next tick, for the arrival wake).  Replies: ``{"ok": true, ...}`` or
 ``{"ok": false, "status": int, "reason": str}``.
 """
 import argparse
@@ -58,6 +59,9 @@ def handle_request(manager, request):
             return {'ok': True, 'item': view.to_dict()}
         if op == 'status':
             return {'ok': True, 'status': manager.status()}
+        if op == 'tick':
+            manager.note_next_tick(float(request['t']))
+            return {'ok': True}
         return {'ok': False, 'status': 400, 'reason': 'unknown op %r' % op}
     except ActuatorError as err:
         return {'ok': False, 'status': err.status, 'reason': err.reason}
@@ -198,6 +202,15 @@ class GpuManagerClient(object):
 
     def patch_namespaced_job(self, name, namespace, body):
         return self._patch('job', name, namespace, body)
+
+    def note_next_tick(self, t_monotonic):
+        """Tell the daemon when this autoscaler ticks next (arrival wake,
+        ``POOL_WAKE_LEAD_S``).  Best effort: an unreachable daemon must not
+        end the reconcile loop -- the next list/patch reports that."""
+        try:
+            self._call({'op': 'tick', 't': float(t_monotonic)})
+        except ActuatorError:
+            pass
 
     def register(self, kind, namespace, name, template):
         reply = self._call({'op': 'register', 'kind': kind,

@@ -120,11 +120,22 @@ def test_daemon_transport(tmp_path):
             assert daemon.main(['--status', '--socket', path]) == 0
         status = json.loads(out.getvalue())
         assert status['resources'][0]['metadata']['name'] == 'w'
+        # the client's next tick reaches the daemon's manager (arrival
+        # wake); with two clients the earliest upcoming tick wins
+        import time
+        now = time.monotonic()
+        client.note_next_tick(now + 5.0)
+        assert manager._next_tick == now + 5.0
+        gpumgr.GpuManagerClient(path).note_next_tick(now + 3.0)
+        client.note_next_tick(now + 4.0)
+        assert manager._next_tick == now + 3.0
     finally:
         server.stop()
     with pytest.raises(ActuatorError) as info:
         gpumgr.GpuManagerClient(path, timeout=1).list_namespaced_job('ns')
     assert info.value.status == 503
+    # an unreachable daemon never ends the loop through the tick report
+    gpumgr.GpuManagerClient(path, timeout=1).note_next_tick(0.0)
 
 
 def test_requeue_exact_worker_keys():
