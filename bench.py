@@ -752,6 +752,11 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         'idle_node_hbm_pct_of_gpu': _r((hbm or {}).get('idle_pct_of_gpu'),
                                        3),
         'serving_hbm_mib_max': _r((hbm or {}).get('serving_mib_max'), 1),
+        # idle HBM at the end of the run minus at its start (leak check)
+        'idle_node_hbm_drift_mib': _r(
+            (hbm or {}).get('idle_last_mib') - (hbm or {}).get('idle_first_mib')
+            if (hbm or {}).get('idle_last_mib') is not None and
+            (hbm or {}).get('idle_first_mib') is not None else None, 1),
         'cold_starts': summary['cold_starts'],
         'first_key_latency_mean_s': _r(summary['first_key_latency_mean_s']),
         'latency_p50_s': _r(summary['latency_p50_s']),

@@ -233,14 +233,20 @@ def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
     if pool_boot and any(pool_boot.get(b, 0.0) < v for b, v in base.items()):
         base = {}      # the "baseline" held memory the run later did not
     idle, busy, idle_released = [], [], []
+    idle_timed = []     # (t, MiB): leak check over a long run
     for bdf, samples in device.items():
         zero = base.get(bdf, 0.0)
         for t, used in samples:
             if t_lo <= t <= t_hi:
                 on = serving(t)
                 (busy if on else idle).append(used - zero)
+                if not on:
+                    idle_timed.append((t, used - zero))
                 if not on and releases and released(t):
                     idle_released.append(used - zero)
+    idle_timed.sort()
+    first = [v for _, v in idle_timed[:10]]
+    last = [v for _, v in idle_timed[-10:]]
     totals = [v for v in ((vram or {}).get('total_mib') or {}).values() if v]
     total = max(totals) if totals else None
     boot = None
@@ -256,6 +262,9 @@ def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
                             if idle_mib is not None and total else None),
         'hbm_total_mib': total,
         'idle_released_mib_median': _pct(idle_released, 0.5),
+        # median of the first / last 10 idle samples (HBM drift of the run)
+        'idle_first_mib': _pct(first, 0.5),
+        'idle_last_mib': _pct(last, 0.5),
         'samples': {'idle': len(idle), 'serving': len(busy),
                     'idle_released': len(idle_released)},
         'over_baseline': bool(base),
