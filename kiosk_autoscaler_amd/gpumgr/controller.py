@@ -161,6 +161,7 @@ class _Process(object):
         self.node_ok = False    # runs a node-communicator agent
         self.hbm_free = None    # free HBM bytes the standby measured
         self.woken = False      # spawned by an arrival wake (prebuilds)
+        self.engine_cached = False  # standby holds a built engine
 
     @property
     def pid(self):
@@ -842,6 +843,19 @@ class GpuManager(object):
                 self.events.emit('pool_resumed')
                 logger.info('Demand returned: refilling the warm pool.')
             return False
+        released = [p for p in self.standbys.values()
+                    if p.booted and not p.engine_cached and
+                    self.pool_mode == 'device']
+        if not self.pool_idle_release_s > 0 and released and \
+                self._arrived(now):
+            # ENGINE_IDLE_RELEASE_S freed these standbys' engines: a key's
+            # arrival has them rebuild it before the scale-up tick
+            for proc in released:
+                proc.pipe.send({'cmd': 'prebuild',
+                                'spec': self._prebuild_spec(
+                                    self.pool_template)})
+                proc.engine_cached = True     # (until told otherwise)
+            self.events.emit('engine_rebuild', standbys=len(released))
         if self.pool_idle_release_s > 0 and self._arrived(now):
             wake_at = now
             lead = self.wake_lead()
@@ -1006,6 +1020,7 @@ class GpuManager(object):
             self.node.on_message(proc, message)
             return
         if message.get('ev') == 'engine_released':
+            proc.engine_cached = False
             proc.hbm_free = message.get('hbm_free')
             self.events.emit('engine_released', pid=proc.pid, slot=proc.slot,
                              released_bytes=message.get('released_bytes'),
@@ -1015,12 +1030,14 @@ class GpuManager(object):
             self._check_device(proc, message.get('pci'))
             return
         if message.get('ev') == 'prebuilt':
+            proc.engine_cached = not message.get('error')
             self.events.emit('standby_prebuilt', pid=proc.pid, slot=proc.slot,
                              ms=message.get('ms'),
                              hbm_bytes=message.get('hbm_bytes'),
                              error=message.get('error'))
             return
         if message.get('ev') == 'standby':
+            proc.engine_cached = bool(message.get('engine_cached'))
             if proc.woken and not proc.booted:
                 # spawn -> booted and prebuilt: what the wake lead must cover
                 # (once: a recycled worker reports 'standby' again later)

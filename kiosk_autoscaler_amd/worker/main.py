@@ -538,6 +538,13 @@ def _wait_for_assignment(channel, pin, preload_ns, backend, preinit):
             continue
         if message is None or message.get('cmd') in ('exit', 'eof'):
             return None
+        if message.get('cmd') == 'prebuild':
+            # a key arrived while this standby's engine was released
+            # (ENGINE_IDLE_RELEASE_S): rebuild it before the assignment
+            _prebuild_engine(backend, dict(pin or {},
+                                           prebuild=message.get('spec')),
+                             channel)
+            continue
         if message.get('cmd') == 'assign':
             break
     if pin and str(message.get('gpu')) != str(pin.get('gpu')):

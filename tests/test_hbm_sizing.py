@@ -157,3 +157,35 @@ def test_engine_idle_release_frees_the_kept_engine(stack):
              .items[0].status.ready_replicas == 1, timeout=30)
     workers = manager.status()['resources'][0]['workers']
     assert workers[0]['pid'] == pid and workers[0]['from_pool']
+
+
+@pytest.mark.slow
+def test_arrival_rebuilds_a_released_engine(stack):
+    """ENGINE_IDLE_RELEASE_S + POOL_WAKE_POLL_S: once a resident standby has
+    freed its engine, a key's arrival has it rebuild the engine before the
+    scale-up tick (no decision is taken: declared stays 0), so the
+    assignment reuses it."""
+    s, client, manager, scaler, events = stack(
+        MAX_PODS='1', WARM_POOL='1',
+        extra_env={'ENGINE_IDLE_RELEASE_S': '0.3', 'MOCK_WORK_MS': '10'})
+    wait_for(lambda: manager.standbys and all(
+        p.booted for p in manager.standbys.values()), timeout=30)
+    manager.patch_namespaced_deployment('worker', 'default',
+                                        {'spec': {'replicas': 1}})
+    wait_for(lambda: manager.list_namespaced_deployment('default')
+             .items[0].status.ready_replicas == 1, timeout=30)
+    manager.patch_namespaced_deployment('worker', 'default',
+                                        {'spec': {'replicas': 0}})
+    wait_for(lambda: [e for e in events.records
+                      if e['ev'] == 'engine_released'], timeout=30)
+    wait_for(lambda: manager.standbys and
+             not manager.standbys[0].engine_cached, timeout=30)
+    client.hset('predict:late', mapping={'status': 'new'})
+    client.lpush('predict', 'predict:late')
+    built = wait_for(lambda: [e for e in events.records
+                              if e['ev'] == 'standby_prebuilt'], timeout=30)
+    assert built[-1]['error'] is None
+    assert [e for e in events.records if e['ev'] == 'engine_rebuild']
+    view = manager.list_namespaced_deployment('default').items[0]
+    assert view.spec.replicas == 0
+    assert manager.standbys[0].engine_cached

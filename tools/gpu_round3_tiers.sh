@@ -15,6 +15,8 @@
 #        command (20 + 5 steps), then the torch plug-in
 #   bash tools/gpu_round3_tiers.sh G -> config-4 shape (60 s Poisson bursts,
 #        60 s off), resident pool vs arrival-woken deep idle
+#   bash tools/gpu_round3_tiers.sh H -> engine tier (ENGINE_IDLE_RELEASE_S=5,
+#        6 s idle gaps) with the arrival-driven engine rebuild
 set -o pipefail
 OUT=${OUT:-gpurun_out/r3_tiers}
 mkdir -p $OUT
@@ -58,4 +60,6 @@ elif [ "$1" = "F" ]; then
 elif [ "$1" = "G" ]; then
   run config4_resident 420 --gpus 1 --steps 2 --warmup 0 --on 60 --off 60 --budget-s 400 --cold-cycles 0 && \
   POOL_IDLE_RELEASE_S=0.5 run config4_deep_idle_wake 420 --gpus 1 --steps 2 --warmup 0 --on 60 --off 60 --budget-s 400 --cold-cycles 0
+elif [ "$1" = "H" ]; then
+  ENGINE_IDLE_RELEASE_S=5 run engine_release_5s_rebuild 300 --gpus 1 --steps 8 --warmup 1 --off 6 --budget-s 270 --cold-cycles 0
 fi
