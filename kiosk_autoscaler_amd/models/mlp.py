@@ -71,6 +71,10 @@ class CpuMlpEngine(object):
                 np.zeros(dim, np.float32)))
         self.dim = dim
         self._service_ms = 0.0
+        # the worker's engine cache (worker/main.py:_cached_engine) reuses
+        # an engine whose ``engine`` is set, as it does the HIP one's
+        self.engine = self
+        self.reused = False
         if stage:
             stage('device_ready')
 
@@ -116,6 +120,7 @@ class CpuMlpEngine(object):
 
     def close(self):
         self.layers = []
+        self.engine = None
 
 
 class HipMlpEngine(object):

@@ -216,10 +216,13 @@ def _prebuild_engine(backend, pin, channel):
     spec = pin.get('prebuild') or {}
     t0 = time.monotonic_ns()
     try:
+        template = {}
+        if spec.get('keys_per_pod'):
+            template['keys_per_pod'] = spec['keys_per_pod']
         cfg = WorkerConfig(os.environ, {
             'worker_id': 'standby', 'kind': spec.get('kind', 'deployment'),
             'slot': pin.get('slot', 0), 'gpu': pin.get('gpu', ''),
-            'template': {'keys_per_pod': spec.get('keys_per_pod')}})
+            'template': template})
         engine = _cached_engine(backend, cfg, None)
         if os.environ.get('WARM_START', '1').lower() not in (
                 '0', 'false', 'no', 'off'):

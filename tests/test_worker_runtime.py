@@ -1,6 +1,8 @@
 """Worker runtime: poison jobs fail on their own and
 oversized batches are split to the engine's capacity.  CPU-only, in-proc
 fake Redis, the mock CPU engine."""
+import os
+
 import pytest
 
 from kiosk_autoscaler_amd.models import mlp
@@ -212,3 +214,45 @@ def test_worker_fenced_out_stops_pulling(redis_client):
     agent.by_group[group] = {'seq': 7, 'epoch': 6, 'slots': [1]}
     assert not run.excluded()
     assert ('fenced_in', {'seq': 7}) in run.channel.events
+
+
+class _Emits(object):
+    def __init__(self):
+        self.out = []
+
+    def emit(self, ev, **fields):
+        self.out.append(dict(fields, ev=ev))
+
+
+def test_standby_prebuild_builds_the_engine_the_assignment_reuses(
+        monkeypatch):
+    """An arrival-woken standby (pin ``prebuild``) builds the engine for the
+    resource's shape before any assignment: the assignment with the same
+    model gets it from the cache; a failed prebuild leaves nothing cached
+    and reports the error."""
+    from kiosk_autoscaler_amd.worker import main as wm
+    monkeypatch.setenv('MODEL_DIM', '64')
+    monkeypatch.setenv('MODEL_HIDDEN', '128')
+    monkeypatch.setenv('MODEL_LAYERS', '1')
+    monkeypatch.setenv('ROWS_PER_KEY', '16')
+    monkeypatch.delenv('WORKER_ENGINE', raising=False)
+    wm._ENGINES.clear()
+    chan = _Emits()
+    try:
+        wm._prebuild_engine('cpu', {'slot': 0, 'gpu': '', 'prebuild': {
+            'kind': 'deployment', 'keys_per_pod': 1}}, chan)
+        built = [e for e in chan.out if e['ev'] == 'prebuilt']
+        assert built and 'error' not in built[0] and len(wm._ENGINES) == 1
+        cfg = rt.WorkerConfig(os.environ, {'worker_id': 'w', 'slot': 0})
+        engine = wm._cached_engine('cpu', cfg, None)
+        assert engine.reused is True
+        # a failure is contained: nothing stays cached
+        chan = _Emits()
+
+        def boom(*args):
+            raise RuntimeError('no device')
+        monkeypatch.setattr(wm, '_cached_engine', boom)
+        wm._prebuild_engine('cpu', {'prebuild': {}}, chan)
+        assert 'no device' in chan.out[-1]['error'] and not wm._ENGINES
+    finally:
+        wm._drop_cached_engines()
