@@ -750,6 +750,67 @@ def test_gpu_zygote_cold_spawn(resp_server, engine):
     assert all(e['ready_s'] < 10.0 for e in ups)
 
 
+@pytest.mark.gpu
+def test_gpu_arrival_woken_standby_prebuilds(resp_server):
+    """MI355X, deep idle with the arrival wake: the parked node holds no
+    process; a key's arrival forks a standby from the zygote, which opens
+    the GPU and prebuilds the engine (HBM arena, weights, forward graph)
+    before any scale-up; the scale-up then reuses that engine, so READY is
+    the warm-start kernel alone."""
+    import time
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict', 'RESOURCE_NAME': 'wake', 'MAX_PODS': '1',
+           'WORKER_BACKEND': 'hip', 'WARM_POOL': '1', 'FENCE': 'none',
+           'REDIS_INTERVAL': '0', 'GPU_IDS': '0', 'MODEL_DIM': '1024',
+           'MODEL_HIDDEN': '4096', 'MODEL_LAYERS': '2', 'ROWS_PER_KEY': '256',
+           'POOL_IDLE_RELEASE_S': '0.5', 'POOL_WAKE_POLL_S': '0.02',
+           'INTERVAL': '1'}
+    s = Settings(Config(environ=env, use_files=False))
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    events = EventLog(source='test')
+    events.keep = True
+    manager = gpumgr.build_manager(s, redis_client=client,
+                                   events=events).start()
+
+    def until(predicate, timeout=120):
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            if predicate():
+                return
+            time.sleep(0.02)
+        raise AssertionError('timed out')
+    try:
+        until(lambda: manager.pool_parked and not manager.standbys)
+        client.hset('predict:w0', mapping={'status': 'new', 'rows': 256})
+        client.lpush('predict', 'predict:w0')
+        until(lambda: any(e['ev'] == 'standby_prebuilt'
+                          for e in events.records))
+        built = [e for e in events.records if e['ev'] == 'standby_prebuilt']
+        assert built[-1]['error'] is None and built[-1]['hbm_bytes'] > 0
+        until(lambda: manager.standbys and all(
+            p.booted for p in manager.standbys.values()))
+        manager.patch_namespaced_deployment('wake', 'default',
+                                            {'spec': {'replicas': 1}})
+        until(lambda: client.hget('predict:w0', 'status') == 'done')
+        manager.patch_namespaced_deployment('wake', 'default',
+                                            {'spec': {'replicas': 0}})
+        until(lambda: not manager.status()['resources'][0]['workers'])
+    finally:
+        manager.stop(timeout=20)
+    ups = [e for e in events.records if e['ev'] == 'worker_up']
+    assigned = [e for e in events.records if e['ev'] == 'worker_assigned']
+    assert assigned[-1]['from_pool'] is True
+    print('arrival-woken standby: prebuild %.1f ms, assign -> READY %.1f ms'
+          % (built[-1]['ms'], 1e3 * ups[-1]['ready_s']))
+    # engine prebuilt: READY is the warm-start kernel (~1 ms; a fresh
+    # standby building its engine at the assignment takes ~12-17 ms)
+    assert ups[-1]['ready_s'] < 0.25
+
+
 @pytest.mark.parametrize('mode,park,expected', [
     ('device', 0.0, None),      # long-lived GPU standbys: RCCL (FENCE)
     ('device', 3.0, 'shm'),     # deep idle: new processes every wake
