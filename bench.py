@@ -633,6 +633,14 @@ def main():
     return 0 if error is None else 1
 
 
+def _setting(name):
+    """The value the autoscaler (scale.py) runs with for ``name``."""
+    from kiosk_autoscaler_amd.config import EXTRA_DEFAULTS
+    cast, default = next((c, d) for n, c, d in EXTRA_DEFAULTS if n == name)
+    value = os.environ.get(name)
+    return cast(value) if value not in (None, '') else default
+
+
 def base_line(args, episodes, elapsed):
     steps = len(episodes)
     return {
@@ -664,12 +672,10 @@ def base_line(args, episodes, elapsed):
             'warm_pool_mode': args.pool_mode,
             'worker_recycle': not args.no_recycle,
             # deep idle (standbys exit after this many idle seconds; 0 =
-            # kept) and the arrival wake's queue-read period
-            'pool_idle_release_s': float(os.environ.get(
-                'POOL_IDLE_RELEASE_S') or 0.0),
-            'pool_wake_poll_s': (float(os.environ.get('POOL_WAKE_POLL_S')
-                                       or 0.05) if os.environ.get(
-                                           'POOL_IDLE_RELEASE_S') else None),
+            # kept) and the arrival wake's queue-read period: the values
+            # scale.py runs with (environment, else the config default)
+            'pool_idle_release_s': _setting('POOL_IDLE_RELEASE_S'),
+            'pool_wake_poll_s': _setting('POOL_WAKE_POLL_S'),
         },
         'steps_requested': args.steps,
     }

@@ -144,6 +144,13 @@ class _Pipe(object):
                 pass
 
 
+# A pool that parks only after this long without demand wakes rarely: its
+# node communicator stays on RCCL (one generation per wake, ~2 s of RCCL
+# init that starts after the woken worker is READY); one that parks sooner
+# fences over host shared memory (a generation per wake in ~0.3 ms).
+RCCL_PARK_MIN_S = 60.0
+
+
 class _Process(object):
     """A child process (standby or worker) and its control pipe."""
 
@@ -383,7 +390,8 @@ class GpuManager(object):
                 self.pool_size >= len(self.slots)):
             transport = fence_transport
             if transport is None and pool_template.backend == 'hip' and \
-                    (pool_mode != 'device' or self.pool_idle_release_s > 0):
+                    (pool_mode != 'device' or
+                     0 < self.pool_idle_release_s < RCCL_PARK_MIN_S):
                 transport = 'shm'
             self.node = NodeComm(self, fence_timeout=min(fence_timeout, 30.0),
                                  init_timeout=fence_init_timeout,
@@ -846,8 +854,9 @@ class GpuManager(object):
         released = [p for p in self.standbys.values()
                     if p.booted and not p.engine_cached and
                     self.pool_mode == 'device']
-        if not self.pool_idle_release_s > 0 and released and \
-                self._arrived(now):
+        arrived = (self.pool_idle_release_s > 0 or bool(released)) and \
+            self._arrived(now)
+        if arrived and released:
             # ENGINE_IDLE_RELEASE_S freed these standbys' engines: a key's
             # arrival has them rebuild it before the scale-up tick
             for proc in released:
@@ -856,7 +865,7 @@ class GpuManager(object):
                                     self.pool_template)})
                 proc.engine_cached = True     # (until told otherwise)
             self.events.emit('engine_rebuild', standbys=len(released))
-        if self.pool_idle_release_s > 0 and self._arrived(now):
+        if arrived and self.pool_idle_release_s > 0:
             wake_at = now
             lead = self.wake_lead()
             if self.pool_parked and lead > 0 and \

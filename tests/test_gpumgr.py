@@ -814,6 +814,7 @@ def test_gpu_arrival_woken_standby_prebuilds(resp_server):
 @pytest.mark.parametrize('mode,park,expected', [
     ('device', 0.0, None),      # long-lived GPU standbys: RCCL (FENCE)
     ('device', 3.0, 'shm'),     # deep idle: new processes every wake
+    ('device', 600.0, None),    # parks after 10 min idle: rare wakes, RCCL
     ('context', 0.0, 'shm'),    # standbys without a GPU queue / HBM
     ('import', 0.0, 'shm'),
 ])

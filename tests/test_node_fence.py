@@ -1016,11 +1016,14 @@ def test_withheld_fence_holds_available_replicas(resp_server, tmp_path):
             manager.patch_namespaced_deployment('worker', 'default',
                                                 {'spec': {'replicas': 2}})
             wait_for(lambda: view().status.ready_replicas == 2, timeout=30)
+            # (under load the epoch may start a moment after READY)
+            wait_for(lambda: view().status.fence['pending'], timeout=10)
             time.sleep(0.5)
             v = view()
             assert v.status.available_replicas == 0
             assert v.status.fenced_replicas == 0
-            assert v.status.fence['pending'] and not v.status.fence['in_sync']
+            assert v.status.fence['pending'] and \
+                not v.status.fence['in_sync'], v.status.fence
             assert scaler.get_current_pods('default', 'deployment', 'worker',
                                            only_running=True) == 0
             assert scaler.get_current_pods('default', 'deployment',
