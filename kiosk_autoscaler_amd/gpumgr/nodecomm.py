@@ -150,6 +150,11 @@ class NodeComm(object):
             for worker in resource.workers.values():
                 if worker.state == 'starting':
                     return None
+        if time.monotonic() < getattr(self.m, '_wake_until', 0.0):
+            # an arrival woke the pool for a scale-up due within a tick:
+            # the generation waits for it (and then for READY), or for the
+            # hold to lapse if the tick does not scale
+            return None
         return out
 
     # ------------------------------------------------------------------

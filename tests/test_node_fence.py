@@ -1224,3 +1224,38 @@ def test_sweep_stale_shm_segments(tmp_path):
                               older_than=300.0, now=t)
     assert sorted(removed) == sorted([str(old), str(old_child)])
     assert fresh.exists() and other.exists() and not old.exists()
+
+
+@pytest.mark.slow
+def test_arrival_woken_pool_builds_its_generation_after_ready(resp_server,
+                                                              tmp_path):
+    """A pool woken by a key's arrival builds no node communicator before
+    the scale-up it was woken for: a generation's init (seconds over RCCL)
+    would compete with the assignment's warm-start.  It is built once the
+    worker is READY, and the scale-up is fenced by it."""
+    s, client, events, manager, scaler = _node_stack(
+        resp_server, 'shm', tmp_path, MAX_PODS='2', WARM_POOL='2',
+        POOL_IDLE_RELEASE_S='0.3', POOL_WAKE_POLL_S='0.02', INTERVAL='2')
+    try:
+        wait_for(lambda: manager.pool_parked and not manager.standbys,
+                 timeout=60)
+        parked_at = len(events.records)
+        client.hset('predict:a', mapping={'status': 'new', 'rows': 8})
+        client.lpush('predict', 'predict:a')
+        wait_for(lambda: len(manager.standbys) == 2 and all(
+            p.booted for p in manager.standbys.values()), timeout=60)
+        time.sleep(0.3)
+        later = events.records[parked_at:]
+        assert not [e for e in later if e['ev'] == 'node_comm_init']
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 1}})
+        wait_for(lambda: client.hget('predict:a', 'status') == 'done',
+                 timeout=30)
+        wait_for(lambda: manager.list_namespaced_deployment('default')
+                 .items[0].status.available_replicas == 1, timeout=30)
+        later = events.records[parked_at:]
+        ready = _index(later, lambda e: e['ev'] == 'worker_up')
+        init = _index(later, lambda e: e['ev'] == 'node_comm_init')
+        assert ready is not None and init is not None and init > ready
+    finally:
+        manager.stop(timeout=15)
