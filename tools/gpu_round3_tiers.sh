@@ -17,6 +17,8 @@
 #        60 s off), resident pool vs arrival-woken deep idle
 #   bash tools/gpu_round3_tiers.sh H -> engine tier (ENGINE_IDLE_RELEASE_S=5,
 #        6 s idle gaps) with the arrival-driven engine rebuild
+#   bash tools/gpu_round3_tiers.sh I -> deep idle that keeps RCCL (release
+#        60 s, 65 s idle gaps): wake, READY, then the RCCL generation
 set -o pipefail
 OUT=${OUT:-gpurun_out/r3_tiers}
 mkdir -p $OUT
@@ -62,4 +64,6 @@ elif [ "$1" = "G" ]; then
   POOL_IDLE_RELEASE_S=0.5 run config4_deep_idle_wake 420 --gpus 1 --steps 2 --warmup 0 --on 60 --off 60 --budget-s 400 --cold-cycles 0
 elif [ "$1" = "H" ]; then
   ENGINE_IDLE_RELEASE_S=5 run engine_release_5s_rebuild 300 --gpus 1 --steps 8 --warmup 1 --off 6 --budget-s 270 --cold-cycles 0
+elif [ "$1" = "I" ]; then
+  POOL_IDLE_RELEASE_S=60 run deep_idle_rccl_60s 420 --gpus 1 --steps 3 --warmup 0 --off 65 --budget-s 400 --cold-cycles 0
 fi
