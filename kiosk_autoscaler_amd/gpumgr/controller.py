@@ -1160,8 +1160,6 @@ class GpuManager(object):
         }
         proc = self._take_standby(resource.template, slot)
         from_pool = proc is not None
-        if from_pool and self.node is not None:
-            self.node.preempt_for(proc)
         if from_pool and proc.hbm_free:
             self._size_from_free(resource, assign, proc.hbm_free, slot)
         if from_pool:

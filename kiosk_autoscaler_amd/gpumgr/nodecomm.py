@@ -29,7 +29,6 @@ logger = logging.getLogger('NodeComm')
 NONE, INIT, READY, SHRINK = 'none', 'init', 'ready', 'shrink'
 # worker -> manager messages of the node agent (parallel.nodefence)
 NODE_EVENTS = ('comm_uid', 'comm_ready', 'fenced', 'node_agent')
-PREEMPT_MAX = 2
 
 
 class NodeComm(object):
@@ -88,9 +87,6 @@ class NodeComm(object):
         self.can_shrink = False
         self.fallback_used = None
         self.last_error = None   # why the last generation / shrink failed
-        # generations a scale-up preempted since the last one that came up
-        # (at most PREEMPT_MAX in a row: sustained churn cannot starve it)
-        self.preempted = 0
 
     # ------------------------------------------------------------------
     @property
@@ -216,21 +212,6 @@ class NodeComm(object):
             self._open_verdict('fence', set(), now - self.hang_grace,
                                'fence seq %d timed out' % seq, seq=seq)
             self._conclude(now)
-
-    def preempt_for(self, proc):
-        """A scale-up is about to assign ``proc`` while the generation it
-        is a member of is still initialising: drop that generation (not a
-        failure) so its communicator init -- seconds over RCCL, which holds
-        the device -- does not run beside the assignment's warm-start; it
-        is rebuilt once the worker is READY (``candidates``).  At most
-        ``PREEMPT_MAX`` generations in a row are preempted.  True if it
-        was."""
-        if self.state != INIT or self.preempted >= PREEMPT_MAX or \
-                not any(p is proc for _, p in self.members):
-            return False
-        self.preempted += 1
-        self.break_('preempted by a scale-up on slot %s' % proc.slot)
-        return True
 
     def _open_verdict(self, kind, reported, now, detail, seq=None):
         self.verdict = {'kind': kind, 'reported': set(reported), 't0': now,
@@ -421,7 +402,6 @@ class NodeComm(object):
                     self.shrinks += 1
                 else:
                     self.failures = 0
-                    self.preempted = 0
                     self.generations += 1
                 self.m.events.emit('node_comm_ready', gen=self.gen,
                                    sub=self.sub, n=len(self.members),
