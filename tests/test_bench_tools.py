@@ -193,6 +193,10 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
     line = json.loads(lines[0])
     assert line['n_gpus'] == 2 and line['config']['max_pods'] == 2
     assert line['keys_done'] == line['keys'] > 0
+    # the pool settings scale.py ran with (config defaults, env unset)
+    if 'POOL_IDLE_RELEASE_S' not in os.environ:
+        assert line['config']['pool_idle_release_s'] == 600.0
+        assert line['config']['pool_wake_poll_s'] == 0.05
 
 
 def test_util_sampler_degrades_without_driver():
