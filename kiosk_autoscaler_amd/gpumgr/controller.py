@@ -149,9 +149,6 @@ class _Pipe(object):
 # init that starts after the woken worker is READY); one that parks sooner
 # fences over host shared memory (a generation per wake in ~0.3 ms).
 RCCL_PARK_MIN_S = 60.0
-# device-mode HIP standbys build their engine at boot (KIOSK_PREBUILD_AT_BOOT=1,
-# opt-in while it is measured): see GpuManager._spawn
-PREBUILD_AT_BOOT = os.environ.get('KIOSK_PREBUILD_AT_BOOT', '0') == '1'
 
 
 class _Process(object):
@@ -771,24 +768,13 @@ class GpuManager(object):
         # due within a tick, so it builds the engine now, not at the assign
         woken = (assign is None and slot is not None and role == 'standby'
                  and time.monotonic() < self._wake_until)
-        # a device-mode standby builds its engine at boot, before it joins
-        # a node-communicator generation: an assignment that lands during
-        # the generation's RCCL init (seconds, holding the device) then
-        # needs only the warm-start kernel; ENGINE_IDLE_RELEASE_S frees it
-        # if the slot stays idle
-        prebuild = woken or (assign is None and slot is not None and
-                             role == 'standby' and
-                             self.pool_mode == 'device' and
-                             self.pool_template is not None and
-                             template.backend == 'hip' and
-                             PREBUILD_AT_BOOT)
         if assign is not None:
             args += ['--assign', json.dumps(assign)]
         elif slot is not None:
             pin = {'gpu': slot.visible_id, 'slot': slot.index,
                    'cpus': slot.cpus, 'preinit': self.pool_mode,
                    'node_fence': self.node is not None}
-            if prebuild:
+            if woken:
                 pin['prebuild'] = self._prebuild_spec(template)
             args += ['--pin', json.dumps(pin)]
         env = self._environment(template)

@@ -391,13 +391,11 @@ def main(argv=None):
     if pin is not None and not args.assign:
         _preimport(backend)
         _preconnect()
-    if pin is not None and pin.get('prebuild') and not args.assign:
-        # before the node agent: a generation's RCCL init must not run
-        # beside the engine build
-        _prebuild_engine(backend, pin, channel)
     node_agent = None
     if node:
         node_agent = _start_node_agent(channel, backend, early.get('slot', 0))
+    if pin is not None and pin.get('prebuild') and not args.assign:
+        _prebuild_engine(backend, pin, channel)
     assignment = parse_assignment(args.assign) if args.assign else None
     recycles = 0
     max_recycles = int(os.environ.get('WORKER_MAX_RECYCLES', 64))
