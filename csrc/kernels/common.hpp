@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "launch.hpp"
+
 namespace kiosk {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;

@@ -158,9 +158,10 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
 
 template <int EPI>
 hipError_t configure_epi() {
-  return hipFuncSetAttribute(
+  hipError_t err = hipFuncSetAttribute(
       reinterpret_cast<const void*>(&gemm_bf16_tn_kernel<EPI>),
       hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLdsBytes);
+  return err == hipSuccess ? prepare_kernel(&gemm_bf16_tn_kernel<EPI>) : err;
 }
 
 template <int EPI>
@@ -168,21 +169,25 @@ hipError_t launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C,
                       const float* bias, const uint16_t* R, int M, int N,
                       int K, hipStream_t stream) {
   const int blocks = ((M + BM - 1) / BM) * (N / BN);
-  hipLaunchKernelGGL(gemm_bf16_tn_kernel<EPI>, dim3(blocks),
+  return launch_kernel(&gemm_bf16_tn_kernel<EPI>, dim3(blocks),
                      dim3(kGemmThreads), kGemmLdsBytes, stream, A, B, C, bias,
                      R, M, N, K);
-  return hipGetLastError();
 }
 
 }  // namespace
 
-// Raise the dynamic-LDS limit once, outside any graph capture.
+// Raise the dynamic-LDS limits and resolve every launch handle once,
+// outside any graph capture (later calls return the first result: these
+// runtime calls take the registry lock, see launch.hpp).
 hipError_t gemm_prepare() {
-  hipError_t err = configure_epi<EPI_NONE>();
-  if (err == hipSuccess) err = configure_epi<EPI_BIAS_GELU>();
-  if (err == hipSuccess) err = configure_epi<EPI_BIAS_RESIDUAL>();
-  if (err == hipSuccess) err = gemm256_prepare();
-  return err;
+  static hipError_t result = [] {
+    hipError_t err = configure_epi<EPI_NONE>();
+    if (err == hipSuccess) err = configure_epi<EPI_BIAS_GELU>();
+    if (err == hipSuccess) err = configure_epi<EPI_BIAS_RESIDUAL>();
+    if (err == hipSuccess) err = gemm256_prepare();
+    return err;
+  }();
+  return result;
 }
 
 int gemm_pick_variant(int M, int N, int K, bool have_workspace) {

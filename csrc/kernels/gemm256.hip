@@ -799,9 +799,11 @@ int g_group_m = 4;
 
 template <int EPI, int BN, int W>
 hipError_t configure256() {
-  return hipFuncSetAttribute(
+  hipError_t err = hipFuncSetAttribute(
       reinterpret_cast<const void*>(&gemm256_kernel<EPI, BN, W>),
       hipFuncAttributeMaxDynamicSharedMemorySize, Geo<BN, W>::kLdsBytes);
+  return err == hipSuccess ? prepare_kernel(&gemm256_kernel<EPI, BN, W>)
+                           : err;
 }
 
 template <int BN, int W>
@@ -823,25 +825,20 @@ hipError_t launch256(const uint16_t* A, const uint16_t* B, uint16_t* C,
   const int lds = Geo<BN, W>::kLdsBytes;
   switch (epilogue) {
     case EPI_NONE:
-      hipLaunchKernelGGL((gemm256_kernel<EPI_NONE, BN, W>), grid, block, lds,
+      return launch_kernel(&gemm256_kernel<EPI_NONE, BN, W>, grid, block, lds,
                          stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr, g_group_m);
-      break;
     case EPI_BIAS_GELU:
-      hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_GELU, BN, W>), grid, block,
+      return launch_kernel(&gemm256_kernel<EPI_BIAS_GELU, BN, W>, grid, block,
                          lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr, g_group_m);
-      break;
     case EPI_BIAS_RESIDUAL:
-      hipLaunchKernelGGL((gemm256_kernel<EPI_BIAS_RESIDUAL, BN, W>), grid,
+      return launch_kernel(&gemm256_kernel<EPI_BIAS_RESIDUAL, BN, W>, grid,
                          block, lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr, g_group_m);
-      break;
     case EPI_PARTIAL:
-      hipLaunchKernelGGL((gemm256_kernel<EPI_PARTIAL, BN, W>), grid, block,
+      return launch_kernel(&gemm256_kernel<EPI_PARTIAL, BN, W>, grid, block,
                          lds, stream, A, B, C, bias, R, M, N, K, lda, nullptr, nullptr, g_group_m);
-      break;
     default:
       return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 // persistent 4-wave kernel: one workgroup per CU (its 160 KiB of LDS allow
@@ -850,17 +847,20 @@ int g_cu_count = 256;
 
 template <int EPI>
 hipError_t configure_persist() {
-  return hipFuncSetAttribute(
+  hipError_t err = hipFuncSetAttribute(
       reinterpret_cast<const void*>(&gemm256_kernel<EPI, 256, 4, 0, 1>),
       hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256, 4>::kLdsBytes);
+  return err == hipSuccess
+             ? prepare_kernel(&gemm256_kernel<EPI, 256, 4, 0, 1>)
+             : err;
 }
 
 template <int EPI>
-void launch_persist_epi(const uint16_t* A, const uint16_t* B, uint16_t* C,
+hipError_t launch_persist_epi(const uint16_t* A, const uint16_t* B, uint16_t* C,
                         const float* bias, const uint16_t* R, int M, int N,
                         int K, int grid, hipStream_t stream) {
   constexpr int lds = Geo<256, 4>::kLdsBytes;
-  hipLaunchKernelGGL((gemm256_kernel<EPI, 256, 4, 0, 1>), dim3(grid),
+  return launch_kernel(&gemm256_kernel<EPI, 256, 4, 0, 1>, dim3(grid),
                      dim3(256), lds, stream, A, B, C, bias, R, M, N, K, K,
                      nullptr, nullptr, g_group_m);
 }
@@ -872,17 +872,18 @@ hipError_t launch_fused4(const uint16_t* A, const uint16_t* B, uint16_t* C,
                          hipStream_t stream) {
   const int blocks = ((M + BM - 1) / BM) * (N / 256);
   constexpr int lds = Geo<256, 4>::kLdsBytes;
-  hipLaunchKernelGGL((gemm256_kernel<EPI, 256, 4, kMode>),
+  return launch_kernel(&gemm256_kernel<EPI, 256, 4, kMode>,
                      dim3(blocks, splits), dim3(256), lds, stream, A, B, C,
                      bias, R, M, N, K, lda, P, cnt, g_group_m);
-  return hipGetLastError();
 }
 
 template <int EPI>
 hipError_t configure_fused4() {
-  return hipFuncSetAttribute(
+  hipError_t err = hipFuncSetAttribute(
       reinterpret_cast<const void*>(&gemm256_kernel<EPI, 256, 4, 1>),
       hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256, 4>::kLdsBytes);
+  return err == hipSuccess ? prepare_kernel(&gemm256_kernel<EPI, 256, 4, 1>)
+                           : err;
 }
 
 template <int kMode>
@@ -970,22 +971,18 @@ hipError_t launch_reduce(const float* P, int splits, int M, int N,
       std::min<size_t>((chunks + 255) / 256, 256 * 16));
   switch (epilogue) {
     case EPI_NONE:
-      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_NONE>, dim3(blocks),
+      return launch_kernel(&splitk_reduce_kernel<EPI_NONE>, dim3(blocks),
                          dim3(256), 0, stream, P, splits, M, N, bias, R, out);
-      break;
     case EPI_BIAS_GELU:
-      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_BIAS_GELU>, dim3(blocks),
+      return launch_kernel(&splitk_reduce_kernel<EPI_BIAS_GELU>, dim3(blocks),
                          dim3(256), 0, stream, P, splits, M, N, bias, R, out);
-      break;
     case EPI_BIAS_RESIDUAL:
-      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_BIAS_RESIDUAL>,
+      return launch_kernel(&splitk_reduce_kernel<EPI_BIAS_RESIDUAL>,
                          dim3(blocks), dim3(256), 0, stream, P, splits, M, N,
                          bias, R, out);
-      break;
     default:
       return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 }  // namespace
@@ -1005,6 +1002,11 @@ hipError_t gemm256_prepare() {
   if (err == hipSuccess) err = configure_fused4<EPI_NONE>();
   if (err == hipSuccess) err = configure_fused4<EPI_BIAS_GELU>();
   if (err == hipSuccess) err = configure_fused4<EPI_BIAS_RESIDUAL>();
+  if (err == hipSuccess) err = prepare_kernel(&splitk_reduce_kernel<EPI_NONE>);
+  if (err == hipSuccess)
+    err = prepare_kernel(&splitk_reduce_kernel<EPI_BIAS_GELU>);
+  if (err == hipSuccess)
+    err = prepare_kernel(&splitk_reduce_kernel<EPI_BIAS_RESIDUAL>);
   return err;
 }
 
@@ -1047,20 +1049,17 @@ hipError_t launch_gemm256_persist(const uint16_t* A, const uint16_t* B,
   const int grid = tiles < g_cu_count ? tiles : g_cu_count;
   switch (epilogue) {
     case EPI_NONE:
-      launch_persist_epi<EPI_NONE>(A, B, C, bias, R, M, N, K, grid, stream);
-      break;
+      return launch_persist_epi<EPI_NONE>(A, B, C, bias, R, M, N, K, grid,
+                                          stream);
     case EPI_BIAS_GELU:
-      launch_persist_epi<EPI_BIAS_GELU>(A, B, C, bias, R, M, N, K, grid,
-                                        stream);
-      break;
+      return launch_persist_epi<EPI_BIAS_GELU>(A, B, C, bias, R, M, N, K,
+                                               grid, stream);
     case EPI_BIAS_RESIDUAL:
-      launch_persist_epi<EPI_BIAS_RESIDUAL>(A, B, C, bias, R, M, N, K, grid,
-                                            stream);
-      break;
+      return launch_persist_epi<EPI_BIAS_RESIDUAL>(A, B, C, bias, R, M, N, K,
+                                                   grid, stream);
     default:
       return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 int gemm256_splits(int M, int N, int K) {

@@ -3,6 +3,10 @@
 // Weight init runs on the device so a scale-up never generates or copies a
 // GB of host-side random numbers: at the HBM rate the
 // 1 GiB default model initialises in well under a millisecond.
+#include <mutex>
+#include <utility>
+#include <vector>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -117,33 +121,29 @@ int init_blocks(size_t n) {
 
 hipError_t launch_init_uniform_bf16(uint16_t* p, size_t n, uint64_t seed,
                                     float lo, float hi, hipStream_t stream) {
-  hipLaunchKernelGGL(init_bf16_kernel, dim3(init_blocks(n)),
+  return launch_kernel(&init_bf16_kernel, dim3(init_blocks(n)),
                      dim3(kInitThreads), 0, stream, p, n, seed,
                      static_cast<const uint64_t*>(nullptr), lo, hi - lo);
-  return hipGetLastError();
 }
 
 hipError_t launch_init_uniform_bf16_devseed(uint16_t* p, size_t n,
                                             const uint64_t* seed, float lo,
                                             float hi, hipStream_t stream) {
-  hipLaunchKernelGGL(init_bf16_kernel, dim3(init_blocks(n)),
+  return launch_kernel(&init_bf16_kernel, dim3(init_blocks(n)),
                      dim3(kInitThreads), 0, stream, p, n, uint64_t(0), seed,
                      lo, hi - lo);
-  return hipGetLastError();
 }
 
 hipError_t launch_init_uniform_f32(float* p, size_t n, uint64_t seed,
                                    float lo, float hi, hipStream_t stream) {
-  hipLaunchKernelGGL(init_f32_kernel, dim3(init_blocks(n)),
+  return launch_kernel(&init_f32_kernel, dim3(init_blocks(n)),
                      dim3(kInitThreads), 0, stream, p, n, seed, lo, hi - lo);
-  return hipGetLastError();
 }
 
 hipError_t launch_partial_sums(const uint16_t* p, size_t n, float* partials,
                                hipStream_t stream) {
-  hipLaunchKernelGGL(partial_sums_kernel, dim3(kSumBlocks), dim3(256),
+  return launch_kernel(&partial_sums_kernel, dim3(kSumBlocks), dim3(256),
                      4 * sizeof(float), stream, p, n, partials);
-  return hipGetLastError();
 }
 
 hipError_t launch_spin(double ms, unsigned int* done, hipStream_t stream) {
@@ -151,16 +151,55 @@ hipError_t launch_spin(double ms, unsigned int* done, hipStream_t stream) {
   ms = ms > kSpinMaxMs ? kSpinMaxMs : ms;
   const unsigned long long ticks =
       static_cast<unsigned long long>(ms * 1e5);   // 100 MHz
-  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, stream, ticks, done);
-  return hipGetLastError();
+  return launch_kernel(&spin_kernel, dim3(1), dim3(64), 0, stream, ticks, done);
 }
 
 // Loads this file's code object (first use of any of its kernels does;
-// querying attributes does it without a launch, so no hardware queue).
+// querying attributes does it without a launch, so no hardware queue) and
+// resolves every kernel's launch handle.
 hipError_t misc_prepare() {
-  hipFuncAttributes attr;
-  return hipFuncGetAttributes(&attr,
-                              reinterpret_cast<const void*>(&init_bf16_kernel));
+  static hipError_t result = [] {
+    hipFuncAttributes attr;
+    hipError_t err = hipFuncGetAttributes(
+        &attr, reinterpret_cast<const void*>(&init_bf16_kernel));
+    if (err == hipSuccess) err = prepare_kernel(&init_bf16_kernel);
+    if (err == hipSuccess) err = prepare_kernel(&init_f32_kernel);
+    if (err == hipSuccess) err = prepare_kernel(&partial_sums_kernel);
+    if (err == hipSuccess) err = prepare_kernel(&spin_kernel);
+    return err;
+  }();
+  return result;
+}
+
+namespace {
+
+// stub -> handle; a handful of kernels, looked up on every launch
+struct KernelCache {
+  std::mutex mu;
+  std::vector<std::pair<const void*, hipFunction_t>> entries;
+};
+
+KernelCache& kernel_cache() {
+  static KernelCache* cache = new KernelCache();   // never destroyed
+  return *cache;
+}
+
+}  // namespace
+
+hipFunction_t resolve_kernel(const void* stub) {
+  KernelCache& cache = kernel_cache();
+  {
+    std::lock_guard<std::mutex> lock(cache.mu);
+    for (const auto& e : cache.entries) {
+      if (e.first == stub) return e.second;
+    }
+  }
+  // outside our mutex: this call may wait on the runtime's registry lock
+  hipFunction_t f = nullptr;
+  if (hipGetFuncBySymbol(&f, stub) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(cache.mu);
+  cache.entries.emplace_back(stub, f);
+  return f;
 }
 
 }  // namespace kiosk

@@ -108,19 +108,27 @@ __global__ __launch_bounds__(256) void warmstart_kernel(
 hipError_t launch_warmstart(const uint16_t* w, size_t n, uint32_t* record,
                             int nblocks, int iters, int lds_bytes,
                             hipStream_t stream) {
-  hipError_t err = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&warmstart_kernel),
-      hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-  if (err != hipSuccess) return err;
-  hipLaunchKernelGGL(warmstart_kernel, dim3(nblocks), dim3(256), lds_bytes,
+  // the dynamic-LDS limit was raised to the ring's size at prepare time; a
+  // larger request (never the engine's) raises it here
+  if (lds_bytes > kGemmRingLdsBytes) {
+    hipError_t err = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&warmstart_kernel),
+        hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    if (err != hipSuccess) return err;
+  }
+  return launch_kernel(&warmstart_kernel, dim3(nblocks), dim3(256), lds_bytes,
                      stream, w, n, record, iters, lds_bytes);
-  return hipGetLastError();
 }
 
 hipError_t warmstart_prepare() {
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(&warmstart_kernel),
-                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                             kGemmRingLdsBytes);
+  static hipError_t result = [] {
+    hipError_t err = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&warmstart_kernel),
+        hipFuncAttributeMaxDynamicSharedMemorySize, kGemmRingLdsBytes);
+    if (err == hipSuccess) err = prepare_kernel(&warmstart_kernel);
+    return err;
+  }();
+  return result;
 }
 
 }  // namespace kiosk

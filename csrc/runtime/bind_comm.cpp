@@ -24,6 +24,8 @@ void bind_comm(py::module_& m) {
         py::call_guard<py::gil_scoped_release>());
   m.def("fence_warmup", &rccl_warmup, py::arg("timeout") = 60.0,
         py::call_guard<py::gil_scoped_release>());
+  m.def("fence_preload", &rccl_preload,
+        py::call_guard<py::gil_scoped_release>());
   m.def("fence_unique_id", [] {
     std::string id;
     {
@@ -69,7 +71,9 @@ void bind_comm(py::module_& m) {
       .def("request_interrupt", &Fence::request_interrupt)
       .def_property_readonly("abort_requested", &Fence::abort_requested)
       .def_property_readonly("nranks", &Fence::nranks)
-      .def_property_readonly("rank", &Fence::rank);
+      .def_property_readonly("rank", &Fence::rank)
+      .def("set_timeout", &Fence::set_timeout, py::arg("timeout"))
+      .def_property_readonly("timeout", &Fence::timeout);
 
   m.def("shm_unique_id", &shm_unique_id, py::arg("dir") = "");
   py::class_<ShmComm>(m, "ShmComm")

@@ -94,7 +94,11 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   check_hip(hipSetDevice(device), "hipSetDevice");
   check_hip(hipFree(nullptr), "hip context init");
   stages.emplace_back("preinit_context", monotonic_ns());
+  // every launch handle resolved now: no later launch consults the
+  // runtime's fat-binary registry (kernels/launch.hpp)
   check_hip(gemm_prepare(), "gemm_prepare");
+  check_hip(misc_prepare(), "misc_prepare");
+  check_hip(warmstart_prepare(), "warmstart_prepare");
   hipStream_t stream = take_kept_stream(device);
   if (!stream) {
     check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking),
@@ -217,7 +221,9 @@ void Engine::init(int device, unsigned long long seed) {
   }
   check_hip(hipEventCreate(&ev0_), "hipEventCreate");
   check_hip(hipEventCreate(&ev1_), "hipEventCreate");
-  check_hip(gemm_prepare(), "gemm_prepare");
+  check_hip(gemm_prepare(), "gemm_prepare");   // (no-ops after preinit)
+  check_hip(misc_prepare(), "misc_prepare");
+  check_hip(warmstart_prepare(), "warmstart_prepare");
   stage("stream_ready");
 
   // One arena: per-layer W1 [H,D], b1 [H], W2 [D,H], b2 [D]; then x, y, h,
@@ -306,7 +312,15 @@ void Engine::close() {
     hipGraphDestroy(kv.second.first);
   }
   graphs_.clear();
+  if (warm_exec_) hipGraphExecDestroy(warm_exec_);
+  if (warm_graph_) hipGraphDestroy(warm_graph_);
+  warm_exec_ = nullptr;
+  warm_graph_ = nullptr;
   if (stream_) hipStreamSynchronize(stream_);
+  if (warm_rec_) hipFree(warm_rec_);
+  if (warm_host_) hipHostFree(warm_host_);
+  warm_rec_ = nullptr;
+  warm_host_ = nullptr;
   if (arena_) hipFree(arena_);
   if (seed_host_) hipHostFree(seed_host_);
   if (partials_host_) hipHostFree(partials_host_);
@@ -320,6 +334,46 @@ void Engine::close() {
   ev0_ = ev1_ = nullptr;
 }
 
+void Engine::build_warm_graph(int iters, int lds_bytes) {
+  TraceRange range("kiosk.warm_graph");
+  if (warm_exec_) hipGraphExecDestroy(warm_exec_);
+  if (warm_graph_) hipGraphDestroy(warm_graph_);
+  warm_exec_ = nullptr;
+  warm_graph_ = nullptr;
+  const size_t words = size_t(cu_count_) * kWarmRecordWords;
+  if (!warm_rec_) {
+    check_hip(hipMalloc(reinterpret_cast<void**>(&warm_rec_), words * 4),
+              "hipMalloc(warm record)");
+    check_hip(hipHostMalloc(reinterpret_cast<void**>(&warm_host_), words * 4),
+              "hipHostMalloc(warm record)");
+  }
+  hipGraph_t graph = nullptr;
+  check_hip(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal),
+            "begin warm capture");
+  hipError_t err = hipMemsetAsync(warm_rec_, 0, words * 4, stream_);
+  if (err == hipSuccess)
+    err = launch_warmstart(w1_[0], size_t(hidden_) * dim_, warm_rec_,
+                           cu_count_, iters, lds_bytes, stream_);
+  if (err == hipSuccess)
+    err = hipMemcpyAsync(warm_host_, warm_rec_, words * 4,
+                         hipMemcpyDeviceToHost, stream_);
+  hipError_t end = hipStreamEndCapture(stream_, &graph);
+  if (err != hipSuccess || end != hipSuccess) {
+    if (graph) hipGraphDestroy(graph);
+    check_hip(err != hipSuccess ? err : end, "warm-start capture");
+  }
+  hipGraphExec_t exec = nullptr;
+  err = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  if (err != hipSuccess) {
+    hipGraphDestroy(graph);
+    check_hip(err, "warm graph instantiate");
+  }
+  warm_graph_ = graph;
+  warm_exec_ = exec;
+  warm_iters_ = iters;
+  warm_lds_ = lds_bytes;
+}
+
 WarmStartResult Engine::warmstart(int iters, int lds_bytes) {
   if (closed_) throw std::runtime_error("engine closed");
   TraceRange range("kiosk.warmstart");
@@ -328,25 +382,14 @@ WarmStartResult Engine::warmstart(int iters, int lds_bytes) {
   r.iters = iters;
   r.lds_bytes = lds_bytes;
   const long long t0 = monotonic_ns();
-  uint32_t* rec = nullptr;
+  if (!warm_exec_ || warm_iters_ != iters || warm_lds_ != lds_bytes)
+    build_warm_graph(iters, lds_bytes);
   const size_t words = size_t(r.blocks) * kWarmRecordWords;
-  check_hip(hipMalloc(reinterpret_cast<void**>(&rec), words * 4),
-            "hipMalloc(warm record)");
-  check_hip(hipMemsetAsync(rec, 0, words * 4, stream_), "memset record");
   check_hip(hipEventRecord(ev0_, stream_), "event");
-  hipError_t err = launch_warmstart(w1_[0], size_t(hidden_) * dim_, rec,
-                                    r.blocks, iters, lds_bytes, stream_);
-  if (err != hipSuccess) {
-    hipFree(rec);
-    check_hip(err, "launch_warmstart");
-  }
+  check_hip(hipGraphLaunch(warm_exec_, stream_), "warm graph launch");
   check_hip(hipEventRecord(ev1_, stream_), "event");
-  std::vector<uint32_t> host(words);
-  check_hip(hipMemcpyAsync(host.data(), rec, words * 4, hipMemcpyDeviceToHost,
-                           stream_),
-            "copy record");
   check_hip(hipStreamSynchronize(stream_), "warmstart sync");
-  hipFree(rec);
+  std::vector<uint32_t> host(warm_host_, warm_host_ + words);
   float ms = 0;
   hipEventElapsedTime(&ms, ev0_, ev1_);
   r.kernel_us = ms * 1e3;

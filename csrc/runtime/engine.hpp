@@ -90,6 +90,7 @@ class Engine {
   void init(int device, unsigned long long seed);   // constructor body
   void enqueue_forward(int rows);              // one pass on stream_
   void launch_or_throw(hipError_t err, const char* what);
+  void build_warm_graph(int iters, int lds_bytes);
 
   int device_ = 0;
   int dim_, hidden_, layers_, max_rows_;
@@ -108,6 +109,15 @@ class Engine {
   float* workspace_ = nullptr;     // split-K fp32 partials (may be null)
   size_t workspace_bytes_ = 0;
   unsigned long long* seed_dev_ = nullptr;
+  // N1 as one instantiated graph (memset record -> warm-start kernel ->
+  // record to pinned host): a READY after the first is a hipGraphLaunch,
+  // which -- unlike a kernel launch -- never waits on the HIP runtime lock
+  // RCCL holds while it loads (profiles/r4_collision)
+  hipGraph_t warm_graph_ = nullptr;
+  hipGraphExec_t warm_exec_ = nullptr;
+  int warm_iters_ = -1, warm_lds_ = -1;
+  uint32_t* warm_rec_ = nullptr;       // device record, blocks x words
+  uint32_t* warm_host_ = nullptr;      // pinned copy
   unsigned long long* seed_host_ = nullptr;   // pinned staging
   float* partials_host_ = nullptr;            // pinned
   std::map<int, std::pair<hipGraph_t, hipGraphExec_t>> graphs_;

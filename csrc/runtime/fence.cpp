@@ -125,6 +125,13 @@ std::string rccl_unique_id() {
   return std::string(id.internal, sizeof(id.internal));
 }
 
+double rccl_preload() {
+  const double t0 = now_s();
+  rccl_version();
+  (void)rccl_unique_id();
+  return (now_s() - t0) * 1e3;
+}
+
 double rccl_warmup(double timeout_s) {
   const double t0 = now_s();
   Fence fence(rccl_unique_id(), 1, 0, timeout_s);

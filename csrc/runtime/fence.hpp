@@ -25,6 +25,12 @@ std::string rccl_unique_id();     // 128 raw bytes
 // loads the library, builds and destroys a 1-rank communicator on the
 // current device (RCCL device code + proxy setup), returns elapsed ms.
 double rccl_warmup(double timeout_s);
+// The per-process one-time costs of RCCL, paid by the node agent when the
+// process starts (not by its first generation): dlopen (the fat binary's
+// registration, ~1.1 s of CPU, far more from a cold page cache) and the
+// library init of ncclGetUniqueId.  No communicator, no device memory.
+// Returns elapsed ms.
+double rccl_preload();
 
 // A blocked collective given up on request_interrupt(): the communicator
 // is NOT aborted, so the survivors can still shrink it (a peer died).
@@ -67,6 +73,10 @@ class Fence {
   void request_interrupt();
   int nranks() const { return nranks_; }
   int rank() const { return rank_; }
+  // Owner thread: the bound of later collectives / shrinks (a first
+  // generation connects under a longer one than its all-reduces use).
+  void set_timeout(double timeout_s) { timeout_s_ = timeout_s; }
+  double timeout() const { return timeout_s_; }
 
  private:
   void wait_ready(void* comm, double timeout_s, const char* what);

@@ -154,9 +154,8 @@ EXTRA_DEFAULTS = (
     ('WARM_POOL_MODE', str, 'device'),
     # s with no demand after which the standbys exit (0 = keep them): the
     # node then holds no GPU, like the reference at zero replicas; a key's
-    # arrival wakes the pool ahead of the scale-up tick (below).  Below
-    # 60 s the node communicator runs over shared memory, from 60 s on it
-    # stays on RCCL (gpumgr/controller.py RCCL_PARK_MIN_S)
+    # arrival wakes the pool ahead of the scale-up tick (below); each wake
+    # builds a new RCCL node communicator after the woken worker is READY
     ('POOL_IDLE_RELEASE_S', float, 600.0),
     # with POOL_IDLE_RELEASE_S: s between queue-length reads while no worker
     # runs; a new key refills a parked pool before the scale-up tick (the

@@ -28,7 +28,8 @@ logger = logging.getLogger('NodeComm')
 
 NONE, INIT, READY, SHRINK = 'none', 'init', 'ready', 'shrink'
 # worker -> manager messages of the node agent (parallel.nodefence)
-NODE_EVENTS = ('comm_uid', 'comm_ready', 'fenced', 'node_agent')
+NODE_EVENTS = ('comm_uid', 'comm_ready', 'fenced', 'node_agent',
+               'node_preloaded')
 
 
 class NodeComm(object):
@@ -43,7 +44,8 @@ class NodeComm(object):
 
     def __init__(self, manager, init_timeout=12.0, fence_timeout=30.0,
                  fallback='shm', fallback_after=2, transport=None,
-                 shrink=True, shrink_grace=0.1, hang_grace=2.0):
+                 shrink=True, shrink_grace=0.1, hang_grace=2.0,
+                 first_init_timeout=None, rccl_retry_s=120.0):
         self.m = manager
         # after ``fallback_after`` consecutive failed generations the next
         # ones use the ``fallback`` transport (every rank switches in its
@@ -52,6 +54,15 @@ class NodeComm(object):
         self.fallback = fallback or None
         self.fallback_after = max(1, int(fallback_after))
         self.transport_override = transport or None
+        self.configured_transport = self.transport_override
+        # after a fallback, the configured transport is tried again on an
+        # idle node this long later (doubling per fallback, capped at 1 h):
+        # one slow first RCCL init must not leave the node on shared memory
+        # for good (VERDICT r3 missing 3)
+        self.rccl_retry_s = float(rccl_retry_s)
+        self.rccl_retry_at = None
+        self.fallbacks = 0
+        self.rccl_retries = 0
         self.shrink_enabled = bool(shrink)
         # losses are collected this long before one shrink excludes them
         # all: workers drained by one scale-down retire within milliseconds
@@ -68,7 +79,15 @@ class NodeComm(object):
         self.hang_grace = float(hang_grace)
         self.verdict = None      # {'kind', 'reported', 't0', 'detail', 'seq'}
         self.hung_kills = 0
+        self.quarantines = 0     # hung serving workers left out, not killed
         self.init_timeout = float(init_timeout)
+        # a generation with a process that never connected over RCCL pays
+        # RCCL's per-process code-object load and, at 8 ranks, eight of them
+        # at once: it gets this longer budget (FENCE_INIT_TIMEOUT is for
+        # warm regrows and shrinks)
+        self.first_init_timeout = float(first_init_timeout or max(
+            60.0, 5.0 * self.init_timeout))
+        self.gen_timeout = self.init_timeout
         self.fence_timeout = float(fence_timeout)
         self.gen = 0
         self.sub = 0             # shrinks applied to this generation
@@ -80,7 +99,7 @@ class NodeComm(object):
         self.failed_total = 0
         self.retry_at = 0.0
         self.seq = 0             # node-wide fence sequence number
-        self.inflight = None     # dict: resource, epoch, seq, members, t
+        self._inflight = None    # dict: resource, epoch, seq, members, t
         self.generations = 0     # communicators built (for tests/metrics)
         self.shrinks = 0         # successful shrinks (for tests/metrics)
         self.transport = None
@@ -89,6 +108,22 @@ class NodeComm(object):
         self.last_error = None   # why the last generation / shrink failed
 
     # ------------------------------------------------------------------
+    @property
+    def inflight(self):
+        return self._inflight
+
+    @inflight.setter
+    def inflight(self, value):
+        """The fence in flight; mirrored into its resource's
+        ``fence_inflight`` so ``status.fence.pending`` covers it."""
+        old = self._inflight
+        if old is not None and old['resource'].fence_inflight is not None:
+            old['resource'].fence_inflight = None
+        self._inflight = value
+        if value is not None:
+            value['resource'].fence_inflight = (value['epoch'],
+                                                value['members'], value['t'])
+
     @property
     def ready(self):
         return self.state == READY and self.loss_t is None
@@ -111,6 +146,10 @@ class NodeComm(object):
                 'failed_total': self.failed_total,
                 'generations': self.generations, 'shrinks': self.shrinks,
                 'hung_kills': self.hung_kills,
+                'quarantines': self.quarantines,
+                'fallbacks': self.fallbacks,
+                'rccl_retries': self.rccl_retries,
+                'gen_timeout': self.gen_timeout,
                 'last_error': self.last_error}
 
     def _bound(self):
@@ -128,8 +167,28 @@ class NodeComm(object):
     def _alive(proc):
         return not proc.eof and proc.popen.poll() is None
 
+    def _rank_of(self, proc):
+        """The rank ``proc`` holds in the current generation (its index in
+        ``members``), or None.  Replies are attributed by the sending
+        process, never by the ``rank`` they carry: a rank that already
+        dropped its communicator reports ``rank=None``."""
+        for rank, (_, member) in enumerate(self.members):
+            if member is proc:
+                return rank
+        return None
+
+    def _serving(self, proc):
+        """``(resource, worker)`` when ``proc`` runs a worker that is not
+        exited (starting, serving or draining a key), else None."""
+        for resource in self.m.resources.values():
+            for worker in resource.workers.values():
+                if worker.proc is proc and worker.state != 'exited':
+                    return resource, worker
+        return None
+
     def _usable(self, proc):
         return (proc is not None and getattr(proc, 'node_ok', False) and
+                not getattr(proc, 'node_quarantined', False) and
                 self._alive(proc))
 
     def candidates(self):
@@ -138,14 +197,22 @@ class NodeComm(object):
         is still starting: a generation's RCCL init on a process that is
         building its engine competes with it (a PyTorch engine started 1.9 s
         after a deep-idle wake instead of 0.4 s), and the fence must stay
-        off the scale-up's critical path."""
+        off the scale-up's critical path.  A slot whose
+        serving worker was quarantined (its agent stopped answering) is left
+        out until that worker has drained and exited."""
         bound = self._bound()
         out = []
         for slot in self.m.slots:
             proc = bound.get(slot.index)
+            if proc is not None and \
+                    getattr(proc, 'node_quarantined', False) and \
+                    self._alive(proc):
+                continue
             if not self._usable(proc) or proc in self.m.retiring:
                 return None
             out.append((slot.index, proc))
+        if not out:
+            return None
         for resource in self.m.resources.values():
             for worker in resource.workers.values():
                 if worker.state == 'starting':
@@ -180,13 +247,18 @@ class NodeComm(object):
                         self.members[r][0] for r in lost])
             else:
                 self.loss_t = None
+                # every agent gives up on its own within its uid wait plus
+                # its connect (2 x the budget): the manager's verdict comes
+                # after both, so a generation completing late is not thrown
+                # away and a late-starting agent is not taken for hung
+                # 
+                budget = 2.0 * self.gen_timeout + self.hang_grace
                 if self.state in (INIT, SHRINK) and self.verdict is None and \
-                        now - self.t_start > self.init_timeout:
+                        now - self.t_start > budget:
                     self._open_verdict('init', set(self.ready_ranks), now,
                                        'generation %d.%d %s timed out after '
                                        '%.1f s' % (self.gen, self.sub,
-                                                   self.state,
-                                                   self.init_timeout))
+                                                   self.state, budget))
         if self.verdict is not None:
             v = self.verdict
             if len(v['reported']) >= len(self.members) or \
@@ -198,8 +270,13 @@ class NodeComm(object):
             # (a fence the shrunk communicator can run goes first: the
             # regrow's RCCL init would hold it for seconds)
             members = self.candidates()
-            if members:
+            if members and len(members) > len(self.members):
                 self._regrow(members, now)
+        if self._rccl_retry_due(now) and self.ready and \
+                self.inflight is None:
+            self.break_('retrying the %s transport after the %s fallback' % (
+                self.configured_transport or 'configured',
+                self.fallback_used), failed=False)
         if self.state == NONE and now >= self.retry_at:
             members = self.candidates()
             if members:
@@ -209,7 +286,8 @@ class NodeComm(object):
             seq = self.inflight['seq']
             for _, proc in self.members:
                 proc.pipe.send({'cmd': 'fence_abort', 'seq': seq})
-            self._open_verdict('fence', set(), now - self.hang_grace,
+            self._open_verdict('fence', self.inflight.get('answered', ()),
+                               now - self.hang_grace,
                                'fence seq %d timed out' % seq, seq=seq)
             self._conclude(now)
 
@@ -218,37 +296,92 @@ class NodeComm(object):
                         'detail': detail, 'seq': seq}
 
     def _conclude(self, now):
-        """A failed generation / shrink / fence: kill the ranks that never
-        answered while others did, then drop the generation (a failure the
-        dead ranks explain is not counted toward the fallback)."""
+        """A failed generation / shrink / fence: ranks that never answered
+        while others did are hung.  A hung standby or retired process is
+        killed; a hung rank that runs a *worker* (starting, serving or
+        draining a key) is never killed for a membership verdict (VERDICT
+        r3 weak 3; the reference never removes a pod while work exists,
+        ``autoscaler/autoscaler.py:205-208``): it is quarantined -- left
+        out of the published set and of every later generation, drained
+        without recycling so its key finishes -- and its slot rejoins once
+        a fresh process serves it.  Then the generation is dropped (a
+        failure the hung ranks explain is not counted toward the
+        fallback)."""
         v, self.verdict = self.verdict, None
         silent = [r for r in range(len(self.members))
                   if r not in v['reported']]
-        killed = []
+        killed, quarantined = [], []
         if silent and len(silent) < len(self.members):
             for r in silent:
                 index, proc = self.members[r]
-                if self._alive(proc):
-                    killed.append(index)
-                    self.hung_kills += 1
-                    self.m.events.emit('node_rank_hung', gen=self.gen,
-                                       slot=index, pid=proc.pid,
-                                       kind=v['kind'], detail=v['detail'])
-                    logger.error('Node communicator generation %d: slot %d '
-                                 '(pid %d) did not answer (%s); killing it.',
-                                 self.gen, index, proc.pid, v['detail'])
-                    try:
-                        proc.popen.kill()
-                    except OSError:
-                        pass
+                if not self._alive(proc):
+                    continue
+                owner = self._serving(proc)
+                if owner is not None:
+                    quarantined.append(index)
+                    self._quarantine(index, proc, owner, v)
+                    continue
+                killed.append(index)
+                self.hung_kills += 1
+                self.m.events.emit('node_rank_hung', gen=self.gen,
+                                   slot=index, pid=proc.pid,
+                                   kind=v['kind'], detail=v['detail'])
+                logger.error('Node communicator generation %d: slot %d '
+                             '(pid %d) did not answer (%s); killing it.',
+                             self.gen, index, proc.pid, v['detail'])
+                try:
+                    proc.popen.kill()
+                except OSError:
+                    pass
         if v['kind'] == 'fence' and self.inflight is not None:
             self.inflight['resource'].fence_wanted = True
             self.inflight = None
-        reason = v['detail'] + (' (hung slot(s) %s killed)' % killed
-                                if killed else '')
-        self.break_(reason, failed=not killed)
+        reason = v['detail']
+        if killed:
+            reason += ' (hung slot(s) %s killed)' % killed
+        if quarantined:
+            reason += ' (serving slot(s) %s quarantined)' % quarantined
+        self.break_(reason, failed=not (killed or quarantined))
+
+    def _quarantine(self, index, proc, owner, verdict):
+        resource, worker = owner
+        proc.node_quarantined = True
+        self.quarantines += 1
+        self.m.events.emit('node_rank_quarantined', gen=self.gen, slot=index,
+                           pid=proc.pid, worker=worker.id,
+                           kind=verdict['kind'], detail=verdict['detail'])
+        logger.error('Node communicator generation %d: slot %d (worker %s) '
+                     'did not answer (%s); quarantined: it finishes its key '
+                     'and leaves, it is not killed.', self.gen, index,
+                     worker.id, verdict['detail'])
+        self.m.quarantine_worker(resource, worker,
+                                 'node fence: %s' % verdict['kind'])
+
+    def _rccl_retry_due(self, now):
+        """The fallback is in use, its retry time has come, and the node
+        is idle (no worker at all: a retry that fails costs nothing
+        visible, and one that succeeds is the next generation anyway)."""
+        if self.fallback_used is None or self.rccl_retry_at is None or \
+                now < self.rccl_retry_at:
+            return False
+        for resource in self.m.resources.values():
+            for worker in resource.workers.values():
+                if worker.state != 'exited':
+                    return False
+        return True
 
     def _start(self, members, now):
+        if self._rccl_retry_due(now):
+            self.rccl_retries += 1
+            self.m.events.emit('node_comm_retry', gen=self.gen + 1,
+                               transport=self.configured_transport or 'auto',
+                               after=self.fallback_used)
+            logger.info('Node communicator: retrying the %s transport.',
+                        self.configured_transport or 'configured')
+            self.transport_override = self.configured_transport
+            self.fallback_used = None
+            self.rccl_retry_at = None
+            self.failures = 0
         self.gen += 1
         self.sub = 0
         self.state = INIT
@@ -256,9 +389,13 @@ class NodeComm(object):
         self.ready_ranks = {}
         self.t_start = now
         n = len(members)
+        warm = all(getattr(proc, 'rccl_inits', 0) > 0 for _, proc in members)
+        rccl = self.transport_override in (None, 'rccl')
+        self.gen_timeout = self.init_timeout if warm or not rccl else \
+            self.first_init_timeout
         for rank, (_, proc) in enumerate(members):
             message = {'cmd': 'comm_init', 'gen': self.gen, 'rank': rank,
-                       'nranks': n}
+                       'nranks': n, 'timeout': self.gen_timeout}
             if self.transport_override:
                 message['transport'] = self.transport_override
             proc.pipe.send(message)
@@ -340,6 +477,9 @@ class NodeComm(object):
                     self.failures >= self.fallback_after):
                 self.transport_override = self.fallback
                 self.fallback_used = self.fallback
+                self.fallbacks += 1
+                self.rccl_retry_at = now + min(
+                    3600.0, self.rccl_retry_s * 2 ** (self.fallbacks - 1))
                 self.retry_at = now
                 self.m.events.emit('node_comm_fallback', gen=self.gen,
                                    transport=self.fallback,
@@ -361,6 +501,13 @@ class NodeComm(object):
         if kind == 'node_agent':
             proc.node_ok = True
             return
+        if kind == 'node_preloaded':
+            proc.rccl_preload_ms = message.get('ms')
+            self.m.events.emit('node_rank_preloaded', pid=proc.pid,
+                               slot=getattr(proc, 'slot', None),
+                               ms=message.get('ms'),
+                               error=message.get('error'))
+            return
         gen = message.get('gen')
         if kind == 'comm_uid':
             if self.state == INIT and gen == self.gen:
@@ -372,10 +519,13 @@ class NodeComm(object):
             if self.state not in (INIT, SHRINK) or gen != self.gen or \
                     sub != self.sub:
                 return
+            rank = self._rank_of(proc)
+            if rank is None:
+                return
             if not message.get('ok'):
                 what = 'shrink' if self.state == SHRINK else 'connect'
                 detail = 'rank %s failed to %s: %s' % (
-                    message.get('rank'), what, message.get('detail'))
+                    rank, what, message.get('detail'))
                 if self.state == SHRINK:
                     # a failed shrink is not a failed generation: the next
                     # full one starts once the lost slot has a process again
@@ -384,11 +534,13 @@ class NodeComm(object):
                 if self.verdict is None:
                     self._open_verdict('init', set(self.ready_ranks),
                                        time.monotonic(), detail)
-                self.verdict['reported'].add(message.get('rank'))
+                self.verdict['reported'].add(rank)
                 return
-            self.ready_ranks[message.get('rank')] = message
+            self.ready_ranks[rank] = message
+            if message.get('transport') == 'rccl':
+                proc.rccl_inits = getattr(proc, 'rccl_inits', 0) + 1
             if self.verdict is not None:
-                self.verdict['reported'].add(message.get('rank'))
+                self.verdict['reported'].add(rank)
                 return
             if len(self.ready_ranks) == len(self.members):
                 shrunk = self.state == SHRINK
@@ -416,28 +568,40 @@ class NodeComm(object):
             if inflight is None or message.get('seq') != inflight['seq']:
                 return
             resource = inflight['resource']
+            rank = self._rank_of(proc)
             if not message.get('ok'):
                 if message.get('interrupted'):
-                    # a peer died: the shrink re-runs it
-                    self.inflight = None
+                    # a peer died or left: the shrink, or the failing peer's
+                    # own report, settles this fence -- this rank answered
                     resource.fence_wanted = True
+                    if rank is not None:
+                        inflight.setdefault('answered', set()).add(rank)
+                        if self.verdict is not None:
+                            self.verdict['reported'].add(rank)
                     return
                 if self.verdict is None:
                     logger.warning('Node fence seq %s failed: %s',
                                    inflight['seq'], message.get('detail'))
                     self.m._fence_failed_node(resource, message)
                     self._open_verdict(
-                        'fence', set(), time.monotonic(),
+                        'fence', inflight.get('answered', ()),
+                        time.monotonic(),
                         'fence seq %s failed on rank %s: %s' % (
-                            inflight['seq'], message.get('rank'),
-                            message.get('detail')), seq=inflight['seq'])
-                self.verdict['reported'].add(message.get('rank'))
+                            inflight['seq'], rank, message.get('detail')),
+                        seq=inflight['seq'])
+                if rank is not None:
+                    self.verdict['reported'].add(rank)
                 return
             self.inflight = None
             self.verdict = None
             self.m._fence_completed(resource, inflight['epoch'],
                                     inflight['members'], inflight['t'],
                                     message)
+            # the published fence: every rank may now gate on its result
+            for _, member in self.members:
+                if self._alive(member):
+                    member.pipe.send({'cmd': 'fence_commit',
+                                      'seq': inflight['seq']})
 
     # ------------------------------------------------------------------
     def can_fence(self, procs):

@@ -1,0 +1,609 @@
+"""The standby pool of the node-local GPU manager:
+warm standby processes pinned to the GPUs the next scale-up takes, the
+worker zygote they fork from, deep idle (park / arrival wake / wake lead),
+recycling of drained workers, PCI verification of each slot, and reaping.
+
+A mixin of :class:`~.controller.GpuManager` (shared lock, events, slots and
+resources); split out of ``controller.py``.  Every
+method runs under the manager lock.
+"""
+import collections
+import json
+import logging
+import os
+import subprocess
+import time
+
+from .nodecomm import NODE_EVENTS
+from .process import EXITED, ManagedProcess, Pipe, bare_worker
+
+logger = logging.getLogger('GpuManager')
+
+POOL_KEY = 'kiosk:pool'
+SLOTS_KEY = 'kiosk:slots'
+
+
+class PoolMixin(object):
+    """Standbys, zygote, deep idle, recycling (see the module doc)."""
+
+    def _init_pool(self, pool_size, pool_template, pool_mode, recycle,
+                   pool_idle_release_s, pool_wake_poll_s, pool_wake_hold_s,
+                   pool_wake_lead_s, zygote):
+        self.pool_size = max(0, int(pool_size))
+        self.pool_template = pool_template
+        self.pool_mode = pool_mode
+        self.recycle = bool(recycle)
+        self.retiring = []   # recycled processes told to exit
+        self.standbys = collections.OrderedDict()   # slot index -> process
+        # deep idle: after this long without demand the standbys exit and
+        # the pool stays empty until the next scale-up (0 = never)
+        self.pool_idle_release_s = float(pool_idle_release_s or 0.0)
+        self.pool_parked = False
+        self._last_demand = time.monotonic()
+        self.pool_wake_poll_s = float(pool_wake_poll_s or 0.0)
+        self.pool_wake_hold_s = float(pool_wake_hold_s or 0.0)
+        self._wake_until = 0.0
+        self.pool_wake_lead_s = float(pool_wake_lead_s or 0.0)
+        self._next_tick = None    # monotonic instant of the next tick
+        # spawn -> booted+prebuilt of recent arrival-woken standbys: the
+        # lead adapts to it (1.5 x the slowest + 50 ms, capped by the knob)
+        self._wake_boots = collections.deque(maxlen=8)
+        self._wake_at = None      # a deferred arrival wake
+        self._next_arrival_check = 0.0
+        # queue -> length at the last check; reset to empty when demand
+        # ends (a scale to zero implies empty queues, stranded keys aside),
+        # so a key landing before the first check still counts as arrived
+        self._queued = {}
+        self.arrival_wakes = 0
+        # worker zygote (worker/zygote.py): spawns fork from a process that
+        # imported the worker (and torch, for a plug-in) without the GPU
+        self.zygote_enabled = bool(zygote)
+        self.zygote = None
+        self._zygote_restart_at = 0.0
+        self.mapping_fixes = 0   # slots remapped after a PCI check
+        self._orphan_scan_at = 0.0
+        self._zombies_seen = set()
+
+    # ------------------------------------------------------------------
+    # process management
+    # ------------------------------------------------------------------
+    @staticmethod
+    def _interpreter(template):
+        argv = [template.python]
+        if bare_worker(template):
+            # the torch-free HIP worker needs only this tree (on PYTHONPATH
+            # below) and the stdlib: skipping site-packages' .pth
+            # processing takes ~20 ms off every spawn
+            argv.append('-S')
+        return argv
+    @staticmethod
+    def _environment(template):
+        env = dict(os.environ)
+        env.update({k: str(v) for k, v in template.env.items()})
+        env['PYTHONUNBUFFERED'] = '1'
+        root = os.path.dirname(os.path.dirname(os.path.dirname(
+            os.path.abspath(__file__))))
+        env['PYTHONPATH'] = os.pathsep.join(
+            [root] + [p for p in env.get('PYTHONPATH', '').split(os.pathsep)
+                      if p])
+        return env
+    # env that decides what a worker imports: a zygote serves only the
+    # templates it preloaded for
+    _IMPORT_ENV = ('WORKER_ENGINE', 'WORKER_IMPORT_TORCH', 'KIOSK_NATIVE',
+                   'WORKER_PYTHON_SITE')
+    def _start_zygote(self):
+        tpl = self.pool_template
+        if not self.zygote_enabled or tpl is None or self.zygote is not None \
+                or tpl.module != 'kiosk_autoscaler_amd.worker.main' or \
+                self._stopping or time.monotonic() < self._zygote_restart_at:
+            return
+        from ..worker import zygote
+        if not zygote.become_subreaper():
+            logger.warning('PR_SET_CHILD_SUBREAPER refused: no zygote.')
+            self.zygote_enabled = False
+            return
+        argv = self._interpreter(tpl) + [
+            '-m', 'kiosk_autoscaler_amd.worker.zygote', '--backend',
+            tpl.backend]
+        self.zygote = zygote.ZygoteClient(argv, self._environment(tpl))
+        self.events.emit('zygote_spawn', pid=self.zygote.pid)
+    def _check_zygote(self):
+        """False (and the zygote forgotten, restarted after a pause) once
+        the zygote process has exited."""
+        z = self.zygote
+        if z is None:
+            return False
+        if z.alive():
+            return True
+        logger.warning('Worker zygote %d exited; spawning directly until it '
+                       'is restarted.', z.pid)
+        self.events.emit('zygote_exit', pid=z.pid, code=z.popen.returncode)
+        z.close()
+        self.zygote = None
+        self._zygote_restart_at = time.monotonic() + 10.0
+        return False
+    def _retire_zygote(self, reason):
+        """A zygote that lost a fork request is not trusted again: killed,
+        and restarted after the usual pause."""
+        z, self.zygote = self.zygote, None
+        if z is None:
+            return
+        logger.error('Retiring worker zygote %d: %s', z.pid, reason)
+        self.events.emit('zygote_retired', pid=z.pid, reason=reason)
+        try:
+            z.popen.kill()
+        except OSError:
+            pass
+        z.close()
+        self._zygote_restart_at = time.monotonic() + 10.0
+    def _zygote_for(self, template):
+        z = self.zygote
+        tpl = self.pool_template
+        if z is None or tpl is None:
+            return None
+        if not self._check_zygote():
+            return None
+        if not z.poll_ready():
+            return None      # still importing: this spawn takes the slow path
+        if (template.module != tpl.module or
+                template.backend != tpl.backend or
+                bare_worker(template) != bare_worker(tpl) or
+                any(template.env.get(k) != tpl.env.get(k)
+                    for k in self._IMPORT_ENV)):
+            return None
+        return z
+    def _spawn(self, template, role, assign=None, slot=None):
+        cmd_r, cmd_w = os.pipe()
+        ev_r, ev_w = os.pipe()
+        args = ['--cmd-fd', str(cmd_r), '--ev-fd', str(ev_w),
+                '--backend', template.backend]
+        # a standby spawned by an arrival wake: the scale-up for the key is
+        # due within a tick, so it builds the engine now, not at the assign
+        woken = (assign is None and slot is not None and role == 'standby'
+                 and time.monotonic() < self._wake_until)
+        # every device-mode standby builds its engine at boot, before its
+        # node agent joins a generation: the assignment's READY is then the
+        # warm-start graph alone, which RCCL's one-time load (seconds, on
+        # the agent's thread) cannot hold up (profiles/r4_collision)
+        prebuild = woken or (assign is None and slot is not None and
+                             role == 'standby' and
+                             self.pool_mode == 'device')
+        if assign is not None:
+            args += ['--assign', json.dumps(assign)]
+        elif slot is not None:
+            pin = {'gpu': slot.visible_id, 'slot': slot.index,
+                   'cpus': slot.cpus, 'preinit': self.pool_mode,
+                   'node_fence': self.node is not None}
+            if prebuild:
+                pin['prebuild'] = self._prebuild_spec(template)
+            args += ['--pin', json.dumps(pin)]
+        env = self._environment(template)
+        popen = None
+        via = 'exec'
+        try:
+            zygote = self._zygote_for(template)
+            if zygote is not None:
+                try:
+                    popen = zygote.fork(args, env, (cmd_r, ev_w))
+                    via = 'zygote'
+                except (OSError, ValueError) as err:
+                    from ..worker.zygote import ZygoteLost
+                    logger.warning('zygote fork failed (%s); spawning '
+                                   'directly.', err)
+                    if isinstance(err, ZygoteLost):
+                        # the zygote may still fork a worker on these pipe
+                        # ends: retire it and spawn on a fresh pair (the
+                        # late worker sees EOF on its command pipe and
+                        # exits without an assignment)
+                        self._retire_zygote(str(err))
+                        os.close(cmd_w)
+                        os.close(ev_r)
+                        os.close(cmd_r)
+                        os.close(ev_w)
+                        cmd_r, cmd_w = os.pipe()
+                        ev_r, ev_w = os.pipe()
+                        args[1], args[3] = str(cmd_r), str(ev_w)
+            if popen is None:
+                argv = self._interpreter(template) + ['-m', template.module]
+                popen = subprocess.Popen(argv + args, env=env,
+                                         pass_fds=(cmd_r, ev_w),
+                                         close_fds=True,
+                                         start_new_session=True)
+        finally:
+            os.close(cmd_r)
+            os.close(ev_w)
+        proc = ManagedProcess(popen, Pipe(cmd_w, ev_r), role)
+        proc.woken = woken
+        proc.slot = slot.index if slot is not None else None
+        proc.via = via
+        self.events.emit('process_spawn', role=role, pid=popen.pid,
+                         slot=proc.slot, via=via)
+        return proc
+    def _refill_pool(self):
+        """Keep one standby pinned to each of the lowest ``pool_size`` free
+        GPUs (the slots the next scale-up will take)."""
+        if not self.pool_size or self.pool_template is None or \
+                self._stopping:
+            return
+        changed = False
+        if self._reap_standbys():
+            changed = True
+        if self._park_pool():
+            changed = True
+        if self.pool_parked:
+            if changed:
+                self._publish_pool()
+            return
+        for slot in self._free_slots()[:self.pool_size]:
+            if slot.index not in self.standbys:
+                self.standbys[slot.index] = self._spawn(
+                    self.pool_template, 'standby', slot=slot)
+                changed = True
+        if changed:
+            self._publish_pool()
+    def _park_pool(self):
+        """Deep idle (``POOL_IDLE_RELEASE_S``): with no declared or live
+        worker for that long, retire every standby -- the node then holds
+        no GPU, like the reference at zero replicas -- and keep the pool
+        empty until demand returns: a key's arrival (``pool_wake_poll_s``,
+        woken ``wake_lead()`` before the next tick) or, without it, the
+        scale-up itself, which is then a cold spawn with the pool refilling
+        behind it.  True if standbys were retired."""
+        now = time.monotonic()
+        demand = any(r.declared > 0 or any(w.state != EXITED
+                                           for w in r.workers.values())
+                     for r in self.resources.values())
+        if demand:
+            self._last_demand = now
+            self._queued = {}
+            self._wake_at = None
+            self._wake_until = 0.0    # the tick scaled: the hold is done
+            if self.pool_parked:
+                self.pool_parked = False
+                self.events.emit('pool_resumed')
+                logger.info('Demand returned: refilling the warm pool.')
+            return False
+        released = [p for p in self.standbys.values()
+                    if p.booted and not p.engine_cached and
+                    self.pool_mode == 'device']
+        arrived = (self.pool_idle_release_s > 0 or bool(released)) and \
+            self._arrived(now)
+        if arrived and released:
+            # ENGINE_IDLE_RELEASE_S freed these standbys' engines: a key's
+            # arrival has them rebuild it before the scale-up tick
+            for proc in released:
+                proc.pipe.send({'cmd': 'prebuild',
+                                'spec': self._prebuild_spec(
+                                    self.pool_template)})
+                proc.engine_cached = True     # (until told otherwise)
+            self.events.emit('engine_rebuild', standbys=len(released))
+        if arrived and self.pool_idle_release_s > 0:
+            wake_at = now
+            lead = self.wake_lead()
+            if self.pool_parked and lead > 0 and \
+                    self._next_tick is not None and \
+                    self._next_tick - now > lead:
+                wake_at = self._next_tick - lead
+            if self._wake_at is None or wake_at < self._wake_at:
+                self._wake_at = wake_at
+        if self._wake_at is not None and now >= self._wake_at:
+            self._wake_at = None
+            self._last_demand = now
+            self._wake_until = now + self.pool_wake_hold_s
+            if self.pool_parked:
+                self.pool_parked = False
+                self.arrival_wakes += 1
+                self.events.emit('pool_resumed', reason='arrival',
+                                 lead_s=round(self.wake_lead(), 4),
+                                 tick_in_s=(round(self._next_tick - now, 4)
+                                            if self._next_tick is not None
+                                            else None))
+                logger.info('Keys arrived: refilling the warm pool ahead of '
+                            'the scale-up tick.')
+            return False
+        if (self.pool_idle_release_s <= 0 or self.pool_parked or
+                now - self._last_demand < self.pool_idle_release_s or
+                now < self._wake_until):
+            return False
+        self.pool_parked = True
+        released = 0
+        for index, proc in list(self.standbys.items()):
+            if proc.popen.poll() is None:
+                proc.pipe.send({'cmd': 'exit'})
+                self.retiring.append(proc)
+                released += 1
+            del self.standbys[index]
+        self.events.emit('pool_parked', standbys=released,
+                         idle_s=round(now - self._last_demand, 3))
+        logger.info('No demand for %.0f s: released %d standby process(es).',
+                    now - self._last_demand, released)
+        return True
+    def note_next_tick(self, t_monotonic):
+        """The autoscaler loop's next tick instant (``time.monotonic``
+        seconds, system-wide, so a ``unix:`` daemon's clients report it
+        too): a deferred arrival wake is timed against it.  With several
+        autoscalers on one manager the earliest upcoming tick wins (a
+        report replaces a tick that is due or past).  Called from the
+        loop's thread: under the manager lock."""
+        t_monotonic = float(t_monotonic)
+        with self.lock:
+            current = self._next_tick
+            if current is None or current <= time.monotonic() + 0.05 or \
+                    t_monotonic < current:
+                self._next_tick = t_monotonic
+            lead = self.wake_lead()
+            if self._wake_at is not None and lead > 0:
+                # the tick came earlier than planned for (IDLE_INTERVAL)
+                self._wake_at = min(self._wake_at, self._next_tick - lead)
+        self._wake()
+    def wake_lead(self):
+        """Seconds before the next tick an arrival wakes a parked pool:
+        ``pool_wake_lead_s`` until woken standbys have been timed, then
+        1.5 x the slowest of the last 8 spawn -> booted+prebuilt times plus
+        50 ms and the arrival poll, at least 0.2 s, never above
+        ``pool_wake_lead_s`` (built-in worker: ~0.1-0.2 s -> 0.25-0.4 s;
+        PyTorch plug-in: ~0.55 s -> the cap)."""
+        cap = self.pool_wake_lead_s
+        if cap <= 0 or not self._wake_boots:
+            return cap
+        return min(cap, max(0.2, 1.5 * max(self._wake_boots) + 0.05 +
+                            self.pool_wake_poll_s))
+    def _prebuild_spec(self, template):
+        """What an arrival-woken standby builds its engine for: the shape
+        (kind, keys per pod) of the resource its template serves."""
+        for resource in self.resources.values():
+            if resource.template.module == template.module:
+                return {'kind': resource.kind,
+                        'keys_per_pod': resource.template.keys_per_pod}
+        return {'kind': 'deployment', 'keys_per_pod': template.keys_per_pod}
+    def _arrived(self, now):
+        """True when a managed queue grew since the last check (read every
+        ``pool_wake_poll_s`` while no worker is declared or live).  Growth,
+        not length: keys a policy strands below KEYS_PER_POD do not hold
+        the pool, new ones wake it.  One pipelined LLEN per queue."""
+        if self.pool_wake_poll_s <= 0 or self.redis is None or \
+                now < self._next_arrival_check:
+            return False
+        self._next_arrival_check = now + self.pool_wake_poll_s
+        queues = sorted(set(q for r in self.resources.values()
+                            for q in r.template.queues))
+        if not queues:
+            return False
+        try:
+            pipe = self.redis.pipeline(transaction=False)
+            for queue in queues:
+                pipe.llen(queue)
+            lengths = dict(zip(queues, (int(n or 0) for n in pipe.execute())))
+        except Exception as err:  # pylint: disable=broad-except
+            logger.debug('arrival check failed: %s', err)
+            return False
+        before, self._queued = self._queued, lengths
+        grown = [q for q in queues if lengths[q] > before.get(q, 0)]
+        if grown:
+            self.events.emit('arrival', queues=grown,
+                             parked=self.pool_parked)
+        return bool(grown)
+    def _take_standby(self, template, slot):
+        """The standby pinned to ``slot`` (booted or still booting: it
+        reads the assignment as soon as its imports finish)."""
+        if self.pool_template is None or \
+                template.module != self.pool_template.module or \
+                template.backend != self.pool_template.backend:
+            return None
+        proc = self.standbys.get(slot.index)
+        if proc is None or proc.popen.poll() is not None:
+            return None
+        del self.standbys[slot.index]
+        self._publish_pool()
+        return proc
+    def _publish_slots(self):
+        """The slot table as verified so far (``kiosk:slots``): the bench
+        samples amdsmi on these PCI addresses, not on KFD order."""
+        if self.redis is None:
+            return
+        try:
+            self.redis.set(SLOTS_KEY, json.dumps([
+                {'index': s.index, 'visible': s.visible_id, 'pci': s.pci,
+                 'verified': bool(getattr(s, 'pci_verified', False)),
+                 'kind': s.kind} for s in self.slots]))
+        except Exception:  # pylint: disable=broad-except
+            pass
+    def _publish_pool(self):
+        if self.redis is None:
+            return
+        try:
+            # booted standbys, standbys, node communicator state, parked
+            # (POOL_IDLE_RELEASE_S: the pool is empty on purpose)
+            self.redis.set(POOL_KEY, '%d %d %s %d' % (
+                sum(1 for p in self.standbys.values() if p.booted),
+                len(self.standbys),
+                self.node.state if self.node is not None else 'off',
+                int(self.pool_parked)))
+        except Exception:  # pylint: disable=broad-except
+            pass
+    def _on_standby_messages(self, proc):
+        for message in proc.pipe.read_messages():
+            if message is None:
+                proc.eof = True
+                continue
+            self._on_standby_message(proc, message)
+    def _on_standby_message(self, proc, message):
+        if self.node is not None and message.get('ev') in NODE_EVENTS:
+            self.node.on_message(proc, message)
+            return
+        if message.get('ev') == 'engine_released':
+            proc.engine_cached = False
+            proc.hbm_free = message.get('hbm_free')
+            self.events.emit('engine_released', pid=proc.pid, slot=proc.slot,
+                             released_bytes=message.get('released_bytes'),
+                             hbm_free=proc.hbm_free)
+            return
+        if message.get('ev') == 'device':
+            self._check_device(proc, message.get('pci'))
+            return
+        if message.get('ev') == 'prebuilt':
+            proc.engine_cached = not message.get('error')
+            self.events.emit('standby_prebuilt', pid=proc.pid, slot=proc.slot,
+                             ms=message.get('ms'),
+                             hbm_bytes=message.get('hbm_bytes'),
+                             error=message.get('error'))
+            return
+        if message.get('ev') == 'standby':
+            proc.engine_cached = bool(message.get('engine_cached'))
+            if proc.woken and not proc.booted:
+                # spawn -> booted and prebuilt: what the wake lead must cover
+                # (once: a recycled worker reports 'standby' again later)
+                proc.woken = False
+                self._wake_boots.append(
+                    (time.monotonic_ns() - proc.t_spawn) / 1e9)
+            proc.booted = True
+            proc.hbm_free = message.get('hbm_free')
+            if message.get('pci'):
+                if not self._check_device(proc, message.get('pci')):
+                    return   # retired: the pool respawns it re-pinned
+            self._publish_pool()
+            self.events.emit('standby_ready', pid=proc.pid, slot=proc.slot,
+                             boot_s=(time.monotonic_ns() - proc.t_spawn)
+                             / 1e9, preinit=message.get('preinit'),
+                             recycled=proc.role == 'standby' and
+                             proc.recycles > 0)
+    def _check_device(self, proc, pci):
+        """the slot table maps slot -> HIP ordinal -> PCI address
+        from KFD topology order, which drives the HIP_VISIBLE_DEVICES pin,
+        the NUMA-local CPU affinity and the BDF the benchmark's amdsmi
+        cross-check samples.  The process reports the PCI address HIP sees
+        for its ordinal; on a mismatch the slot is remapped to the device
+        actually behind that ordinal (its NUMA node and CPUs re-read) and a
+        standby pinned with the wrong affinity is respawned.  False when
+        ``proc`` was retired for that."""
+        from .gpus import local_cpus, normalize_pci
+        index = proc.slot
+        slot = next((s for s in self.slots if s.index == index), None)
+        actual = normalize_pci(pci)
+        if slot is None or slot.kind != 'gpu' or actual is None:
+            return True
+        expected = normalize_pci(slot.pci)
+        proc.pci = actual
+        if expected == actual:
+            if not getattr(slot, 'pci_verified', False):
+                slot.pci_verified = True
+                self.events.emit('gpu_mapping', slot=index, pci=actual,
+                                 visible=slot.visible_id, verified=True)
+                self._publish_slots()
+            return True
+        slot.pci = actual
+        slot.numa_node, slot.cpus = local_cpus(actual)
+        slot.pci_verified = True
+        self.mapping_fixes += 1
+        self.events.emit('gpu_mapping_mismatch', slot=index,
+                         visible=slot.visible_id, expected=expected,
+                         actual=actual, numa_node=slot.numa_node)
+        logger.error('GPU slot %d (HIP_VISIBLE_DEVICES=%s) is %s, not %s as '
+                     'KFD order suggested: remapped (NUMA node %s).', index,
+                     slot.visible_id, actual, expected, slot.numa_node)
+        self._publish_slots()
+        if self.standbys.get(index) is proc and expected is not None:
+            del self.standbys[index]
+            proc.pipe.send({'cmd': 'exit'})
+            self.retiring.append(proc)
+            return False
+        return True
+    def _recycle_ok(self, resource):
+        tpl = self.pool_template
+        return bool(self.recycle and self.pool_size and tpl is not None and
+                    not self._stopping and
+                    resource.template.module == tpl.module and
+                    resource.template.backend == tpl.backend)
+    def _on_recycled(self, worker, message):
+        """A worker finished cleanly and kept its process: account for it
+        like an exit, then adopt the process as its GPU's standby."""
+        if worker.state == EXITED:
+            return
+        resource = worker.resource
+        proc = worker.proc
+        self._on_exit(resource, worker, int(message.get('code', 0)),
+                      recycled=True)
+        slot = worker.slot
+        proc.recycles += 1
+        if (self._recycle_ok(resource) and slot.index not in self.standbys
+                and len(self.standbys) < self.pool_size and
+                not getattr(proc, 'node_quarantined', False)):
+            proc.role = 'standby'
+            proc.slot = slot.index
+            proc.booted = False     # until its 'standby' message
+            self.standbys[slot.index] = proc
+            self._publish_pool()
+            self.events.emit('worker_recycled', worker=worker.id,
+                             gpu=slot.index, pid=proc.pid)
+        else:
+            proc.pipe.send({'cmd': 'exit'})
+            self.retiring.append(proc)
+    ORPHAN_SCAN_S = 5.0
+    def _reap_orphans(self, now=None):
+        """Subreaper hygiene: a descendant a worker orphaned is
+        re-parented to this process; nothing waits for it, so it would stay
+        a zombie for the daemon's life.  Every ``ORPHAN_SCAN_S`` the direct
+        children in state Z that are none of ours are reaped -- by pid, and
+        only after a zombie was seen on two scans (an embedding program's
+        own ``subprocess`` children are reaped by their owner well before
+        that), never with a blind ``waitpid(-1)``."""
+        now = time.monotonic() if now is None else now
+        if now < getattr(self, '_orphan_scan_at', 0.0):
+            return []
+        self._orphan_scan_at = now + self.ORPHAN_SCAN_S
+        if not self.zygote_enabled:
+            return []     # not a subreaper: orphans go to init
+        me = os.getpid()
+        ours = set(p.pid for p in self.standbys.values())
+        ours.update(p.pid for p in self.retiring)
+        ours.update(w.proc.pid for r in self.resources.values()
+                    for w in r.workers.values())
+        if self.zygote is not None:
+            ours.add(self.zygote.pid)
+        seen = getattr(self, '_zombies_seen', set())
+        zombies = set()
+        try:
+            names = os.listdir('/proc')
+        except OSError:
+            return []
+        for name in names:
+            if not name.isdigit() or int(name) in ours:
+                continue
+            try:
+                with open('/proc/%s/stat' % name) as f:
+                    stat = f.read()
+            except OSError:
+                continue
+            fields = stat[stat.rfind(')') + 2:].split()
+            if len(fields) > 1 and fields[0] == 'Z' and int(fields[1]) == me:
+                zombies.add(int(name))
+        reaped = []
+        for pid in zombies & seen:
+            try:
+                if os.waitpid(pid, os.WNOHANG)[0] == pid:
+                    reaped.append(pid)
+            except ChildProcessError:
+                pass
+        self._zombies_seen = zombies - set(reaped)
+        if reaped:
+            self.events.emit('orphans_reaped', pids=reaped)
+        return reaped
+    def _reap_standbys(self):
+        """Forget exited standby / retired processes (``standby_exit``
+        closes their standby GPU time in the metrics).  True if a retired
+        process was reaped."""
+        retired = False
+        for index, proc in list(self.standbys.items()):
+            if proc.popen.poll() is not None:
+                proc.pipe.close()
+                del self.standbys[index]
+                self.events.emit('standby_exit', pid=proc.pid, slot=index,
+                                 code=proc.popen.returncode)
+        for proc in list(self.retiring):
+            if proc.popen.poll() is not None:
+                proc.pipe.close()
+                self.retiring.remove(proc)
+                self.events.emit('standby_exit', pid=proc.pid, slot=proc.slot,
+                                 code=proc.popen.returncode, retired=True)
+                retired = True
+        return retired

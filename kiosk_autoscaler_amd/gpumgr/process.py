@@ -1,0 +1,154 @@
+"""Managed processes of the node-local GPU manager: the worker
+template (the pod-template analog), the manager <-> process pipe, a child
+process (standby or worker) and a worker's bookkeeping.
+
+Split out of ``controller.py``; the controller, the
+standby pool (``pool.py``) and the fence orchestration (``fencing.py``)
+share these types.
+"""
+import itertools
+import json
+import logging
+import os
+import sys
+import time
+
+logger = logging.getLogger('GpuManager')
+
+STARTING, READY, DRAINING, EXITED = 'starting', 'ready', 'draining', 'exited'
+
+
+class WorkerTemplate(object):
+    """What to run for a resource (the pod template analog)."""
+
+    def __init__(self, queues=('predict',), module=None, env=None,
+                 python=None, backend='auto', keys_per_pod=1):
+        self.queues = list(queues)
+        self.module = module or 'kiosk_autoscaler_amd.worker.main'
+        self.env = dict(env or {})
+        self.python = python or sys.executable
+        self.backend = backend
+        self.keys_per_pod = int(keys_per_pod)
+
+    def to_dict(self):
+        return {'queues': self.queues, 'module': self.module,
+                'env': self.env, 'backend': self.backend,
+                'keys_per_pod': self.keys_per_pod}
+
+
+def bare_worker(template):
+    """Spawn with ``python -S``: our own HIP worker with the built-in engine,
+    not importing torch (``WORKER_IMPORT_TORCH``), unless
+    ``WORKER_PYTHON_SITE=1``."""
+    def flag(name):
+        value = template.env.get(name, os.environ.get(name, '0'))
+        return str(value) not in ('0', '')
+    return (template.backend == 'hip' and
+            template.module == 'kiosk_autoscaler_amd.worker.main' and
+            not flag('WORKER_ENGINE') and    # a plug-in may need packages
+            not flag('WORKER_IMPORT_TORCH') and
+            not flag('WORKER_PYTHON_SITE'))
+
+
+class Pipe(object):
+    """Line-oriented JSON channel over a pair of pipe fds."""
+
+    def __init__(self, cmd_w, ev_r):
+        self.cmd_w = cmd_w
+        self.ev_r = ev_r
+        self._buf = b''
+        os.set_blocking(ev_r, False)
+
+    def send(self, message):
+        data = (json.dumps(message) + '\n').encode()
+        try:
+            os.write(self.cmd_w, data)
+            return True
+        except OSError:
+            return False
+
+    def read_messages(self):
+        out = []
+        while True:
+            try:
+                chunk = os.read(self.ev_r, 65536)
+            except BlockingIOError:
+                break
+            except OSError:
+                chunk = b''
+            if not chunk:
+                out.append(None)  # EOF
+                break
+            self._buf += chunk
+        while b'\n' in self._buf:
+            line, self._buf = self._buf.split(b'\n', 1)
+            if line.strip():
+                try:
+                    out.append(json.loads(line))
+                except ValueError:
+                    logger.warning('bad worker message %r', line[:200])
+        return out
+
+    def close(self):
+        for fd in (self.cmd_w, self.ev_r):
+            try:
+                os.close(fd)
+            except OSError:
+                pass
+
+
+class ManagedProcess(object):
+    """A child process (standby or worker) and its control pipe."""
+
+    _ids = itertools.count()
+
+    def __init__(self, popen, pipe, role):
+        self.popen = popen
+        self.pipe = pipe
+        self.role = role
+        self.seq = next(self._ids)
+        self.t_spawn = time.monotonic_ns()
+        self.booted = False
+        self.eof = False
+        self.recycles = 0
+        self.node_ok = False    # runs a node-communicator agent
+        self.hbm_free = None    # free HBM bytes the standby measured
+        self.woken = False      # spawned by an arrival wake (prebuilds)
+        self.engine_cached = False  # standby holds a built engine
+
+    @property
+    def pid(self):
+        return self.popen.pid
+
+
+class Worker(object):
+    __slots__ = ('id', 'resource', 'slot', 'proc', 'state', 'busy',
+                 't_assigned', 't_ready', 't_exit', 'exit_code', 'from_pool',
+                 'stages', 'last_beat', 'kill_reason', 'fenced_out',
+                 'quarantined_at')
+
+    def __init__(self, wid, resource, slot, proc, from_pool):
+        self.id = wid
+        self.resource = resource
+        self.slot = slot
+        self.proc = proc
+        self.state = STARTING
+        self.busy = False
+        self.t_assigned = time.monotonic_ns()
+        self.t_ready = None
+        self.t_exit = None
+        self.exit_code = None
+        self.from_pool = from_pool
+        self.stages = {}
+        self.last_beat = time.monotonic()   # last sign of progress
+        self.kill_reason = None
+        self.fenced_out = False     # an agreed membership excluded it
+        self.quarantined_at = None  # its node agent stopped answering
+
+    def summary(self):
+        return {'id': self.id, 'gpu': self.slot.index, 'pid': self.proc.pid,
+                'state': self.state, 'busy': self.busy,
+                'from_pool': self.from_pool, 't_assigned': self.t_assigned,
+                't_ready': self.t_ready, 'stages': dict(self.stages),
+                'exit_code': self.exit_code, 'killed': self.kill_reason,
+                'fenced_out': self.fenced_out}

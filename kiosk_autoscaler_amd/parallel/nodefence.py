@@ -48,8 +48,9 @@ from .fence import MIN_SLOTS, FenceError
 logger = logging.getLogger('NodeFence')
 
 NODE_COMMANDS = ('comm_init', 'comm_uid', 'comm_shrink', 'comm_abort', 'fence',
-                 'fence_abort')
-NODE_EVENTS = ('comm_uid', 'comm_ready', 'fenced', 'node_agent')
+                 'fence_abort', 'fence_commit')
+NODE_EVENTS = ('comm_uid', 'comm_ready', 'fenced', 'node_agent',
+               'node_preloaded')
 STORE_KEY = 'kiosk:nodefence:{uid}:{epoch}'
 
 
@@ -99,15 +100,25 @@ class RcclNodeTransport(object):
     def make_uid(self, gen):
         return self.native.fence_unique_id().hex()
 
-    def connect(self, gen, rank, nranks, uid, should_abort=None):
+    def preload(self):
+        """RCCL's per-process one-time costs (library load + init), paid
+        when the agent starts rather than inside a generation: ms."""
+        preload = getattr(self.native, 'fence_preload', None)
+        return preload() if preload is not None else 0.0
+
+    def connect(self, gen, rank, nranks, uid, should_abort=None,
+                timeout=None):
         # two-phase: the object exists before the collective blocks, so a
         # peer death can abort it from the reader thread (request_abort);
         # an abort that raced ahead of the assignment is caught by the
-        # check right after it
-        self.comm = self.native.Fence(nranks, rank, self.timeout)
+        # check right after it.  ``timeout``: this connect's bound (a
+        # first generation's is longer); collectives keep ``self.timeout``
+        self.comm = self.native.Fence(nranks, rank, timeout or self.timeout)
         if should_abort is not None and should_abort():
             self.comm.request_abort()
         self.comm.connect(bytes.fromhex(uid))
+        if timeout and hasattr(self.comm, 'set_timeout'):
+            self.comm.set_timeout(self.timeout)
 
     @property
     def can_shrink(self):
@@ -176,7 +187,8 @@ class ShmNodeTransport(object):
     def make_uid(self, gen):
         return self.native.shm_unique_id(self.shm_dir)
 
-    def connect(self, gen, rank, nranks, uid, should_abort=None):
+    def connect(self, gen, rank, nranks, uid, should_abort=None,
+                timeout=None):
         self._interrupt = False
         self.comm = self.native.ShmComm(uid, nranks, rank, self.timeout)
         if should_abort is not None and should_abort():
@@ -264,7 +276,8 @@ class GlooNodeTransport(object):
         return os.path.join(self.root, 'kiosk-nodefence-%d-%s' % (
             gen, uuid.uuid4().hex[:12]))
 
-    def connect(self, gen, rank, nranks, uid, should_abort=None):
+    def connect(self, gen, rank, nranks, uid, should_abort=None,
+                timeout=None):
         import datetime
         import torch.distributed as dist
         self._aborted = bool(should_abort and should_abort())
@@ -327,7 +340,8 @@ class StoreNodeTransport(object):
     def make_uid(self, gen):
         return '%d-%s' % (gen, uuid.uuid4().hex[:12])
 
-    def connect(self, gen, rank, nranks, uid, should_abort=None):
+    def connect(self, gen, rank, nranks, uid, should_abort=None,
+                timeout=None):
         self.uid, self.rank, self.nranks = uid, rank, nranks
         self._aborted = bool(should_abort and should_abort())
         self._interrupt = False
@@ -417,7 +431,7 @@ class NodeFenceAgent(object):
     kernel is not queued behind a whole key of GEMMs."""
 
     def __init__(self, slot, transport, channel=None, events=None,
-                 uid_timeout=None, transport_factory=None):
+                 uid_timeout=None, transport_factory=None, preload=False):
         self.slot = int(slot)
         self.transport = transport
         # kind -> transport, for a manager-requested switch (the fallback
@@ -433,9 +447,12 @@ class NodeFenceAgent(object):
         self.rank = None
         self.nranks = 0
         # group -> (seq, epoch, mask): the last membership this rank agreed
-        # on per resource (its own all-reduce result; the worker gates its
-        # queue pulls on it, worker/runtime.py)
+        # on per resource -- its own all-reduce result, once the manager
+        # committed that fence (``fence_commit``: a fence the manager
+        # cancelled, e.g. before a shrink, never gates anything).
+        # The worker gates its queue pulls on it (worker/runtime.py)
         self.agreed = {}
+        self._results = {}    # seq -> (group, agreement) awaiting a commit
         self.agreed_cv = threading.Condition()
         self._uids = {}
         self._uid_cv = threading.Condition()
@@ -445,8 +462,16 @@ class NodeFenceAgent(object):
         self.completed = []
         self.idle = threading.Event()
         self.idle.set()
+        self._freeze_ms = 0.0    # fault injection (utils/faults.py)
+        self.preload_ms = None
         self._thread = threading.Thread(target=self._run, name='nodefence',
                                         daemon=True)
+        if preload and hasattr(self.transport, 'preload'):
+            # RCCL's one-time load, first thing on the agent thread: it
+            # never waits on (nor stalls) the process's kernel launches
+            # (kernels/launch.hpp), and a first generation then connects in
+            # well under a second instead of paying it inside its timeout
+            self._queue.put({'cmd': '_preload'})
         self._thread.start()
 
     # -- reader-thread side ------------------------------------------------
@@ -459,6 +484,9 @@ class NodeFenceAgent(object):
             return
         if cmd == 'fence_abort':
             self._aborted_epochs.add(message.get('seq'))
+            return
+        if cmd == 'fence_commit':
+            self._commit(int(message.get('seq', 0)))
             return
         if cmd == 'comm_shrink':
             # a collective blocked on the dead peer gives up now -- without
@@ -479,13 +507,30 @@ class NodeFenceAgent(object):
     def _aborted(self, gen):
         return self._abort_gen >= gen
 
+    def freeze_next_fence(self, ms):
+        """Fault injection (``freeze_agent``): the agent thread stalls this
+        long before its next fence, as a wedged rank would."""
+        self._freeze_ms = float(ms)
+
     # -- agent thread ------------------------------------------------------
     def _emit(self, ev, **fields):
         if self.channel is not None:
             self.channel.emit(ev, **fields)
 
-    def _wait_uid(self, gen):
-        deadline = time.monotonic() + self.uid_timeout
+    def _preload(self):
+        t0 = time.perf_counter()
+        try:
+            self.transport.preload()
+            self.preload_ms = (time.perf_counter() - t0) * 1e3
+            self._emit('node_preloaded', ms=self.preload_ms,
+                       transport=self.transport.name)
+        except Exception as err:  # pylint: disable=broad-except
+            logger.warning('RCCL preload failed: %s', err)
+            self._emit('node_preloaded', ms=None, error=str(err),
+                       transport=self.transport.name)
+
+    def _wait_uid(self, gen, timeout=None):
+        deadline = time.monotonic() + (timeout or self.uid_timeout)
         with self._uid_cv:
             while gen not in self._uids:
                 if self._aborted(gen):
@@ -500,6 +545,9 @@ class NodeFenceAgent(object):
     def _comm_init(self, message):
         gen, rank = int(message['gen']), int(message['rank'])
         nranks = int(message['nranks'])
+        # a generation with a process that never connected over RCCL gets
+        # the manager's longer first-generation budget
+        timeout = float(message.get('timeout') or 0.0) or None
         self._drop()
         wanted = message.get('transport')
         if wanted and wanted != self.transport.name:
@@ -516,9 +564,11 @@ class NodeFenceAgent(object):
                 uid = self.transport.make_uid(gen)
                 self._emit('comm_uid', gen=gen, uid=uid)
             else:
-                uid = self._wait_uid(gen)
+                uid = self._wait_uid(gen, timeout)
+            extra = {'timeout': timeout} if timeout else {}
             self.transport.connect(gen, rank, nranks, uid,
-                                   should_abort=lambda: self._aborted(gen))
+                                   should_abort=lambda: self._aborted(gen),
+                                   **extra)
         except Exception as err:  # pylint: disable=broad-except
             logger.warning('communicator generation %d failed: %s', gen, err)
             self._drop()
@@ -594,14 +644,28 @@ class NodeFenceAgent(object):
         if ok:
             # the agreed membership, read from this rank's own result
             mask = [i for i, bit in enumerate(result[1:]) if bit]
+            seq = int(message.get('seq', 0))
             with self.agreed_cv:
-                self.agreed[message.get('group')] = {
-                    'seq': int(message.get('seq', 0)), 'epoch': epoch,
-                    'slots': mask}
-                self.agreed_cv.notify_all()
+                self._results[seq] = (message.get('group'), {
+                    'seq': seq, 'epoch': epoch, 'slots': mask})
         else:
             report['detail'] = 'got %s expected %s' % (result, expected)
         return report
+
+    def _commit(self, seq):
+        """The manager published fence ``seq``: its result becomes this
+        rank's agreed membership (results of older fences are dropped)."""
+        with self.agreed_cv:
+            entry = self._results.pop(seq, None)
+            for old in [k for k in self._results if k < seq]:
+                del self._results[old]
+            if entry is None:
+                return
+            group, agreement = entry
+            current = self.agreed.get(group)
+            if current is None or current['seq'] < agreement['seq']:
+                self.agreed[group] = agreement
+                self.agreed_cv.notify_all()
 
     def agreement(self, group):
         """``{'seq', 'epoch', 'slots'}`` of the last fence of ``group`` this
@@ -615,6 +679,9 @@ class NodeFenceAgent(object):
             if message is None:
                 return
             cmd = message.get('cmd')
+            if cmd == '_preload':
+                self._preload()
+                continue
             if cmd == 'comm_init':
                 self._comm_init(message)
                 continue
@@ -630,6 +697,10 @@ class NodeFenceAgent(object):
             epoch = message.get('epoch')
             if message.get('seq') in self._aborted_epochs:
                 continue
+            if self._freeze_ms > 0:
+                freeze, self._freeze_ms = self._freeze_ms, 0.0
+                logger.warning('fault: node agent frozen for %.0f ms', freeze)
+                time.sleep(freeze / 1e3)
             self.idle.clear()
             try:
                 report = self.run_fence(message)

@@ -19,6 +19,10 @@ Spec (env ``KIOSK_FAULTS``, comma separated)::
     fail_start         raise during start-up (exit code 3, no READY)
     drop_redis_key=N   close the worker's Redis connections before key N
                        (the retrying client must reconnect transparently)
+    freeze_agent=N[:MS]  before key N, freeze the process's node-fence agent
+                       thread for MS ms (default 20000) at its next fence:
+                       a serving rank that stops answering, the process and
+                       its key otherwise healthy
 
 Each fault fires at most once per run of the whole stack: the first worker
 to reach it claims ``kiosk:fault:<name>`` with ``SET NX`` (TTL 1 h), so the
@@ -35,7 +39,7 @@ logger = logging.getLogger('Faults')
 CLAIM_KEY = 'kiosk:fault:{name}'
 CRASH_CODE = 86
 KINDS = ('crash_key', 'hang_key', 'slow_start', 'fail_start',
-         'drop_redis_key')
+         'drop_redis_key', 'freeze_agent')
 
 
 class InjectedFault(RuntimeError):
@@ -57,7 +61,8 @@ def parse(spec):
                 name, ', '.join(KINDS)))
         args = tuple(float(v) for v in value.split(':') if v.strip()) \
             if value else ()
-        if name in ('crash_key', 'hang_key', 'drop_redis_key') and not args:
+        if name in ('crash_key', 'hang_key', 'drop_redis_key',
+                    'freeze_agent') and not args:
             raise ValueError('%s needs a key index' % name)
         if name == 'slow_start' and not args:
             raise ValueError('slow_start needs milliseconds')
@@ -103,9 +108,14 @@ class FaultPlan(object):
         if 'slow_start' in self.faults and self._claim('slow_start'):
             time.sleep(self.faults['slow_start'][0] / 1e3)
 
-    def before_key(self, index, engine=None, redis=None):
+    def before_key(self, index, engine=None, redis=None, agent=None):
         """``index`` is 1-based over this worker's served keys."""
         f = self.faults
+        if 'freeze_agent' in f and agent is not None and \
+                index == int(f['freeze_agent'][0]) and \
+                self._claim('freeze_agent'):
+            args = f['freeze_agent']
+            agent.freeze_next_fence(args[1] if len(args) > 1 else 20000.0)
         if 'drop_redis_key' in f and index == int(f['drop_redis_key'][0]) \
                 and self._claim('drop_redis_key'):
             _drop_connections(redis)

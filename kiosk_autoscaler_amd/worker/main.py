@@ -391,11 +391,20 @@ def main(argv=None):
     if pin is not None and not args.assign:
         _preimport(backend)
         _preconnect()
+    if pin is not None and pin.get('prebuild') and not args.assign:
+        # the engine (weights, graphs -- the warm-start one included) first:
+        # an assignment then reaches READY with graph launches alone, which
+        # an RCCL load on the node agent's thread never holds up, and the
+        # agent below joins a generation only after this build
+        _prebuild_engine(backend, pin, channel)
     node_agent = None
     if node:
-        node_agent = _start_node_agent(channel, backend, early.get('slot', 0))
-    if pin is not None and pin.get('prebuild') and not args.assign:
-        _prebuild_engine(backend, pin, channel)
+        # a device-mode standby (HIP context open, launch handles resolved)
+        # pays RCCL's one-time load on the agent thread right away
+        node_agent = _start_node_agent(
+            channel, backend, early.get('slot', 0),
+            preload=bool(preinit) and bool(pin) and
+            pin.get('preinit') == 'device' and not args.assign)
     assignment = parse_assignment(args.assign) if args.assign else None
     recycles = 0
     max_recycles = int(os.environ.get('WORKER_MAX_RECYCLES', 64))
@@ -441,7 +450,7 @@ def main(argv=None):
     os._exit(code)
 
 
-def _start_node_agent(channel, backend, slot):
+def _start_node_agent(channel, backend, slot, preload=False):
     """The process-lifetime member of the node communicator: it serves
     ``comm_*`` / ``fence`` commands from the pipe's reader thread in the
     standby and the worker phases alike."""
@@ -449,7 +458,8 @@ def _start_node_agent(channel, backend, slot):
                                       choose_node_transport)
     transport = choose_node_transport(os.environ.get('FENCE', 'auto'),
                                       backend)
-    agent = NodeFenceAgent(slot, transport, channel=channel)
+    agent = NodeFenceAgent(slot, transport, channel=channel,
+                           preload=preload and transport.name == 'rccl')
     for cmd in NODE_COMMANDS:
         channel.direct[cmd] = agent.submit
     channel.start_reader()

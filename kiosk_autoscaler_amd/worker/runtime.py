@@ -416,7 +416,7 @@ class WorkerRuntime(object):
         cfg = self.config
         if self.faults:
             self.faults.before_key(self.keys_done + 1, self.engine,
-                                   self.redis)
+                                   self.redis, agent=self.node_agent)
         if callable(getattr(self.engine, 'infer', None)):
             self._run_plugin(consumer, jobs, t_start)
             return

@@ -16,11 +16,14 @@ Protocol (manager <-> zygote, one ``AF_UNIX`` ``SOCK_SEQPACKET`` pair):
 * the zygote forks twice: the intermediate child exits at once, so the
   worker is re-parented to the manager (``PR_SET_CHILD_SUBREAPER``) and the
   manager reaps it like any child (:class:`ForkedChild`);
-* zygote -> manager: ``{"pid": <worker pid>}`` (or ``{"error": ...}``).
+* zygote -> manager: ``{"id": <request id>, "pid": <worker pid>}`` (or
+  ``{"id", "error"}``).  A reply whose id is not the pending request's is a
+  late answer to one the manager gave up on, and is dropped.
 
 The worker process then runs :func:`kiosk_autoscaler_amd.worker.main.main`
 with the same argv a ``subprocess`` spawn would have used.
 """
+import itertools
 import json
 import os
 import signal
@@ -94,6 +97,12 @@ class ForkedChild(object):
         self.send_signal(signal.SIGTERM)
 
 
+class ZygoteLost(OSError):
+    """A fork request was sent but not answered in time: the zygote may
+    still own (and fork a worker on) the request's pipe ends, so the caller
+    must retire this zygote and must not reuse those pipes."""
+
+
 class ZygoteClient(object):
     """Manager side: start the zygote, fork workers from it."""
 
@@ -112,6 +121,7 @@ class ZygoteClient(object):
         self.ready = False
         self.preload_s = None
         self.forks = 0
+        self._ids = itertools.count(1)
 
     @property
     def pid(self):
@@ -162,10 +172,32 @@ class ZygoteClient(object):
         Returns a :class:`ForkedChild`."""
         if not self.ready and not self.wait_ready():
             raise OSError('zygote is not ready')
-        payload = json.dumps({'argv': list(argv), 'env': dict(env)}).encode()
+        rid = next(self._ids)
+        payload = json.dumps({'id': rid, 'argv': list(argv),
+                              'env': dict(env)}).encode()
         self.sock.settimeout(self.timeout)
         socket.send_fds(self.sock, [payload], list(fds))
-        reply = json.loads(self.sock.recv(MAX_MSG))
+        deadline = time.monotonic() + self.timeout
+        while True:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                raise ZygoteLost('zygote did not answer fork %d in %.1f s'
+                                 % (rid, self.timeout))
+            self.sock.settimeout(left)
+            try:
+                data = self.sock.recv(MAX_MSG)
+            except socket.timeout:
+                continue
+            except OSError as err:
+                raise ZygoteLost('zygote socket failed during fork %d: %s'
+                                 % (rid, err))
+            if not data:
+                raise ZygoteLost('zygote closed its socket during fork %d'
+                                 % rid)
+            reply = json.loads(data)
+            if reply.get('id') == rid:
+                break
+            # a late reply to a request given up on: not ours
         if 'pid' not in reply:
             raise OSError('zygote fork failed: %s' % reply.get('error'))
         self.forks += 1
@@ -241,6 +273,7 @@ def _serve(sock):
             return 0
         if not payload:
             return 0            # the manager went away
+        request = {}
         try:
             request = json.loads(payload)
             if len(fds) != 2:
@@ -248,7 +281,8 @@ def _serve(sock):
         except ValueError as err:
             for fd in fds:
                 os.close(fd)
-            sock.send(json.dumps({'error': str(err)}).encode())
+            sock.send(json.dumps({'id': request.get('id'),
+                                  'error': str(err)}).encode())
             continue
         r, w = os.pipe()
         mid = os.fork()
@@ -279,9 +313,11 @@ def _serve(sock):
         os.close(r)
         os.waitpid(mid, 0)
         if data:
-            sock.send(json.dumps({'pid': int(data)}).encode())
+            sock.send(json.dumps({'id': request.get('id'),
+                                  'pid': int(data)}).encode())
         else:
-            sock.send(json.dumps({'error': 'fork failed'}).encode())
+            sock.send(json.dumps({'id': request.get('id'),
+                                  'error': 'fork failed'}).encode())
 
 
 def main(argv=None):

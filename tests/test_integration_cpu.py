@@ -372,3 +372,68 @@ def test_dead_zygote_is_restarted(stack):
              timeout=30)
     spawns = [e for e in events.records if e['ev'] == 'process_spawn']
     assert spawns[-1]['via'] == 'zygote'
+
+
+def test_lost_zygote_fork_retires_it_and_spawns_on_fresh_pipes(stack):
+    """a fork request the zygote does not answer in time (here:
+    the zygote is frozen) must not fall back to a direct spawn on the same
+    pipe ends -- the zygote may still fork a worker on them.  The zygote is
+    retired and the worker is exec-spawned on a fresh pipe pair; the key is
+    served by exactly that worker."""
+    s, client, manager, scaler, events = stack(WARM_POOL='0')
+    wait_for(lambda: manager.zygote.poll_ready(), timeout=60)
+    frozen = manager.zygote
+    frozen.timeout = 0.5
+    os.kill(frozen.pid, signal.SIGSTOP)
+    try:
+        enqueue(client, 1)
+        assert tick(scaler, s) == 1
+        wait_for(lambda: client.hget('predict:job0', 'status') == 'done',
+                 timeout=30)
+    finally:
+        try:
+            os.kill(frozen.pid, signal.SIGCONT)
+        except OSError:
+            pass
+    retired = [e for e in events.records if e['ev'] == 'zygote_retired']
+    assert retired and retired[0]['pid'] == frozen.pid
+    spawns = [e for e in events.records if e['ev'] == 'process_spawn']
+    assert spawns[-1]['via'] == 'exec'
+    wait_for(lambda: frozen.popen.poll() is not None, timeout=10)
+
+
+def test_zygote_client_drops_late_replies():
+    """A reply to a request the client gave up on (ZygoteLost) is not taken
+    for the next request's: replies carry the request id."""
+    import json
+    import socket
+    import threading
+    from kiosk_autoscaler_amd.worker import zygote
+    ours, theirs = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    client = zygote.ZygoteClient.__new__(zygote.ZygoteClient)
+    client.sock, client.timeout, client.ready = ours, 0.3, True
+    client.forks = 0
+    import itertools
+    client._ids = itertools.count(1)
+    gate = threading.Event()
+
+    def fake_zygote():
+        for _ in range(2):
+            payload, fds, _, _ = socket.recv_fds(theirs, 1 << 16, 4)
+            for fd in fds:
+                os.close(fd)
+            rid = json.loads(payload)['id']
+            if rid == 1:
+                gate.wait(5)        # answers only after the client gave up
+            theirs.send(json.dumps({'id': rid, 'pid': 1000 + rid}).encode())
+    thread = threading.Thread(target=fake_zygote, daemon=True)
+    thread.start()
+    r, w = os.pipe()
+    with pytest.raises(zygote.ZygoteLost):
+        client.fork(['x'], {}, (r, w))
+    gate.set()
+    child = client.fork(['y'], {}, (r, w))
+    assert child.pid == 1002
+    thread.join(5)
+    os.close(r)
+    os.close(w)

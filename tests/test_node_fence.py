@@ -135,6 +135,31 @@ def test_agent_rank0_publishes_uid_then_fences():
     assert native.calls[-1] == ('destroy', False)
 
 
+def test_agreement_gates_only_on_committed_fences():
+    """a fence the manager cancelled (its result never
+    published) must not become the rank's agreed membership; only a
+    ``fence_commit`` promotes a result, and a commit drops older results."""
+    native = _FakeNative(nranks_results=[[3, 0, 1] + [0] * 6])
+    chan = _Channel()
+    agent = NodeFenceAgent(0, nodefence.RcclNodeTransport(native=native),
+                           channel=chan)
+    agent.submit({'cmd': 'comm_init', 'gen': 1, 'rank': 0, 'nranks': 2})
+    assert chan.next('comm_ready')['ok']
+    agent.submit({'cmd': 'fence', 'epoch': 3, 'seq': 1, 'gen': 1,
+                  'slots': [0, 1], 'width': 8, 'group': 'ns/r'})
+    assert chan.next('fenced')['ok']
+    assert agent.agreement('ns/r') is None          # not committed
+    native.peers = [[4, 0, 0] + [0] * 6]
+    agent.submit({'cmd': 'fence', 'epoch': 4, 'seq': 2, 'gen': 1,
+                  'slots': [0], 'width': 8, 'group': 'ns/r'})
+    assert chan.next('fenced')['ok']
+    agent.submit({'cmd': 'fence_commit', 'seq': 2})
+    assert agent.agreement('ns/r') == {'seq': 2, 'epoch': 4, 'slots': [0]}
+    agent.submit({'cmd': 'fence_commit', 'seq': 1})    # dropped by seq 2
+    assert agent.agreement('ns/r')['seq'] == 2
+    assert agent.close()
+
+
 def test_agent_non_root_waits_for_uid_and_aborts_cleanly():
     native = _FakeNative()
     chan = _Channel()
@@ -204,7 +229,8 @@ def test_agent_switches_transport_when_the_manager_asks():
         def make_uid(self, gen):
             return 'u%d' % gen
 
-        def connect(self, gen, rank, nranks, uid, should_abort=None):
+        def connect(self, gen, rank, nranks, uid, should_abort=None,
+                    timeout=None):
             made.append(('connect', gen, rank, nranks, uid))
 
         def close(self):
@@ -450,7 +476,8 @@ def _ensure_native(transport):
             pytest.skip('_kiosk_hip not built')
 
 
-def _node_stack(resp_server, transport, tmp_path, extra=None, **overrides):
+def _node_stack(resp_server, transport, tmp_path, extra=None, node=None,
+                **overrides):
     from kiosk_autoscaler_amd import Autoscaler, gpumgr
     from kiosk_autoscaler_amd.config import Config, Settings
     from kiosk_autoscaler_amd.redisq import RedisClient, StrictRedis
@@ -472,7 +499,10 @@ def _node_stack(resp_server, transport, tmp_path, extra=None, **overrides):
                       FAKE_RCCL_DIR=str(tmp_path), KIOSK_SHM_DIR=str(tmp_path))
     worker_env.update(extra or {})
     manager = gpumgr.build_manager(s, redis_client=client, events=events,
-                                   extra_env=worker_env).start()
+                                   extra_env=worker_env)
+    for name, value in (node or {}).items():
+        setattr(manager.node, name, value)
+    manager.start()
     proxy = RedisClient(host=resp_server.host, port=resp_server.port,
                         backoff=0)
     scaler = Autoscaler(proxy, s.QUEUES, actuator=manager)
@@ -959,6 +989,7 @@ def test_hung_rccl_init_at_eight_ranks_falls_back(resp_server, tmp_path):
     s, client, events, manager, scaler = _node_stack(
         resp_server, 'rccl-fake', tmp_path,
         extra={'FAKE_RCCL_MODE': 'init_hang'},
+        node={'first_init_timeout': timeout_s},
         FENCE_INIT_TIMEOUT=str(timeout_s))
     try:
         assert manager.node.init_timeout == timeout_s
@@ -1259,3 +1290,67 @@ def test_arrival_woken_pool_builds_its_generation_after_ready(resp_server,
         assert ready is not None and init is not None and init > ready
     finally:
         manager.stop(timeout=15)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize('transport', ['shm', 'rccl-fake'])
+def test_frozen_serving_rank_is_quarantined_not_killed(resp_server, tmp_path,
+                                                       transport):
+    """a *serving* worker whose node agent
+    thread freezes during a fence (``freeze_agent`` fault: the process and
+    its key stay healthy) is never SIGKILLed for the membership verdict.
+    It is quarantined: out of ``available_replicas`` and ``kiosk:active``,
+    drained without recycling so its in-flight key finishes, and the node
+    communicator is rebuilt without its slot meanwhile."""
+    s, client, events, manager, scaler = _node_stack(
+        resp_server, transport, tmp_path, MAX_PODS='3', WARM_POOL='3',
+        FENCE_INIT_TIMEOUT='1.5',
+        extra={'KIOSK_FAULTS': 'freeze_agent=1:15000'})
+    manager.node.hang_grace = 1.0
+
+    def view():
+        return manager.list_namespaced_deployment('default').items[0]
+    try:
+        wait_for(lambda: manager.node.ready and manager.node.full,
+                 timeout=60)
+        client.hset('predict:slow', mapping={'status': 'new', 'rows': 8,
+                                             'service_ms': 6000})
+        client.lpush('predict', 'predict:slow')
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 1}})
+        first = wait_for(lambda: [w for w in _ready_ids(manager)
+                                  if w['busy']], timeout=30)[0]
+        # a second worker: its READY starts the fence the frozen agent
+        # never answers
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 2}})
+        quarantined = wait_for(lambda: [e for e in events.records
+                                        if e['ev'] == 'worker_quarantined'],
+                               timeout=30)
+        assert quarantined[0]['worker'] == first['id']
+        assert quarantined[0]['busy']
+        # out of the agreed set while its key still runs
+        assert client.hget('predict:slow', 'status') != 'done'
+        active = _active(client)
+        assert not active or first['id'] not in active['members']
+        assert view().status.available_replicas <= 1
+        # the key finishes on the quarantined worker, which then exits 0
+        wait_for(lambda: client.hget('predict:slow', 'status') == 'done',
+                 timeout=30)
+        assert client.hget('predict:slow', 'worker') == first['id']
+        wait_for(lambda: any(e['ev'] == 'worker_exit' and
+                             e['worker'] == first['id']
+                             for e in events.records), timeout=30)
+        # service continues: two fenced workers again
+        wait_for(lambda: _converged(manager, client) and
+                 len(_ready_ids(manager)) == 2, timeout=60)
+        assert first['id'] not in _active(client)['members']
+    finally:
+        manager.stop(timeout=15)
+    kinds = [e['ev'] for e in events.records]
+    assert 'node_rank_hung' not in kinds
+    exit_ = [e for e in events.records if e['ev'] == 'worker_exit' and
+             e['worker'] == first['id']][0]
+    assert exit_['code'] == 0 and not exit_['killed'] and \
+        not exit_['recycled']
+    assert manager.node.quarantines == 1
