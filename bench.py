@@ -205,8 +205,9 @@ class Services(object):
             'RESOURCE_TYPE': args.resource_type,
             'MIN_PODS': '0', 'MAX_PODS': str(n_gpus),
             'KEYS_PER_POD': str(args.kpp), 'INTERVAL': str(args.interval),
-            'SCALE_POLICY': args.policy,
-            'SCALE_DOWN_DELAY': str(args.scale_down_delay),
+            'SCALE_POLICY': args.policy + (
+                ':%g' % args.scale_down_delay if args.scale_down_delay
+                else ''),
             'IDLE_INTERVAL': str(args.idle_interval),
             # BENCH_GPU_IDS (rehearsal only): e.g. '0,0' puts two slots on
             # the one GPU of a 1-GPU box to run the N=2 launch path there
@@ -215,10 +216,11 @@ class Services(object):
             'WORKER_BACKEND': args.backend, 'WARM_POOL': str(pool),
             'WARM_POOL_MODE': args.pool_mode,
             'WORKER_RECYCLE': '0' if args.no_recycle else '1',
-            'FENCE': args.fence, 'MODEL_DIM': str(args.dim),
-            'MODEL_HIDDEN': str(args.hidden), 'MODEL_LAYERS': str(args.layers),
-            'ROWS_PER_KEY': str(args.rows), 'EVENT_LOG': 'redis',
-            'TICK_KEY': TICK_KEY, 'DEBUG': '0',
+            'FENCE': args.fence,
+            'MODEL': '%dx%dx%d' % (args.dim, args.hidden, args.layers),
+            'ROWS_PER_KEY': str(args.rows),
+            # (EVENT_LOG=redis also publishes the tick instants: TICK_KEY)
+            'EVENT_LOG': 'redis',
             'LOG_FILE': os.path.join(OUT_DIR, '%s_autoscaler.log' % tag),
             'JOB_IDLE_EXIT_S': '0.5',
             'PYTHONPATH': ROOT + os.pathsep + env.get('PYTHONPATH', ''),

@@ -110,6 +110,28 @@ PYBIND11_MODULE(_kiosk_hip, m) {
       py::arg("ptr"), py::arg("n"), py::arg("seed"), py::arg("lo") = -1.0f,
       py::arg("hi") = 1.0f, py::arg("stream") = 0,
       py::call_guard<py::gil_scoped_release>());
+  // the input of a captured forward: the seed is read on the device at
+  // replay time, so one graph serves every job (models/torch_kiosk.py)
+  m.def(
+      "init_uniform_bf16_devseed",
+      [](unsigned long long p, size_t n, unsigned long long seed_ptr,
+         float lo, float hi, unsigned long long stream) {
+        check_hip(kiosk::launch_init_uniform_bf16_devseed(
+                      ptr<uint16_t>(p), n, ptr<const uint64_t>(seed_ptr), lo,
+                      hi, stream_of(stream)),
+                  "init_uniform_bf16_devseed");
+      },
+      py::arg("ptr"), py::arg("n"), py::arg("seed_ptr"), py::arg("lo") = -1.0f,
+      py::arg("hi") = 1.0f, py::arg("stream") = 0,
+      py::call_guard<py::gil_scoped_release>());
+  m.def("prepare_kernels",
+        [] {
+          check_hip(kiosk::gemm_prepare(), "gemm_prepare");
+          check_hip(kiosk::misc_prepare(), "misc_prepare");
+          check_hip(kiosk::warmstart_prepare(), "warmstart_prepare");
+        },
+        "raise LDS limits / load code objects once, outside any capture",
+        py::call_guard<py::gil_scoped_release>());
   m.def(
       "init_uniform_f32",
       [](unsigned long long p, size_t n, unsigned long long seed, float lo,

@@ -84,7 +84,7 @@ def build(settings=None, redis_client=None, actuator=None, events=None):
                        addr=settings.METRICS_ADDR)
     scaler = Autoscaler(redis_client=redis_client, queues=settings.QUEUES,
                         queue_delim=settings.QUEUE_DELIMITER,
-                        actuator=actuator, policy=settings.SCALE_POLICY,
+                        actuator=actuator, policy=settings.policy,
                         scale_down_delay=settings.SCALE_DOWN_DELAY,
                         events=events, tally=settings.TALLY_MODE)
     return redis_client, scaler, manager

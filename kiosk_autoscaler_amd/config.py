@@ -137,10 +137,15 @@ REFERENCE_DEFAULTS = (
     ('KEYS_PER_POD', int, 1),
 )
 
-#: MI355X-native additions (SURVEY §5.6 "New knobs").
+#: MI355X-native additions (SURVEY §5.6 "New knobs").  Round 4 pruned them
+#: from 39 to 25: merged spellings (``SCALE_POLICY``
+#: carries the strict policy's delay, ``MODEL`` the three model sizes,
+#: ``FENCE_FALLBACK`` its threshold, ``METRICS_PORT`` its address,
+#: ``WORKER_TIMEOUT`` the start bound) and former knobs that became
+#: constants (:data:`CONSTANTS`).
 EXTRA_DEFAULTS = (
-    ('SCALE_POLICY', str, 'reference'),     # reference | strict
-    ('SCALE_DOWN_DELAY', float, 0.0),       # strict: idle grace seconds
+    # reference | strict | strict:<s> (strict, scale down after s idle)
+    ('SCALE_POLICY', str, 'reference'),
     ('TALLY_MODE', str, 'reference'),       # reference (LLEN+SCAN) | atomic (MULTI)
     ('FIXED_RATE', bool, False),            # tick every INTERVAL (not tick+INTERVAL)
     ('IDLE_INTERVAL', float, 0.0),          # opt-in faster poll while at 0 pods
@@ -149,63 +154,84 @@ EXTRA_DEFAULTS = (
     ('WORKER_MODULE', str, 'kiosk_autoscaler_amd.worker.main'),
     ('WORKER_BACKEND', str, 'auto'),        # auto | hip | cpu
     ('WARM_POOL', int, -1),                 # standby processes (-1 = MAX_PODS)
-    # device (HIP context + code objects + queue) | context (HIP context
-    # only: no HBM) | import (imports only)
+    # device (HIP context + code objects + queue + prebuilt engine) |
+    # context (HIP context only: no HBM)
     ('WARM_POOL_MODE', str, 'device'),
     # s with no demand after which the standbys exit (0 = keep them): the
     # node then holds no GPU, like the reference at zero replicas; a key's
     # arrival wakes the pool ahead of the scale-up tick (below); each wake
     # builds a new RCCL node communicator after the woken worker is READY
-    ('POOL_IDLE_RELEASE_S', float, 600.0),
+    ('POOL_IDLE_RELEASE_S', float, 2.0),
     # with POOL_IDLE_RELEASE_S: s between queue-length reads while no worker
-    # runs; a new key refills a parked pool before the scale-up tick (the
-    # decision still waits for the tick; 0 = wake at the scale-up only)
+    # runs; a new key refills a parked pool just before the scale-up tick
+    # (the decision still waits for the tick; 0 = wake at the scale-up only)
     ('POOL_WAKE_POLL_S', float, 0.05),
-    # ... and wakes this long before the tick that will scale for the key
-    # (embedded manager: the loop tells it when that is), so the woken
-    # standbys hold the GPU for the lead, not the whole tick phase
-    ('POOL_WAKE_LEAD_S', float, 0.75),
-    # s a recycled standby keeps its engine (weights, arena, graphs; ~1.2
-    # GiB of the idle GPU's 2.6) without an assignment; then it frees it and
-    # keeps context, queue and node communicator (0 = keep forever)
-    ('ENGINE_IDLE_RELEASE_S', float, 60.0),
-    ('WARM_START', bool, True),             # run the N1 warm-start kernel
     # auto (rccl with device standbys, shm otherwise; store on CPU) | rccl
     # | shm | store | gloo | none
     ('FENCE', str, 'auto'),
-    ('MODEL_DIM', int, 4096),
-    ('MODEL_HIDDEN', int, 16384),
-    ('MODEL_LAYERS', int, 4),
+    ('FENCE_COMM', str, 'node'),            # node (persistent) | epoch
+    # node communicator transport after N (default 2) consecutive failed
+    # generations: '<transport>[:N]' ('' = keep retrying RCCL); RCCL is
+    # tried again once the node is idle
+    ('FENCE_FALLBACK', str, 'shm'),
+    # s a warm node-communicator generation (or shrink) may take to connect;
+    # a generation with a process new to RCCL gets max(60, 5 x this)
+    ('FENCE_INIT_TIMEOUT', float, 12.0),
+    ('MODEL', str, '4096x16384x4'),         # DIM x HIDDEN x LAYERS
     ('ROWS_PER_KEY', int, 2048),
     ('HBM_PER_KEY_BYTES', int, 0),          # 0 = derive from the model
     ('HBM_RESERVE_BYTES', int, 8 << 30),    # static sizing (no measurement)
-    ('HBM_FREE_RESERVE_BYTES', int, 1 << 30),  # sizing from measured free HBM
     ('EVENT_LOG', str, ''),                 # JSONL path | 'redis' | '' (off)
-    ('TICK_KEY', str, ''),                  # publish tick times to this key
-    ('STATE_TTL', int, 3600),
-    # s without progress while busy -> kill (0 = off)
+    # s without progress while busy, or from assignment to READY -> kill
+    # (0 = off)
     ('WORKER_TIMEOUT', float, 0.0),
-    # s from assignment to READY -> kill (0 = off)
-    ('START_TIMEOUT', float, 0.0),
     ('WORKER_RECYCLE', bool, True),         # drained worker -> warm pool
-    # spawn workers by fork() from a pre-imported zygote that holds no GPU
-    # (worker/zygote.py): cold spawns skip interpreter start + imports
-    ('WORKER_ZYGOTE', bool, True),
-    ('FENCE_COMM', str, 'node'),            # node (persistent) | epoch
-    # node communicator transport after FENCE_FALLBACK_AFTER consecutive
-    # failed generations ('' = keep retrying RCCL): membership keeps being
-    # fenced, over host shared memory, if RCCL cannot build the node
-    # communicator
-    ('FENCE_FALLBACK', str, 'shm'),
-    ('FENCE_FALLBACK_AFTER', int, 2),
-    # s a node-communicator generation (or shrink) may take to connect; a
-    # hung first init falls back within FENCE_FALLBACK_AFTER x this
-    ('FENCE_INIT_TIMEOUT', float, 12.0),
-    ('METRICS_PORT', int, 0),               # Prometheus /metrics port (0 = off)
-    ('METRICS_ADDR', str, '0.0.0.0'),
-    ('DEBUG', bool, True),
+    ('METRICS_PORT', str, '0'),             # Prometheus [addr:]port (0 = off)
     ('LOG_FILE', str, 'autoscaler.log'),
 )
+
+#: Former knobs, now fixed (round 4).  ``Settings`` still exposes them as
+#: attributes for the code that reads them.
+CONSTANTS = {
+    'DEBUG': True,                 # the reference always logs at DEBUG
+    'STATE_TTL': 3600,             # s the persisted manager state lives
+    'WARM_START': True,            # N1 always runs
+    'WORKER_ZYGOTE': True,         # spawns fork from the pre-imported zygote
+    'POOL_WAKE_LEAD_S': 0.75,      # cap of the adaptive wake lead
+    'ENGINE_IDLE_RELEASE_S': 60.0,  # a standby frees an unused engine
+    'HBM_FREE_RESERVE_BYTES': 1 << 30,  # kept free when sizing from hipMemGetInfo
+}
+TICK_KEY = 'kiosk:autoscaler:tick'   # published with EVENT_LOG=redis
+
+
+def parse_model(spec):
+    """``'4096x16384x4'`` -> ``(4096, 16384, 4)``."""
+    try:
+        dim, hidden, layers = (int(v) for v in str(spec).lower().split('x'))
+    except ValueError:
+        raise ValueError('MODEL must be DIMxHIDDENxLAYERS, got %r' % (spec,))
+    if min(dim, hidden, layers) < 1:
+        raise ValueError('MODEL sizes must be positive, got %r' % (spec,))
+    return dim, hidden, layers
+
+
+def parse_policy(spec):
+    """``'strict:2.5'`` -> ``('strict', 2.5)``; ``'reference'`` ->
+    ``('reference', 0.0)``."""
+    name, _, delay = str(spec).partition(':')
+    return name.strip() or 'reference', float(delay) if delay else 0.0
+
+
+def parse_fallback(spec):
+    """``'shm:3'`` -> ``('shm', 3)``; ``''`` -> ``('', 2)``."""
+    name, _, after = str(spec).partition(':')
+    return name.strip(), int(after) if after else 2
+
+
+def parse_listen(spec, default_addr='0.0.0.0'):
+    """``'9100'`` / ``'127.0.0.1:9100'`` -> ``(addr, port)``; port 0 = off."""
+    addr, _, port = str(spec).rpartition(':')
+    return addr or default_addr, int(port or 0)
 
 
 class Settings(object):
@@ -218,6 +244,17 @@ class Settings(object):
             if default is _MISSING and not require_resource_name:
                 default = ''
             setattr(self, name, config(name, default=default, cast=cast))
+        for name, value in CONSTANTS.items():
+            setattr(self, name, value)
+        # derived from the merged spellings
+        self.MODEL_DIM, self.MODEL_HIDDEN, self.MODEL_LAYERS = \
+            parse_model(self.MODEL)
+        self.policy, self.SCALE_DOWN_DELAY = parse_policy(self.SCALE_POLICY)
+        self.FENCE_FALLBACK, self.FENCE_FALLBACK_AFTER = \
+            parse_fallback(self.FENCE_FALLBACK)
+        self.METRICS_ADDR, self.METRICS_PORT = parse_listen(self.METRICS_PORT)
+        self.START_TIMEOUT = self.WORKER_TIMEOUT
+        self.TICK_KEY = TICK_KEY if self.EVENT_LOG == 'redis' else ''
 
     @property
     def queues(self):

@@ -51,7 +51,7 @@ def worker_env(settings, keys_per_pod=None):
         'MODEL_DIM': settings.MODEL_DIM, 'MODEL_HIDDEN': settings.MODEL_HIDDEN,
         'MODEL_LAYERS': settings.MODEL_LAYERS,
         'ROWS_PER_KEY': settings.ROWS_PER_KEY,
-        'WARM_START': int(settings.WARM_START), 'FENCE': settings.FENCE,
+        'FENCE': settings.FENCE,
         'FENCE_INIT_TIMEOUT': settings.FENCE_INIT_TIMEOUT,
         'ENGINE_IDLE_RELEASE_S': settings.ENGINE_IDLE_RELEASE_S,
         'RESOURCE_NAMESPACE': settings.RESOURCE_NAMESPACE,
@@ -63,14 +63,16 @@ def worker_env(settings, keys_per_pod=None):
     # standby measured (utils.hbm.size_from_free)
     env['HBM_PER_KEY_BYTES'] = settings.HBM_PER_KEY_BYTES
     env['HBM_FREE_RESERVE_BYTES'] = settings.HBM_FREE_RESERVE_BYTES
-    for passthrough in ('PASSES_PER_KEY', 'MOCK_WORK_MS', 'WORKER_BATCH',
-                        'JOB_IDLE_EXIT_S', 'POLL_BLOCK_S', 'MODEL_SEED',
-                        'KIOSK_RCCL_LIB', 'WORKER_EVENTS', 'KIOSK_FAULTS',
-                        'KIOSK_ROCTX', 'WORKER_KEEP_ENGINE',
-                        'WORKER_IMPORT_TORCH', 'WORKER_ENGINE',
-                        'WORKER_PYTHON_SITE', 'KIOSK_SHM_DIR',
-                        'KIOSK_NATIVE', 'FAKE_RCCL_DIR', 'FAKE_RCCL_MODE',
-                        'WORKER_MAX_RECYCLES'):
+    # worker-side settings that are not autoscaler knobs: the engine
+    # plug-in, per-key work shape, and test / debugging hooks
+    for passthrough in ('WORKER_ENGINE', 'WORKER_IMPORT_TORCH',
+                        'PASSES_PER_KEY', 'WORKER_BATCH', 'MODEL_SEED',
+                        'JOB_IDLE_EXIT_S', 'POLL_BLOCK_S', 'WORKER_EVENTS',
+                        'KIOSK_RCCL_LIB', 'KIOSK_FAULTS', 'KIOSK_ROCTX',
+                        'KIOSK_SHM_DIR', 'KIOSK_NATIVE', 'MOCK_WORK_MS',
+                        'FAKE_RCCL_DIR', 'FAKE_RCCL_MODE',
+                        'FAKE_RCCL_INIT_MS', 'WORKER_MAX_RECYCLES',
+                        'WARM_START'):
         if passthrough in os.environ:
             env[passthrough] = os.environ[passthrough]
     return env
@@ -108,9 +110,9 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
             per_key=settings.HBM_PER_KEY_BYTES)
     template = template_for(settings, backend, kpp)
     template.env.update(extra_env or {})
-    if settings.WARM_POOL_MODE not in ('device', 'context', 'import'):
-        raise ValueError('WARM_POOL_MODE must be device, context or import, '
-                         'got %r' % settings.WARM_POOL_MODE)
+    if settings.WARM_POOL_MODE not in ('device', 'context'):
+        raise ValueError('WARM_POOL_MODE must be device or context, got %r'
+                         % settings.WARM_POOL_MODE)
     pool = settings.WARM_POOL
     if pool < 0:
         pool = min(max(settings.MAX_PODS, 0), len(slots))

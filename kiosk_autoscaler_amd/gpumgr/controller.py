@@ -199,6 +199,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
         self._init_fencing(fence, fence_comm, fence_timeout,
                            fence_init_timeout, fence_fallback,
                            fence_fallback_after, fence_transport)
+
     # ------------------------------------------------------------------
     # API (the kubernetes AppsV1Api / BatchV1Api analogs)
     # ------------------------------------------------------------------
@@ -223,15 +224,19 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
             else:
                 self.resources[key].template = template
             return self.resources[key].view()
+
     def _list(self, kind, namespace):
         with self.lock:
             return ResourceList(items=[
                 r.view() for r in self.resources.values()
                 if r.kind == kind and r.namespace == namespace])
+
     def list_namespaced_deployment(self, namespace):
         return self._list('deployment', namespace)
+
     def list_namespaced_job(self, namespace):
         return self._list('job', namespace)
+
     def _patch(self, kind, name, namespace, body):
         declared = desired_from_body(kind, body)
         with self.lock:
@@ -251,10 +256,13 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
             view = resource.view()
         self._wake()
         return view
+
     def patch_namespaced_deployment(self, name, namespace, body):
         return self._patch('deployment', name, namespace, body)
+
     def patch_namespaced_job(self, name, namespace, body):
         return self._patch('job', name, namespace, body)
+
     def status(self):
         with self.lock:
             return {
@@ -274,6 +282,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                     w.summary() for w in r.workers.values()])
                     for r in self.resources.values()],
             }
+
     # ------------------------------------------------------------------
     # lifecycle
     # ------------------------------------------------------------------
@@ -295,11 +304,13 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                                             name='gpumgr', daemon=True)
             self._thread.start()
         return self
+
     def _wake(self):
         try:
             os.write(self._wake_w, b'x')
         except OSError:
             pass
+
     def _loop(self):
         while not self._stop.is_set():
             timeout = 0.05
@@ -308,6 +319,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                 # a deferred arrival wake is due: do not sleep past it
                 timeout = min(timeout, max(0.001, wake_at - time.monotonic()))
             self.poll(timeout)
+
     def stop(self, timeout=10.0):
         """Drain every worker, stop standbys, join the loop."""
         with self.lock:
@@ -349,6 +361,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
             if self.zygote is not None:
                 self.zygote.close()
                 self.zygote = None
+
     # ------------------------------------------------------------------
     # event loop body
     # ------------------------------------------------------------------
@@ -389,6 +402,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                 self._reconcile(resource)
                 self._maybe_fence(resource)
             self._refill_pool()
+
     def _free_slots(self):
         used = set()
         for resource in self.resources.values():
@@ -396,6 +410,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                 if worker.state != EXITED:
                     used.add(worker.slot.index)
         return [s for s in self.slots if s.index not in used]
+
     def _start_worker(self, resource, slot):
         wid = '%s-g%d-%s-%d' % (resource.name, slot.index, self.instance,
                                 next(self._worker_seq))
@@ -430,6 +445,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                     slot.visible_id or slot.index, proc.pid,
                     'warm pool' if from_pool else 'cold spawn')
         return worker
+
     def _size_from_free(self, resource, assign, free, slot):
         """N5: clamp this assignment's KEYS_PER_POD (the job worker's batch)
         to what fits in the HBM the standby measured free."""
@@ -457,6 +473,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
         self.events.emit('hbm_sizing', gpu=slot.index, hbm_free=free,
                          max_keys_per_pod=limit, keys_per_pod=kpp,
                          requested=tpl.keys_per_pod)
+
     def _drain(self, worker, reason, recycle=None):
         if worker.state in (DRAINING, EXITED):
             return
@@ -467,6 +484,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                                'recycle': bool(recycle)})
         self.events.emit('worker_drain', worker=worker.id, reason=reason)
         logger.info('Draining worker %s (%s).', worker.id, reason)
+
     def _reconcile(self, resource):
         live = resource.live()
         if len(live) < resource.declared and not self._stopping:
@@ -508,6 +526,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                     continue
                 self._drain(worker, 'scale-down')
                 excess -= 1
+
     def _on_worker_messages(self, worker):
         for message in worker.proc.pipe.read_messages():
             if message is None:
@@ -562,6 +581,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
     # key and has not exited this long after the drain is hung as a whole:
     # killed (a busy one is the WORKER_TIMEOUT watchdog's)
     QUARANTINE_EXIT_S = 30.0
+
     def _watchdog(self):
         """Failure detection beyond waitpid: kill workers that
         are alive but stuck.  The kill is an ordinary death afterwards --
@@ -596,6 +616,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                     worker.proc.popen.kill()
                 except OSError:
                     pass
+
     def _reap_all(self):
         for resource in self.resources.values():
             for worker in list(resource.workers.values()):
@@ -608,6 +629,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                 self._on_worker_messages(worker)
                 self._on_exit(resource, worker, code)
         self._reap_standbys()
+
     def _on_exit(self, resource, worker, code, recycled=False):
         was_ready = worker.state in (READY, DRAINING) and worker.t_ready
         # a drained worker the watchdog had to kill still counts as failed

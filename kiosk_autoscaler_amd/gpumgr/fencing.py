@@ -98,6 +98,7 @@ class FencingMixin(object):
         self.events.emit('worker_quarantined', worker=worker.id,
                          gpu=worker.slot.index, busy=worker.busy,
                          reason=reason)
+
     # ------------------------------------------------------------------
     # membership fence orchestration
     # ------------------------------------------------------------------
@@ -149,6 +150,7 @@ class FencingMixin(object):
                 'group': '%s/%s' % (resource.namespace, resource.name)})
         resource.fence_inflight = (epoch, members, time.monotonic())
         self.events.emit('fence_start', epoch=epoch, members=members)
+
     def _node_fence_runnable(self):
         """A resource has a membership change the node communicator can
         fence right now (every member runs on one of its ranks)."""
@@ -162,6 +164,7 @@ class FencingMixin(object):
             if self.node.can_fence([w.proc for w in members]):
                 return True
         return False
+
     def _maybe_node_fence(self, resource):
         """One 72-B all-reduce over the persistent communicator; waits
         (fence_wanted stays set) while a generation is being built or
@@ -184,6 +187,7 @@ class FencingMixin(object):
             self._publish_active(resource)
             return
         self.node.fence(resource, members)
+
     def _fence_failed(self, resource):
         """Retry with a fresh communicator after an exponential backoff, so
         a persistently failing bootstrap cannot spin on RCCL inits."""
@@ -194,6 +198,7 @@ class FencingMixin(object):
         resource.fence_retry_at = time.monotonic() + delay
         self.events.emit('fence_retry', name=resource.name, delay_s=delay,
                          failures=resource.fence_failures)
+
     def _on_fenced(self, resource, message):
         inflight = resource.fence_inflight
         if inflight is None or message.get('epoch') != inflight[0]:
@@ -207,6 +212,7 @@ class FencingMixin(object):
             self._fence_failed(resource)
             return
         self._fence_completed(resource, epoch, members, started, message)
+
     def _fence_failed_node(self, resource, message):
         """A node fence failed (not a shrink's interrupt): visible in the
         resource's ``status.fence`` until an epoch succeeds."""
@@ -215,6 +221,7 @@ class FencingMixin(object):
         self.events.emit('fence_failed', name=resource.name,
                          detail=resource.fence_error,
                          failures=resource.fence_failures)
+
     def _fence_completed(self, resource, epoch, members, started, message):
         resource.fence_fresh = False
         resource.fence_failures = 0
@@ -229,6 +236,7 @@ class FencingMixin(object):
                          n=message.get('n'), mode=message.get('mode'),
                          gen=message.get('gen'))
         self._publish_active(resource)
+
     def _publish_active(self, resource):
         if self.redis is None:
             return

@@ -76,6 +76,7 @@ class PoolMixin(object):
             # processing takes ~20 ms off every spawn
             argv.append('-S')
         return argv
+
     @staticmethod
     def _environment(template):
         env = dict(os.environ)
@@ -89,8 +90,8 @@ class PoolMixin(object):
         return env
     # env that decides what a worker imports: a zygote serves only the
     # templates it preloaded for
-    _IMPORT_ENV = ('WORKER_ENGINE', 'WORKER_IMPORT_TORCH', 'KIOSK_NATIVE',
-                   'WORKER_PYTHON_SITE')
+    _IMPORT_ENV = ('WORKER_ENGINE', 'WORKER_IMPORT_TORCH', 'KIOSK_NATIVE')
+
     def _start_zygote(self):
         tpl = self.pool_template
         if not self.zygote_enabled or tpl is None or self.zygote is not None \
@@ -107,6 +108,7 @@ class PoolMixin(object):
             tpl.backend]
         self.zygote = zygote.ZygoteClient(argv, self._environment(tpl))
         self.events.emit('zygote_spawn', pid=self.zygote.pid)
+
     def _check_zygote(self):
         """False (and the zygote forgotten, restarted after a pause) once
         the zygote process has exited."""
@@ -122,6 +124,7 @@ class PoolMixin(object):
         self.zygote = None
         self._zygote_restart_at = time.monotonic() + 10.0
         return False
+
     def _retire_zygote(self, reason):
         """A zygote that lost a fork request is not trusted again: killed,
         and restarted after the usual pause."""
@@ -136,6 +139,7 @@ class PoolMixin(object):
             pass
         z.close()
         self._zygote_restart_at = time.monotonic() + 10.0
+
     def _zygote_for(self, template):
         z = self.zygote
         tpl = self.pool_template
@@ -152,6 +156,7 @@ class PoolMixin(object):
                     for k in self._IMPORT_ENV)):
             return None
         return z
+
     def _spawn(self, template, role, assign=None, slot=None):
         cmd_r, cmd_w = os.pipe()
         ev_r, ev_w = os.pipe()
@@ -219,6 +224,7 @@ class PoolMixin(object):
         self.events.emit('process_spawn', role=role, pid=popen.pid,
                          slot=proc.slot, via=via)
         return proc
+
     def _refill_pool(self):
         """Keep one standby pinned to each of the lowest ``pool_size`` free
         GPUs (the slots the next scale-up will take)."""
@@ -241,6 +247,7 @@ class PoolMixin(object):
                 changed = True
         if changed:
             self._publish_pool()
+
     def _park_pool(self):
         """Deep idle (``POOL_IDLE_RELEASE_S``): with no declared or live
         worker for that long, retire every standby -- the node then holds
@@ -318,6 +325,7 @@ class PoolMixin(object):
         logger.info('No demand for %.0f s: released %d standby process(es).',
                     now - self._last_demand, released)
         return True
+
     def note_next_tick(self, t_monotonic):
         """The autoscaler loop's next tick instant (``time.monotonic``
         seconds, system-wide, so a ``unix:`` daemon's clients report it
@@ -336,6 +344,7 @@ class PoolMixin(object):
                 # the tick came earlier than planned for (IDLE_INTERVAL)
                 self._wake_at = min(self._wake_at, self._next_tick - lead)
         self._wake()
+
     def wake_lead(self):
         """Seconds before the next tick an arrival wakes a parked pool:
         ``pool_wake_lead_s`` until woken standbys have been timed, then
@@ -348,6 +357,7 @@ class PoolMixin(object):
             return cap
         return min(cap, max(0.2, 1.5 * max(self._wake_boots) + 0.05 +
                             self.pool_wake_poll_s))
+
     def _prebuild_spec(self, template):
         """What an arrival-woken standby builds its engine for: the shape
         (kind, keys per pod) of the resource its template serves."""
@@ -356,6 +366,7 @@ class PoolMixin(object):
                 return {'kind': resource.kind,
                         'keys_per_pod': resource.template.keys_per_pod}
         return {'kind': 'deployment', 'keys_per_pod': template.keys_per_pod}
+
     def _arrived(self, now):
         """True when a managed queue grew since the last check (read every
         ``pool_wake_poll_s`` while no worker is declared or live).  Growth,
@@ -383,6 +394,7 @@ class PoolMixin(object):
             self.events.emit('arrival', queues=grown,
                              parked=self.pool_parked)
         return bool(grown)
+
     def _take_standby(self, template, slot):
         """The standby pinned to ``slot`` (booted or still booting: it
         reads the assignment as soon as its imports finish)."""
@@ -396,6 +408,7 @@ class PoolMixin(object):
         del self.standbys[slot.index]
         self._publish_pool()
         return proc
+
     def _publish_slots(self):
         """The slot table as verified so far (``kiosk:slots``): the bench
         samples amdsmi on these PCI addresses, not on KFD order."""
@@ -408,6 +421,7 @@ class PoolMixin(object):
                  'kind': s.kind} for s in self.slots]))
         except Exception:  # pylint: disable=broad-except
             pass
+
     def _publish_pool(self):
         if self.redis is None:
             return
@@ -421,12 +435,14 @@ class PoolMixin(object):
                 int(self.pool_parked)))
         except Exception:  # pylint: disable=broad-except
             pass
+
     def _on_standby_messages(self, proc):
         for message in proc.pipe.read_messages():
             if message is None:
                 proc.eof = True
                 continue
             self._on_standby_message(proc, message)
+
     def _on_standby_message(self, proc, message):
         if self.node is not None and message.get('ev') in NODE_EVENTS:
             self.node.on_message(proc, message)
@@ -467,6 +483,7 @@ class PoolMixin(object):
                              / 1e9, preinit=message.get('preinit'),
                              recycled=proc.role == 'standby' and
                              proc.recycles > 0)
+
     def _check_device(self, proc, pci):
         """the slot table maps slot -> HIP ordinal -> PCI address
         from KFD topology order, which drives the HIP_VISIBLE_DEVICES pin,
@@ -508,12 +525,14 @@ class PoolMixin(object):
             self.retiring.append(proc)
             return False
         return True
+
     def _recycle_ok(self, resource):
         tpl = self.pool_template
         return bool(self.recycle and self.pool_size and tpl is not None and
                     not self._stopping and
                     resource.template.module == tpl.module and
                     resource.template.backend == tpl.backend)
+
     def _on_recycled(self, worker, message):
         """A worker finished cleanly and kept its process: account for it
         like an exit, then adopt the process as its GPU's standby."""
@@ -538,7 +557,9 @@ class PoolMixin(object):
         else:
             proc.pipe.send({'cmd': 'exit'})
             self.retiring.append(proc)
+
     ORPHAN_SCAN_S = 5.0
+
     def _reap_orphans(self, now=None):
         """Subreaper hygiene: a descendant a worker orphaned is
         re-parented to this process; nothing waits for it, so it would stay
@@ -588,6 +609,7 @@ class PoolMixin(object):
         if reaped:
             self.events.emit('orphans_reaped', pids=reaped)
         return reaped
+
     def _reap_standbys(self):
         """Forget exited standby / retired processes (``standby_exit``
         closes their standby GPU time in the metrics).  True if a retired

@@ -39,15 +39,14 @@ class WorkerTemplate(object):
 def bare_worker(template):
     """Spawn with ``python -S``: our own HIP worker with the built-in engine,
     not importing torch (``WORKER_IMPORT_TORCH``), unless
-    ``WORKER_PYTHON_SITE=1``."""
+    a plug-in engine or a torch import needs site-packages."""
     def flag(name):
         value = template.env.get(name, os.environ.get(name, '0'))
         return str(value) not in ('0', '')
     return (template.backend == 'hip' and
             template.module == 'kiosk_autoscaler_amd.worker.main' and
             not flag('WORKER_ENGINE') and    # a plug-in may need packages
-            not flag('WORKER_IMPORT_TORCH') and
-            not flag('WORKER_PYTHON_SITE'))
+            not flag('WORKER_IMPORT_TORCH'))
 
 
 class Pipe(object):

@@ -27,6 +27,7 @@ class StateMixin(object):
     def _state_key(self, resource):
         return STATE_KEY.format(ns=resource.namespace, kind=resource.kind,
                                 name=resource.name)
+
     def _persist(self, resource):
         if self.redis is None:
             return
@@ -43,6 +44,7 @@ class StateMixin(object):
                 self.redis.expire(key, self.state_ttl)
         except Exception as err:  # pylint: disable=broad-except
             logger.warning('could not persist manager state: %s', err)
+
     def _restore(self, resource):
         if self.redis is None:
             return
@@ -63,6 +65,7 @@ class StateMixin(object):
         logger.info('Restored %s %s: declared=%d generation=%d.',
                     resource.kind, resource.name, resource.declared,
                     resource.generation)
+
     def recover_orphans(self, resource):
         """Requeue ``processing-<q>:<resource>-g*`` items whose worker is
         not one of ours (a previous manager instance died with them)."""
@@ -93,6 +96,7 @@ class StateMixin(object):
             logger.warning('Requeued %d orphaned in-flight items of %s.',
                            moved, resource.name)
         return moved
+
     def _requeue(self, resource, worker):
         """Push a dead worker's in-flight items back to their queues."""
         if self.redis is None:
@@ -116,6 +120,7 @@ class StateMixin(object):
         if moved:
             self.events.emit('requeue', worker=worker.id, items=moved)
         return moved
+
     def _publish_worker(self, worker):
         if self.redis is None:
             return

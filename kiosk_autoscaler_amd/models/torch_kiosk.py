@@ -1,0 +1,218 @@
+"""PyTorch-ROCm worker engine on the hand-written gfx950 kernels.
+
+``WORKER_ENGINE=kiosk_autoscaler_amd.models.torch_kiosk:TorchKioskEngine``
+runs the worker model (``MODEL_LAYERS`` blocks of ``MODEL_DIM`` ->
+``MODEL_HIDDEN`` -> ``MODEL_DIM``, tanh-GELU, residual, bf16) in a PyTorch
+process, with every byte of device memory a torch tensor (torch's caching
+allocator, torch's stream) and every kernel one of ours:
+
+* weights: bf16 / fp32 torch tensors filled by the N2 init kernel with the
+  built-in engine's seeds (:func:`~..ops.kernels.model_weights`), so both
+  engines serve bit-identical outputs for the same job;
+* forward: per layer the 256x256 LDS-ring GEMM with the fused bias+GELU
+  epilogue, then the down-projection GEMM with the fused bias+residual
+  epilogue (split-K into a preallocated workspace where the grid alone would
+  leave CUs idle), then the deterministic partial-sum kernel -- the whole
+  forward, input generation included, captured once into a
+  ``torch.cuda.CUDAGraph``.  The job's seed reaches the captured input
+  kernel through a pinned host word copied inside the graph, so a forward
+  is exactly one graph launch;
+* N1 warm-start: the warm-start kernel over the engine's own first weight
+  matrix (every CU, the GEMM's LDS ring zeroed, an MFMA loop), captured as
+  a second graph: once the engine is built, READY is one graph launch --
+  which RCCL's one-time load on the node agent's thread cannot hold up
+  (``profiles/r4_collision``).
+
+The reference's worker is whatever image its Deployment runs
+(``/root/reference/autoscaler/autoscaler.py:235-237``); this is the
+framework's own PyTorch-ROCm one.
+"""
+import time
+
+from ..ops import kernels as ops
+from ..ops import native
+
+# MFMA iterations of the warm-start loop (the native engine's default)
+_WARM_ITERS = 4096
+
+
+class TorchKioskEngine(object):
+    name = 'torch-kiosk'
+
+    @staticmethod
+    def warm_device():
+        """Standby boot (``worker/main.py``): torch's CUDA context and
+        caching allocator plus our launch handles -- no hipBLASLt handle
+        (this engine never calls a torch matmul)."""
+        import torch
+        torch.empty(1, device='cuda').zero_()
+        native.load().prepare_kernels()
+
+    def __init__(self, cfg, stage=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError('TorchKioskEngine needs a GPU')
+        self.torch = torch
+        self.mod = native.load()       # after torch: one HIP runtime
+        self.device = torch.device('cuda')
+        self.dim, self.hidden, self.layers = cfg.dim, cfg.hidden, cfg.layers
+        self.max_rows = max(int(cfg.rows) * int(cfg.batch), 256)
+        self.seed = int(cfg.seed)
+        # LDS limits, code objects, launch handles: once, outside capture
+        self.mod.prepare_kernels()
+        self.stream = torch.cuda.Stream()
+        with torch.cuda.stream(self.stream):
+            self.weights = ops.model_weights(self.dim, self.hidden,
+                                             self.layers, self.seed)
+            rows, dim, hidden = self.max_rows, self.dim, self.hidden
+            bf16 = dict(dtype=torch.bfloat16, device=self.device)
+            self.x = torch.empty((rows, dim), **bf16)    # input / ping
+            self.y = torch.empty((rows, dim), **bf16)    # pong
+            self.h = torch.empty((rows, hidden), **bf16)
+            self.partials = torch.zeros(self.mod.sum_blocks,
+                                        dtype=torch.float32,
+                                        device=self.device)
+            ws = max(self.mod.gemm_workspace_bytes(rows, hidden, dim),
+                     self.mod.gemm_workspace_bytes(rows, dim, hidden))
+            self.workspace = torch.empty(max(1, ws // 4), dtype=torch.float32,
+                                         device=self.device)
+            self.workspace_bytes = ws
+            self.seed_dev = torch.zeros(1, dtype=torch.int64,
+                                        device=self.device)
+            self.warm_record = torch.zeros(
+                (self._cus() * 8,), dtype=torch.int32, device=self.device)
+        self.seed_host = torch.zeros(1, dtype=torch.int64).pin_memory()
+        self.stream.synchronize()
+        if stage:
+            stage('weights_on_device')
+        self.graphs = {}               # rows -> (CUDAGraph, output tensor)
+        self.warm_graph = None
+        self._capture(self.max_rows)
+        self._capture_warm()
+        if stage:
+            stage('graphs_ready')
+
+    # -- construction -----------------------------------------------------
+    def _cus(self):
+        props = self.torch.cuda.get_device_properties(self.device)
+        return int(props.multi_processor_count)
+
+    def _enqueue_forward(self, rows):
+        """The forward on the current stream (captured, never run eagerly
+        outside a graph)."""
+        torch = self.torch
+        mod = self.mod
+        stream = torch.cuda.current_stream().cuda_stream
+        self.seed_dev.copy_(self.seed_host, non_blocking=True)
+        x = self.x[:rows]
+        mod.init_uniform_bf16_devseed(x.data_ptr(), x.numel(),
+                                      self.seed_dev.data_ptr(), -1.0, 1.0,
+                                      stream)
+        cur, nxt = self.x, self.y
+        h = self.h[:rows]
+        for w1, b1, w2, b2 in self.weights:
+            mod.gemm(cur.data_ptr(), w1.data_ptr(), h.data_ptr(),
+                     b1.data_ptr(), 0, rows, self.hidden, self.dim,
+                     ops.EPILOGUES['gelu'], stream, ops.VARIANTS['auto'],
+                     self.workspace.data_ptr(), self.workspace_bytes)
+            mod.gemm(h.data_ptr(), w2.data_ptr(), nxt.data_ptr(),
+                     b2.data_ptr(), cur.data_ptr(), rows, self.dim,
+                     self.hidden, ops.EPILOGUES['residual'], stream,
+                     ops.VARIANTS['auto'], self.workspace.data_ptr(),
+                     self.workspace_bytes)
+            cur, nxt = nxt, cur
+        out = cur[:rows]
+        mod.partial_sums(out.data_ptr(), out.numel(),
+                         self.partials.data_ptr(), stream)
+        return out
+
+    def _capture(self, rows):
+        torch = self.torch
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(self.stream):
+            with torch.cuda.graph(graph, stream=self.stream):
+                out = self._enqueue_forward(rows)
+        self.graphs[rows] = (graph, out)
+        return self.graphs[rows]
+
+    def _capture_warm(self):
+        torch = self.torch
+        w1 = self.weights[0][0]
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(self.stream):
+            with torch.cuda.graph(graph, stream=self.stream):
+                self.warm_record.zero_()
+                self.mod.warmstart_raw(
+                    w1.data_ptr(), w1.numel(), self.warm_record.data_ptr(),
+                    self._cus(), _WARM_ITERS, self.mod.gemm_ring_lds_bytes,
+                    torch.cuda.current_stream().cuda_stream)
+        self.warm_graph = graph
+
+    # -- plug-in contract ---------------------------------------------------
+    def warmstart(self):
+        """N1: one graph launch (every CU, LDS ring, MFMA loop)."""
+        t0 = time.perf_counter()
+        with self.torch.cuda.stream(self.stream):
+            self.warm_graph.replay()
+        self.stream.synchronize()
+        rec = self.warm_record.view(-1, 8)
+        return {'backend': 'torch-kiosk', 'blocks': int(rec.shape[0]),
+                'wall_us': (time.perf_counter() - t0) * 1e6,
+                'graph': True}
+
+    def forward(self, rows, seed):
+        """One forward of ``rows`` rows of the ``seed`` input: a graph
+        launch (rows other than the captured capacity get their own graph,
+        captured once).  Returns the bf16 output view (valid until the next
+        forward)."""
+        if not 1 <= rows <= self.max_rows:
+            raise ValueError('rows=%d outside [1, %d]' % (rows,
+                                                          self.max_rows))
+        entry = self.graphs.get(rows) or self._capture(rows)
+        # the previous replay may still read the pinned seed word
+        self.stream.synchronize()
+        self.seed_host[0] = int(seed)
+        with self.torch.cuda.stream(self.stream):
+            entry[0].replay()
+        return entry[1]
+
+    def infer(self, jobs):
+        """One forward per job; ``service_ms`` (the benchmark's fixed
+        per-key GPU time) repeats it until that much time has passed."""
+        out = []
+        for job in jobs:
+            t0 = time.perf_counter()
+            rows, seed = int(job['rows']), int(job['seed'])
+            self.forward(rows, seed)
+            passes = 1
+            budget = float(job.get('service_ms') or 0) / 1e3
+            while True:
+                self.stream.synchronize()
+                if time.perf_counter() - t0 >= budget:
+                    break
+                self.forward(rows, seed)
+                passes += 1
+            total = float(self.partials.double().sum().item())
+            out.append({'output_sum': '%.6e' % total, 'passes': passes,
+                        'engine': self.name})
+        return out
+
+    def output(self, rows, seed):
+        """The forward's ``[rows, dim]`` output as a fresh tensor (tests)."""
+        y = self.forward(rows, seed)
+        self.stream.synchronize()
+        return y.clone()
+
+    def hbm_bytes(self):
+        return int(sum(t.numel() * t.element_size()
+                       for layer in self.weights for t in layer) +
+                   sum(t.numel() * t.element_size()
+                       for t in (self.x, self.y, self.h, self.workspace)))
+
+    def close(self):
+        self.graphs = {}
+        self.warm_graph = None
+        self.weights = None
+        self.x = self.y = self.h = self.workspace = None
+        self.torch.cuda.synchronize()
+        self.torch.cuda.empty_cache()

@@ -99,8 +99,21 @@ def _warm_torch():
     if not torch.cuda.is_available():
         return {}
     t0 = time.monotonic_ns()
-    a = torch.ones(256, 256, device='cuda', dtype=torch.bfloat16)
-    float((a @ a).float().sum())
+    hook = None
+    spec = os.environ.get('WORKER_ENGINE')
+    if spec:
+        from ..models.plugin import load_factory
+        try:
+            hook = getattr(load_factory(spec), 'warm_device', None)
+        except Exception:  # pylint: disable=broad-except
+            hook = None
+    if callable(hook):
+        # the engine knows what its device start-up needs (the native-kernel
+        # PyTorch engine: torch's context and allocator, no BLAS handle)
+        hook()
+    else:
+        a = torch.ones(256, 256, device='cuda', dtype=torch.bfloat16)
+        float((a @ a).float().sum())
     torch.cuda.synchronize()
     return {'torch_warm_start': t0, 'torch_warm_done': time.monotonic_ns()}
 
@@ -161,7 +174,7 @@ def _report_device(backend):
     if pci:
         _CHANNEL[0].device_reported = True
         _CHANNEL[0].emit('device', pci=pci)
-# HIP engines kept across recycles (WORKER_KEEP_ENGINE=1): the recycled
+# engines kept across recycles: the recycled
 # standby's next assignment with the same model finds its weights, graph
 # and pass time resident and only re-runs the warm-start kernel
 _ENGINES = {}
@@ -183,7 +196,7 @@ def _cached_engine(backend, cfg, stage):
     capacity match (anything else cached is freed first), else a new one."""
     from ..models.mlp import create_engine
     key = _engine_key(backend, cfg)
-    keep = os.environ.get('WORKER_KEEP_ENGINE', '1') not in ('0', '')
+    keep = True
     if key is not None and keep and key in _ENGINES and \
             getattr(_ENGINES[key], 'engine', None) is not None:
         engine = _ENGINES[key]
@@ -407,7 +420,10 @@ def main(argv=None):
             pin.get('preinit') == 'device' and not args.assign)
     assignment = parse_assignment(args.assign) if args.assign else None
     recycles = 0
-    max_recycles = int(os.environ.get('WORKER_MAX_RECYCLES', 64))
+    # forced retirement after N recycles (test hook; 0 = never): the soak
+    # shows no idle-HBM drift over 80 assignments (profiles/r3_soak), and
+    # every retirement cost a shrink plus a regrow
+    max_recycles = int(os.environ.get('WORKER_MAX_RECYCLES', 0)) or None
     while True:
         if assignment is None:
             assignment = _wait_for_assignment(channel, pin, preload_ns,
@@ -424,7 +440,7 @@ def main(argv=None):
         # loaded code objects -- it goes back to being this GPU's standby,
         # so the next scale-up on it skips the ~2 s process boot.
         if not (code == 0 and runtime.recycle and
-                recycles < max_recycles):
+                (max_recycles is None or recycles < max_recycles)):
             break
         recycles += 1
         # the engine's HBM is already freed: report first, collect after

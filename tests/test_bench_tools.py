@@ -195,7 +195,10 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
     assert line['keys_done'] == line['keys'] > 0
     # the pool settings scale.py ran with (config defaults, env unset)
     if 'POOL_IDLE_RELEASE_S' not in os.environ:
-        assert line['config']['pool_idle_release_s'] == 600.0
+        from kiosk_autoscaler_amd.config import EXTRA_DEFAULTS
+        default = dict((n, d) for n, _, d in EXTRA_DEFAULTS)
+        assert line['config']['pool_idle_release_s'] == \
+            default['POOL_IDLE_RELEASE_S']
         assert line['config']['pool_wake_poll_s'] == 0.05
 
 

@@ -79,7 +79,7 @@ def test_start_failure_and_start_timeout(stack):
 def test_slow_start_killed_by_start_timeout(stack):
     s, client, manager, scaler, events = stack(
         extra_env={'KIOSK_FAULTS': 'slow_start=60000'}, WARM_POOL='1',
-        START_TIMEOUT='2.0')
+        WORKER_TIMEOUT='2.0')
     dead = _served_once_after_failure(s, client, manager, scaler, events)
     assert dead['killed'].startswith('not READY')
 
@@ -104,7 +104,7 @@ def test_gpu_hung_kernel_killed_by_watchdog(stack):
     s, client, manager, scaler, events = stack(
         extra_env={'KIOSK_FAULTS': 'hang_key=1:20000'}, WARM_POOL='1',
         WORKER_BACKEND='hip', WORKER_TIMEOUT='2.0', FENCE='none',
-        MODEL_DIM='1024', MODEL_HIDDEN='4096', MODEL_LAYERS='2',
+        MODEL='1024x4096x2',
         ROWS_PER_KEY='256')
     wait_for(lambda: manager.standbys and all(
         p.booted for p in manager.standbys.values()), timeout=120)
@@ -124,7 +124,7 @@ def test_gpu_worker_recycled_and_reused(stack):
     and serves with a freshly built engine."""
     s, client, manager, scaler, events = stack(
         WARM_POOL='1', WORKER_BACKEND='hip', FENCE='none',
-        MODEL_DIM='1024', MODEL_HIDDEN='4096', MODEL_LAYERS='2',
+        MODEL='1024x4096x2',
         ROWS_PER_KEY='256')
     wait_for(lambda: manager.standbys and all(
         p.booted for p in manager.standbys.values()), timeout=120)

@@ -27,9 +27,10 @@ def test_job_kpp4_clamped_to_measured_free(stack):
     weights = hbm.model_bytes(64, 256, 1)
     s, client, manager, scaler, events = stack(
         RESOURCE_TYPE='job', KEYS_PER_POD='4', MAX_PODS='1',
-        MODEL_DIM='64', MODEL_HIDDEN='256', MODEL_LAYERS='1',
-        HBM_PER_KEY_BYTES=str(10 ** 9), HBM_FREE_RESERVE_BYTES='0',
+        MODEL='64x256x1',
+        HBM_PER_KEY_BYTES=str(10 ** 9),
         extra_env={'MOCK_HBM_FREE_BYTES': str(int(weights + 2.5e9)),
+                   'HBM_FREE_RESERVE_BYTES': '0',
                    'JOB_IDLE_EXIT_S': '0.3', 'MOCK_WORK_MS': '50'})
     wait_for(lambda: manager.standbys and all(
         p.booted for p in manager.standbys.values()))
@@ -103,9 +104,10 @@ def test_recycled_standby_reports_its_cached_engine_as_free(stack):
     per_key = 10 ** 9
     s, client, manager, scaler, events = stack(
         RESOURCE_TYPE='deployment', KEYS_PER_POD='4', MAX_PODS='1',
-        WARM_POOL='1', MODEL_DIM='64', MODEL_HIDDEN='256', MODEL_LAYERS='1',
-        HBM_PER_KEY_BYTES=str(per_key), HBM_FREE_RESERVE_BYTES='0',
+        WARM_POOL='1', MODEL='64x256x1',
+        HBM_PER_KEY_BYTES=str(per_key),
         extra_env={'MOCK_HBM_FREE_BYTES': str(int(weights + 3.5 * per_key)),
+                   'HBM_FREE_RESERVE_BYTES': '0',
                    'MOCK_WORK_MS': '20'})
     for cycle in range(2):
         wait_for(lambda: manager.standbys and all(
@@ -180,12 +182,14 @@ def test_arrival_rebuilds_a_released_engine(stack):
                       if e['ev'] == 'engine_released'], timeout=30)
     wait_for(lambda: manager.standbys and
              not manager.standbys[0].engine_cached, timeout=30)
+    before = len(events.records)
     client.hset('predict:late', mapping={'status': 'new'})
     client.lpush('predict', 'predict:late')
-    built = wait_for(lambda: [e for e in events.records
+    wait_for(lambda: [e for e in events.records[before:]
+                      if e['ev'] == 'engine_rebuild'], timeout=30)
+    built = wait_for(lambda: [e for e in events.records[before:]
                               if e['ev'] == 'standby_prebuilt'], timeout=30)
     assert built[-1]['error'] is None
-    assert [e for e in events.records if e['ev'] == 'engine_rebuild']
     view = manager.list_namespaced_deployment('default').items[0]
     assert view.spec.replicas == 0
     assert manager.standbys[0].engine_cached

@@ -488,7 +488,9 @@ def _node_stack(resp_server, transport, tmp_path, extra=None, node=None,
            'QUEUES': 'predict,track', 'RESOURCE_NAME': 'worker',
            'MAX_PODS': '8', 'KEYS_PER_POD': '1', 'WORKER_BACKEND': 'cpu',
            'WARM_POOL': '8', 'FENCE': fence, 'INTERVAL': '1',
-           'REDIS_INTERVAL': '0', 'EVENT_LOG': 'redis'}
+           'REDIS_INTERVAL': '0', 'EVENT_LOG': 'redis',
+           # a resident pool (the deep-idle default parks it after 2 s)
+           'POOL_IDLE_RELEASE_S': '0'}
     env.update(overrides)
     s = Settings(Config(environ=env, use_files=False))
     client = StrictRedis(host=resp_server.host, port=resp_server.port,
@@ -690,8 +692,9 @@ def test_gpu_node_comm_through_the_manager(resp_server):
            'QUEUES': 'predict', 'RESOURCE_NAME': 'worker', 'MAX_PODS': '1',
            'WORKER_BACKEND': 'hip', 'WARM_POOL': '1', 'FENCE': 'auto',
            'INTERVAL': '1', 'REDIS_INTERVAL': '0', 'GPU_IDS': '0',
-           'MODEL_DIM': '1024', 'MODEL_HIDDEN': '4096', 'MODEL_LAYERS': '2',
-           'ROWS_PER_KEY': '256'}
+           'MODEL': '1024x4096x2',
+           'ROWS_PER_KEY': '256',
+           'POOL_IDLE_RELEASE_S': '0'}
     s = Settings(Config(environ=env, use_files=False))
     client = StrictRedis(host=resp_server.host, port=resp_server.port,
                          decode_responses=True)
@@ -745,8 +748,9 @@ def test_gpu_context_pool_keeps_a_node_communicator(resp_server):
            'QUEUES': 'predict', 'RESOURCE_NAME': 'ctx', 'MAX_PODS': '1',
            'WORKER_BACKEND': 'hip', 'WARM_POOL': '1', 'FENCE': 'auto',
            'WARM_POOL_MODE': 'context', 'INTERVAL': '1',
-           'REDIS_INTERVAL': '0', 'GPU_IDS': '0', 'MODEL_DIM': '1024',
-           'MODEL_HIDDEN': '4096', 'MODEL_LAYERS': '2', 'ROWS_PER_KEY': '256'}
+           'REDIS_INTERVAL': '0', 'GPU_IDS': '0',
+           'MODEL': '1024x4096x2', 'ROWS_PER_KEY': '256',
+           'POOL_IDLE_RELEASE_S': '0'}
     s = Settings(Config(environ=env, use_files=False))
     client = StrictRedis(host=resp_server.host, port=resp_server.port,
                          decode_responses=True)
@@ -807,8 +811,9 @@ def test_gpu_failing_node_comm_never_blocks_serving(resp_server):
            'QUEUES': 'predict', 'RESOURCE_NAME': 'dup', 'MAX_PODS': '1',
            'WORKER_BACKEND': 'hip', 'WARM_POOL': '2', 'FENCE': 'auto',
            'INTERVAL': '1', 'REDIS_INTERVAL': '0', 'GPU_IDS': '0,0',
-           'MODEL_DIM': '1024', 'MODEL_HIDDEN': '4096', 'MODEL_LAYERS': '2',
-           'ROWS_PER_KEY': '256'}
+           'MODEL': '1024x4096x2',
+           'ROWS_PER_KEY': '256',
+           'POOL_IDLE_RELEASE_S': '0'}
     s = Settings(Config(environ=env, use_files=False))
     client = StrictRedis(host=resp_server.host, port=resp_server.port,
                          decode_responses=True)
@@ -935,7 +940,7 @@ def test_two_resources_share_the_node_communicator(resp_server):
     env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
            'QUEUES': 'qa', 'RESOURCE_NAME': 'a', 'MAX_PODS': '2',
            'WORKER_BACKEND': 'cpu', 'WARM_POOL': '2', 'FENCE': 'store',
-           'REDIS_INTERVAL': '0'}
+           'REDIS_INTERVAL': '0', 'POOL_IDLE_RELEASE_S': '0'}
     s = Settings(Config(environ=env, use_files=False))
     client = StrictRedis(host=resp_server.host, port=resp_server.port,
                          decode_responses=True)
@@ -953,10 +958,18 @@ def test_two_resources_share_the_node_communicator(resp_server):
             manager.patch_namespaced_deployment(name, 'default',
                                                 {'spec': {'replicas': 1}})
         for name in ('a', 'b'):
-            wait_for(lambda: (client.get('kiosk:active:default:%s' % name)
-                              and len(json.loads(client.get(
-                                  'kiosk:active:default:%s' % name))
-                                  ['members']) == 1), timeout=30)
+            try:
+                wait_for(lambda: (client.get('kiosk:active:default:%s' % name)
+                                  and len(json.loads(client.get(
+                                      'kiosk:active:default:%s' % name))
+                                      ['members']) == 1), timeout=30)
+            except AssertionError:
+                import pprint
+                with open('/tmp/two_debug.txt', 'w') as f:
+                    pprint.pprint(manager.status(), stream=f)
+                    for e in events.records:
+                        f.write('EV %r\n' % (e,))
+                raise
         members = [json.loads(client.get('kiosk:active:default:%s' % n))
                    ['members'][0] for n in ('a', 'b')]
         assert members[0].startswith('a-g') and members[1].startswith('b-g')
@@ -1163,8 +1176,8 @@ def test_gpu_shrink_and_regrow_with_real_workers(resp_server):
            'QUEUES': 'predict', 'RESOURCE_NAME': 'shr', 'MAX_PODS': '2',
            'WORKER_BACKEND': 'hip', 'WARM_POOL': '2', 'FENCE': 'auto',
            'WARM_POOL_MODE': 'context', 'REDIS_INTERVAL': '0',
-           'GPU_IDS': '0,0', 'MODEL_DIM': '1024', 'MODEL_HIDDEN': '4096',
-           'MODEL_LAYERS': '2', 'ROWS_PER_KEY': '256'}
+           'GPU_IDS': '0,0', 'MODEL': '1024x4096x2', 'ROWS_PER_KEY': '256',
+           'POOL_IDLE_RELEASE_S': '0'}
     s = Settings(Config(environ=env, use_files=False))
     client = StrictRedis(host=resp_server.host, port=resp_server.port,
                          decode_responses=True)

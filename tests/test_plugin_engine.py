@@ -105,7 +105,8 @@ def test_plugin_through_the_manager_with_recycling(resp_server):
            'QUEUES': 'predict', 'RESOURCE_NAME': 'plug', 'MAX_PODS': '1',
            'WORKER_BACKEND': 'cpu', 'WARM_POOL': '1', 'FENCE': 'none',
            'INTERVAL': '1', 'REDIS_INTERVAL': '0',
-           'EVENT_LOG': 'redis'}
+           'EVENT_LOG': 'redis',
+           'POOL_IDLE_RELEASE_S': '0'}
     os.environ['WORKER_ENGINE'] = REVERSE
     try:
         s = Settings(Config(environ=env, use_files=False))
@@ -145,7 +146,9 @@ def test_plugin_through_the_manager_with_recycling(resp_server):
     records = drain_redis(client)
     warm = [e for e in records if e['ev'] == 'warmstart']
     assert len(warm) == 2 and warm[0]['backend'] == 'cpu-example'
-    assert [e['reused'] for e in warm] == [False, True]
+    # device-mode standbys build their engine at boot (round 4): both
+    # assignments find it built
+    assert [e['reused'] for e in warm] == [True, True]
 
 
 @pytest.mark.gpu
@@ -161,7 +164,7 @@ def test_gpu_torch_engine_plugin_serves_on_mi355x(resp_server):
            'QUEUES': 'predict', 'RESOURCE_NAME': 'torchplug',
            'MAX_PODS': '1', 'WORKER_BACKEND': 'hip', 'WARM_POOL': '0',
            'FENCE': 'none', 'REDIS_INTERVAL': '0', 'GPU_IDS': '0',
-           'MODEL_DIM': '512', 'MODEL_HIDDEN': '2048', 'MODEL_LAYERS': '2',
+           'MODEL': '512x2048x2',
            'ROWS_PER_KEY': '64'}
     spec = 'kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine'
     os.environ['WORKER_ENGINE'] = spec
@@ -187,8 +190,7 @@ def test_gpu_torch_engine_plugin_serves_on_mi355x(resp_server):
         assert fields['engine'] == 'torch'
     finally:
         manager.stop(timeout=20)
-    cfg = rt.WorkerConfig({'MODEL_DIM': '512', 'MODEL_HIDDEN': '2048',
-                           'MODEL_LAYERS': '2', 'ROWS_PER_KEY': '64'},
+    cfg = rt.WorkerConfig({'MODEL': '512x2048x2', 'ROWS_PER_KEY': '64'},
                           {'worker_id': 'ref'})
     ref = TorchMlpEngine(cfg).reference(64, 7)
     want = float(ref.sum())
