@@ -21,6 +21,16 @@
 //
 // FAKE_RCCL_MODE (read at each call): ok | init_error | init_hang |
 // allreduce_hang | finalize_hang.
+//
+// The device hold measured on MI355X (profiles/r4_collision) is modelled
+// too: a process-wide "HIP runtime lock" that RCCL holds while its fat
+// binary registers -- the first ncclGetUniqueId of the process, for
+// FAKE_RCCL_LOAD_MS -- and while its code object loads -- the first
+// communicator's init, for FAKE_RCCL_INIT_MS, on RCCL's init thread (the
+// init stays ncclInProgress until then).  fake_hip_launch_kernel() takes
+// that lock like hipLaunchKernel does; fake_hip_graph_launch() does not,
+// like hipGraphLaunch.  The CPU mock engine launches through them, so an
+// 8-process CPU test sees exactly the collision a real worker would.
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
@@ -49,6 +59,7 @@ std::string mode() {
 struct FakeComm {
   std::unique_ptr<kiosk::ShmComm> shm;
   int polls_left = 3;        // ncclInProgress this many times, then settle
+  std::atomic<bool> loading{false};   // its code-object load holds the lock
   bool init_fails = false;
   bool init_hangs = false;
   bool finalize_hangs = false;
@@ -74,6 +85,23 @@ struct FakeStream {
 std::mutex g_mu;                       // streams, their queues, comm lifetime
 std::set<FakeStream*> g_streams;
 std::atomic<long> g_live_comms{0};
+
+// the modelled HIP runtime lock (see the file comment)
+std::mutex g_runtime_lock;
+std::once_flag g_load_once;
+std::atomic<bool> g_kernels_loaded{false};
+std::atomic<int> g_loading_comms{0};   // comms whose code-object load runs
+
+long env_ms(const char* name) {
+  const char* v = std::getenv(name);
+  return v ? std::atol(v) : 0;
+}
+
+void hold_runtime_lock(long ms) {
+  if (ms <= 0) return;
+  std::lock_guard<std::mutex> lock(g_runtime_lock);
+  std::this_thread::sleep_for(std::chrono::milliseconds(ms));
+}
 
 // Runs the stream's queue in order as far as it can (g_mu held).  An
 // all-reduce posts its send buffer when it reaches the front (stream
@@ -123,6 +151,13 @@ FakeComm* new_comm(std::unique_ptr<kiosk::ShmComm> shm) {
 }  // namespace
 
 FAKE_API long fake_rccl_live_comms() { return g_live_comms.load(); }
+
+// hipLaunchKernel: waits while RCCL holds the runtime lock
+FAKE_API void fake_hip_launch_kernel() {
+  std::lock_guard<std::mutex> lock(g_runtime_lock);
+}
+// hipGraphLaunch: never does
+FAKE_API void fake_hip_graph_launch() {}
 
 // ---- HIP (host memory stands in for HBM) ---------------------------------
 FAKE_API hipError_t hipStreamCreateWithFlags(hipStream_t* stream,
@@ -198,6 +233,9 @@ FAKE_API ncclResult_t ncclGetVersion(int* version) {
   return ncclSuccess;
 }
 FAKE_API ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
+  // the library's first use: its fat binary registers under the lock
+  std::call_once(g_load_once,
+                 [] { hold_runtime_lock(env_ms("FAKE_RCCL_LOAD_MS")); });
   const char* dir = std::getenv("FAKE_RCCL_DIR");
   const std::string path = kiosk::shm_unique_id(dir ? dir : "");
   std::memset(id->internal, 0, sizeof(id->internal));
@@ -215,8 +253,26 @@ FAKE_API ncclResult_t ncclCommInitRankConfig(ncclComm_t* comm, int nranks,
   } catch (const std::exception&) {
     return ncclInvalidArgument;
   }
-  std::lock_guard<std::mutex> lock(g_mu);
-  *comm = reinterpret_cast<ncclComm_t>(new_comm(std::move(shm)));
+  std::call_once(g_load_once,
+                 [] { hold_runtime_lock(env_ms("FAKE_RCCL_LOAD_MS")); });
+  FakeComm* c = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    c = new_comm(std::move(shm));
+  }
+  *comm = reinterpret_cast<ncclComm_t>(c);
+  const long load_ms = env_ms("FAKE_RCCL_INIT_MS");
+  if (load_ms > 0 && !g_kernels_loaded.exchange(true)) {
+    // the first communicator of the process loads RCCL's code object on
+    // RCCL's init thread, holding the runtime lock; the init settles after
+    c->loading = true;
+    g_loading_comms++;
+    std::thread([c, load_ms] {
+      hold_runtime_lock(load_ms);
+      c->loading = false;
+      g_loading_comms--;
+    }).detach();
+  }
   return ncclInProgress;
 }
 FAKE_API ncclResult_t ncclCommGetAsyncError(ncclComm_t comm,
@@ -225,7 +281,7 @@ FAKE_API ncclResult_t ncclCommGetAsyncError(ncclComm_t comm,
   std::lock_guard<std::mutex> lock(g_mu);
   if (c->finalizing) {
     *state = c->finalize_hangs ? ncclInProgress : ncclSuccess;
-  } else if (c->init_hangs) {
+  } else if (c->init_hangs || c->loading) {
     *state = ncclInProgress;
   } else if (c->polls_left > 0) {
     c->polls_left--;
@@ -239,6 +295,8 @@ FAKE_API ncclResult_t ncclCommGetAsyncError(ncclComm_t comm,
 }
 FAKE_API ncclResult_t ncclCommAbort(ncclComm_t comm) {
   auto* c = reinterpret_cast<FakeComm*>(comm);
+  // like RCCL, an abort waits for the init thread it interrupts
+  while (c->loading) std::this_thread::sleep_for(std::chrono::milliseconds(1));
   std::lock_guard<std::mutex> lock(g_mu);
   drop_ops_of(c);                  // what unblocks the real kernel
   g_live_comms--;
@@ -252,6 +310,7 @@ FAKE_API ncclResult_t ncclCommFinalize(ncclComm_t comm) {
 }
 FAKE_API ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   auto* c = reinterpret_cast<FakeComm*>(comm);
+  while (c->loading) std::this_thread::sleep_for(std::chrono::milliseconds(1));
   std::lock_guard<std::mutex> lock(g_mu);
   drop_ops_of(c);
   g_live_comms--;

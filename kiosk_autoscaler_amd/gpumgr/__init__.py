@@ -71,7 +71,8 @@ def worker_env(settings, keys_per_pod=None):
                         'KIOSK_RCCL_LIB', 'KIOSK_FAULTS', 'KIOSK_ROCTX',
                         'KIOSK_SHM_DIR', 'KIOSK_NATIVE', 'MOCK_WORK_MS',
                         'FAKE_RCCL_DIR', 'FAKE_RCCL_MODE',
-                        'FAKE_RCCL_INIT_MS', 'WORKER_MAX_RECYCLES',
+                        'FAKE_RCCL_INIT_MS', 'FAKE_RCCL_LOAD_MS',
+                        'WORKER_MAX_RECYCLES',
                         'WARM_START'):
         if passthrough in os.environ:
             env[passthrough] = os.environ[passthrough]

@@ -189,7 +189,15 @@ class NodeComm(object):
     def _usable(self, proc):
         return (proc is not None and getattr(proc, 'node_ok', False) and
                 not getattr(proc, 'node_quarantined', False) and
-                self._alive(proc))
+                not self._preloading(proc) and self._alive(proc))
+
+    def _preloading(self, proc):
+        """The rank is still paying RCCL's one-time load (its agent queues a
+        ``comm_init`` behind it anyway): a generation waits for it, up to
+        the first-generation budget."""
+        since = getattr(proc, 'node_preload_since', None)
+        return since is not None and \
+            time.monotonic() - since < self.first_init_timeout
 
     def candidates(self):
         """``[(slot, proc)]`` over every managed slot, or ``None`` while one
@@ -500,8 +508,15 @@ class NodeComm(object):
         kind = message.get('ev')
         if kind == 'node_agent':
             proc.node_ok = True
+            # (the agent thread may report its preload before the main
+            # thread announces the agent)
+            if message.get('preload') and \
+                    not getattr(proc, 'node_preloaded', False):
+                proc.node_preload_since = time.monotonic()
             return
         if kind == 'node_preloaded':
+            proc.node_preloaded = True
+            proc.node_preload_since = None
             proc.rccl_preload_ms = message.get('ms')
             self.m.events.emit('node_rank_preloaded', pid=proc.pid,
                                slot=getattr(proc, 'slot', None),

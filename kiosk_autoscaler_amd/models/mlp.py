@@ -51,6 +51,18 @@ def torch_reference(x, w1, b1, w2, b2, residual=True):
     return y
 
 
+def _fake_launcher():
+    """The fake-HIP module when the CPU stack runs over it, else None."""
+    from ..ops import native
+    if not native.fake_requested():
+        return None
+    try:
+        mod = native.load()
+    except native.NativeUnavailable:
+        return None
+    return mod if hasattr(mod, 'fake_launch_kernel') else None
+
+
 class CpuMlpEngine(object):
     """Mock CPU engine: real (tiny) math plus a configurable service time."""
 
@@ -75,10 +87,27 @@ class CpuMlpEngine(object):
         # an engine whose ``engine`` is set, as it does the HIP one's
         self.engine = self
         self.reused = False
+        # over the fake HIP + RCCL (KIOSK_NATIVE=fake) the mock launches
+        # like the HIP engine: kernel launches to build (weight init, graph
+        # capture), then graph launches (warm start after its first run,
+        # forwards) -- so RCCL's modelled runtime-lock holds reach it
+        self._fake = _fake_launcher()
+        self._warm_graph = False
+        for _ in range(2 * len(self.layers)):
+            self._launch(graph=False)
         if stage:
             stage('device_ready')
 
+    def _launch(self, graph):
+        if self._fake is not None:
+            if graph:
+                self._fake.fake_graph_launch()
+            else:
+                self._fake.fake_launch_kernel()
+
     def warmstart(self):
+        self._launch(graph=self._warm_graph)
+        self._warm_graph = True
         self.forward(8, 1, 0)
         return {'backend': 'cpu', 'cus_touched': 0}
 
@@ -95,6 +124,7 @@ class CpuMlpEngine(object):
     def forward(self, rows, passes, seed):
         import numpy as np
         t0 = time.perf_counter()
+        self._launch(graph=True)
         rng = np.random.default_rng(seed)
         x = rng.standard_normal((min(rows, 256), self.dim)).astype(np.float32)
         for _ in range(max(1, passes)):

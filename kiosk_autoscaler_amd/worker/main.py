@@ -414,10 +414,12 @@ def main(argv=None):
     if node:
         # a device-mode standby (HIP context open, launch handles resolved)
         # pays RCCL's one-time load on the agent thread right away
+        # (the CPU stack over the fake HIP + RCCL does the same)
+        fake = os.environ.get('KIOSK_NATIVE') == 'fake'
         node_agent = _start_node_agent(
             channel, backend, early.get('slot', 0),
-            preload=bool(preinit) and bool(pin) and
-            pin.get('preinit') == 'device' and not args.assign)
+            preload=bool(pin) and not args.assign and (
+                fake or (bool(preinit) and pin.get('preinit') == 'device')))
     assignment = parse_assignment(args.assign) if args.assign else None
     recycles = 0
     # forced retirement after N recycles (test hook; 0 = never): the soak
@@ -474,12 +476,15 @@ def _start_node_agent(channel, backend, slot, preload=False):
                                       choose_node_transport)
     transport = choose_node_transport(os.environ.get('FENCE', 'auto'),
                                       backend)
-    agent = NodeFenceAgent(slot, transport, channel=channel,
-                           preload=preload and transport.name == 'rccl')
+    preload = preload and transport.name == 'rccl'
+    agent = NodeFenceAgent(slot, transport, channel=channel, preload=preload)
     for cmd in NODE_COMMANDS:
         channel.direct[cmd] = agent.submit
     channel.start_reader()
-    channel.emit('node_agent', slot=slot, transport=transport.name)
+    # with ``preload`` the manager counts this rank in a generation once
+    # it reports ``node_preloaded``
+    channel.emit('node_agent', slot=slot, transport=transport.name,
+                 preload=preload)
     return agent
 
 

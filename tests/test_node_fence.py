@@ -1110,8 +1110,20 @@ def test_forced_recycle_exit_is_shrunk_not_broken(resp_server, tmp_path,
             wait_for(lambda: _active(client)['members'] == [], timeout=30)
             wait_for(lambda: not manager.status()['resources'][0]['workers'],
                      timeout=30)
-            wait_for(lambda: manager.node.ready and manager.node.full,
-                     timeout=60)
+            try:
+                wait_for(lambda: manager.node.ready and manager.node.full,
+                         timeout=60)
+            except AssertionError:
+                import pprint
+                with open('/tmp/fr_debug.txt', 'w') as f:
+                    pprint.pprint(manager.status(), stream=f)
+                    for p in list(manager.standbys.values()):
+                        f.write('STANDBY %s node_ok=%s since=%s\n' % (
+                            p.pid, getattr(p, 'node_ok', None),
+                            getattr(p, 'node_preload_since', None)))
+                    for e in events.records:
+                        f.write('EV %r\n' % (e,))
+                raise
     finally:
         manager.stop(timeout=15)
     kinds = [e['ev'] for e in events.records]
@@ -1367,3 +1379,83 @@ def test_frozen_serving_rank_is_quarantined_not_killed(resp_server, tmp_path,
     assert exit_['code'] == 0 and not exit_['killed'] and \
         not exit_['recycled']
     assert manager.node.quarantines == 1
+
+
+def test_fake_models_the_rccl_runtime_lock(tmp_path, monkeypatch):
+    """The fake reproduces what profiles/r4_collision measured: while the
+    first communicator's code object loads (FAKE_RCCL_INIT_MS) a kernel
+    launch waits, a graph launch does not."""
+    import subprocess
+    import sys
+    _ensure_native('rccl-fake')
+    code = r'''
+import os, threading, time, json
+os.environ['KIOSK_NATIVE'] = 'fake'
+from kiosk_autoscaler_amd.ops import native
+mod = native.load()
+done = threading.Event()
+def init():
+    uid = mod.fence_unique_id()
+    f = mod.Fence(uid, 1, 0, 30.0)
+    f.destroy()
+    done.set()
+threading.Thread(target=init).start()
+time.sleep(0.2)
+t0 = time.perf_counter(); mod.fake_graph_launch(); graph = time.perf_counter() - t0
+t0 = time.perf_counter(); mod.fake_launch_kernel(); kernel = time.perf_counter() - t0
+done.wait(30)
+print(json.dumps({'graph': graph, 'kernel': kernel}))
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FAKE_RCCL_INIT_MS='1000', FAKE_RCCL_DIR=str(tmp_path),
+               PYTHONPATH=root)
+    out = subprocess.run([sys.executable, '-c', code], env=env, timeout=60,
+                         stdout=subprocess.PIPE, text=True, check=True)
+    times = json.loads(out.stdout.strip().splitlines()[-1])
+    assert times['graph'] < 0.05
+    assert times['kernel'] > 0.5
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize('init_ms', [3000, 8000])
+def test_slow_rccl_inits_hold_up_no_scale_up(resp_server, tmp_path, init_ms):
+    """VERDICT r3 next-step 1/2, on CPU: eight ranks over the fake RCCL whose
+    first communicator holds the (modelled) HIP runtime lock for 3 s / 8 s
+    per process, and whose library load holds it 1 s.  A scale-up to all
+    eight slots lands while every rank is inside that init: no assignment
+    waits on it (READY is the prebuilt engine's warm-start graph), the
+    generation completes inside the first-generation budget, the node stays
+    on RCCL and the scale-up is fenced over it."""
+    s, client, events, manager, scaler = _node_stack(
+        resp_server, 'rccl-fake', tmp_path, QUEUES='predict',
+        extra={'FAKE_RCCL_INIT_MS': str(init_ms), 'FAKE_RCCL_LOAD_MS': '1000',
+               'MOCK_WORK_MS': '50'})
+    try:
+        # every rank paid its library load before the generation started
+        init = wait_for(lambda: [e for e in events.records
+                                 if e['ev'] == 'node_comm_init'], timeout=90)
+        assert init[0]['n'] == 8
+        loads = [e for e in events.records if e['ev'] == 'node_rank_preloaded']
+        assert len(loads) == 8 and all(e['t'] <= init[0]['t'] for e in loads)
+        time.sleep(0.3 + 0.1 * init_ms / 1000.0)   # inside every rank's init
+        assert manager.node.state == 'init'
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 8}})
+        ups = wait_for(lambda: (lambda u: u if len(u) == 8 else None)(
+            [e for e in events.records if e['ev'] == 'worker_up']),
+            timeout=60)
+        assert manager.node.state == 'init', 'the scale-up outlived the init'
+        slow = [e['ready_s'] for e in ups if e['ready_s'] > 0.5]
+        assert not slow, slow
+        wait_for(lambda: _converged(manager, client) and
+                 len(_ready_ids(manager)) == 8,
+                 timeout=60 + 2 * init_ms / 1000.0)
+    finally:
+        manager.stop(timeout=30)
+    kinds = [e['ev'] for e in events.records]
+    assert 'node_comm_fallback' not in kinds and 'node_rank_hung' not in kinds
+    ready = [e for e in events.records if e['ev'] == 'node_comm_ready']
+    assert ready and ready[0]['transport'] == 'rccl' and ready[0]['n'] == 8
+    assert ready[0]['init_ms'] >= init_ms * 0.9
+    done = [e for e in events.records if e['ev'] == 'fence_done']
+    assert done and all(e['transport'] == 'rccl' for e in done)
