@@ -798,6 +798,9 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         'fence_max_ranks': fence['fence_max_ranks'],
         'fence': {k: _r(v) for k, v in fence.items()
                   if k not in ('fence_transport', 'fence_max_ranks')},
+        # declared targets, multi-queue inflation, concurrent workers /
+        # booted standbys (config 3)
+        'decisions': summary['decisions'],
         'reference_sim_ideal_grid_latency_s': _r(ref_ideal['latency_mean_s']),
         'reference_pod_start_s': args.pod_start_s,
         'reference_sim_pod_start_latency_s': _r((ref_pod or {}).get(

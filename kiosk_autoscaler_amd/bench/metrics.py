@@ -322,6 +322,43 @@ def fence_stats(events):
     }
 
 
+def decision_stats(events):
+    """What the policy declared and what ran (config 3): the
+    largest target, the ticks whose target exceeded the keys they counted
+    (the reference's multi-queue inflation: each queue's clip substitutes
+    the current count), and the most READY workers / booted standbys at
+    once."""
+    ticks = [e for e in events if e.get('ev') == 'tick']
+    inflated = [e for e in ticks
+                if e.get('desired', 0) > sum((e.get('keys') or {}).values())
+                and e.get('desired', 0) > 0]
+    ready, standbys = set(), set()
+    max_ready = max_standbys = 0
+    for e in events:
+        ev = e.get('ev')
+        if ev == 'worker_up':
+            ready.add(e.get('worker'))
+        elif ev == 'worker_exit':
+            ready.discard(e.get('worker'))
+        elif ev == 'standby_ready':
+            standbys.add(e.get('pid'))
+        elif ev in ('worker_assigned', 'standby_exit'):
+            standbys.discard(e.get('pid'))
+        max_ready = max(max_ready, len(ready))
+        max_standbys = max(max_standbys, len(standbys))
+    example = None
+    if inflated:
+        first = max(inflated, key=lambda e: e.get('desired', 0))
+        example = {'keys': first.get('keys'), 'current': first.get('current'),
+                   'desired': first.get('desired')}
+    return {'ticks': len(ticks),
+            'desired_max': max((e.get('desired', 0) for e in ticks),
+                               default=None),
+            'inflated_ticks': len(inflated), 'inflation_example': example,
+            'max_ready_workers': max_ready,
+            'max_booted_standbys': max_standbys}
+
+
 def summarize(events, episodes):
     per = [episode_metrics(events, ep) for ep in episodes]
     lat = [v for p in per for v in p['cold_starts_s']]
@@ -351,5 +388,6 @@ def summarize(events, episodes):
         'keys': sum(p['keys'] for p in per),
         'keys_done': sum(p['keys_done'] for p in per),
         'fence': fence_stats(events),
+        'decisions': decision_stats(events),
         'episodes': per,
     }
