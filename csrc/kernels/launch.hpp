@@ -1,16 +1,18 @@
-// Kernel launches that never wait on the HIP runtime's fat-binary registry.
+// Kernel launches through handles resolved once.
 //
-// hipLaunchKernel(GGL) and hipFuncSetAttribute look a kernel's host stub up
-// in the runtime's fat-binary registry under one process-wide lock.  RCCL
-// holds that lock for ~1.1 s while its 573 MB fat binary registers (the
-// dlopen of librccl) and ~0.55 s while its code object loads onto the device
-// (the "kernels" phase of the first ncclCommInitRank).  Measured on MI355X
-// with the node communicator's first generation running on another thread
-// of a worker: a warm-start launch waited 1127 ms and an init-kernel launch
-// 546 ms, while hipGraphLaunch, hipMalloc and stream calls did not wait at
-// all (profiles/r4_collision).  So every kernel here is launched through a
-// hipFunction_t resolved once, at *_prepare time (hipGetFuncBySymbol), with
-// hipModuleLaunchKernel, which does not consult the registry.
+// Every kernel here is launched with hipModuleLaunchKernel on a
+// hipFunction_t looked up once, at *_prepare time (hipGetFuncBySymbol),
+// instead of hipLaunchKernel, which looks the host stub up in the runtime's
+// fat-binary registry on every launch.
+//
+// What this does NOT buy, measured on MI355X (profiles/r4_collision): while
+// RCCL registers its 573 MB fat binary (~1.1 s) or loads its code object
+// onto the device (~0.55 s, first communicator) on another thread of the
+// process, a kernel launch waits either way -- hipLaunchKernel 1127 / 546 ms,
+// hipModuleLaunchKernel 1045 / 539 ms.  Only hipGraphLaunch (and memory /
+// stream calls) did not wait.  So the worker's READY path is graph launches
+// only (the engine's warm-start graph, engine.cpp), and its engine is built
+// before the node agent first touches RCCL (worker/main.py).
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -26,6 +26,8 @@ void bind_comm(py::module_& m) {
         py::call_guard<py::gil_scoped_release>());
   m.def("fence_preload", &rccl_preload,
         py::call_guard<py::gil_scoped_release>());
+  m.def("fence_dlopen", &rccl_dlopen,
+        py::call_guard<py::gil_scoped_release>());
   m.def("fence_unique_id", [] {
     std::string id;
     {

@@ -125,6 +125,12 @@ std::string rccl_unique_id() {
   return std::string(id.internal, sizeof(id.internal));
 }
 
+double rccl_dlopen() {
+  const double t0 = now_s();
+  rccl();
+  return (now_s() - t0) * 1e3;
+}
+
 double rccl_preload() {
   const double t0 = now_s();
   rccl_version();

@@ -31,6 +31,10 @@ double rccl_warmup(double timeout_s);
 // library init of ncclGetUniqueId.  No communicator, no device memory.
 // Returns elapsed ms.
 double rccl_preload();
+// dlopen + symbol binding only -- no HIP call, no RCCL call: safe in a
+// process that never touches the GPU and forks (the worker zygote).
+// Returns elapsed ms.
+double rccl_dlopen();
 
 // A blocked collective given up on request_interrupt(): the communicator
 // is NOT aborted, so the survivors can still shrink it (a peer died).

@@ -161,7 +161,7 @@ EXTRA_DEFAULTS = (
     # node then holds no GPU, like the reference at zero replicas; a key's
     # arrival wakes the pool ahead of the scale-up tick (below); each wake
     # builds a new RCCL node communicator after the woken worker is READY
-    ('POOL_IDLE_RELEASE_S', float, 1.0),
+    ('POOL_IDLE_RELEASE_S', float, 0.05),
     # with POOL_IDLE_RELEASE_S: s between queue-length reads while no worker
     # runs; a new key refills a parked pool just before the scale-up tick
     # (the decision still waits for the tick; 0 = wake at the scale-up only)

@@ -467,10 +467,12 @@ class NodeFenceAgent(object):
         self._thread = threading.Thread(target=self._run, name='nodefence',
                                         daemon=True)
         if preload and hasattr(self.transport, 'preload'):
-            # RCCL's one-time load, first thing on the agent thread: it
-            # never waits on (nor stalls) the process's kernel launches
-            # (kernels/launch.hpp), and a first generation then connects in
-            # well under a second instead of paying it inside its timeout
+            # RCCL's one-time load, first thing on the agent thread.  It
+            # holds the HIP runtime lock every kernel launch of the process
+            # waits on (profiles/r4_collision); the standby built its engine
+            # before this agent started, so its READY is graph launches that
+            # never wait, and a first generation then connects without
+            # paying the load inside its timeout
             self._queue.put({'cmd': '_preload'})
         self._thread.start()
 
