@@ -248,7 +248,7 @@ class Services(object):
             init_timeout = float(os.environ.get('FENCE_INIT_TIMEOUT', 12.0))
             deadline = time.time() + max(30.0, 2 * init_timeout + 8.0)
             while time.time() < deadline and self.node_state() not in (
-                    'ready', 'off', None):
+                    'ready', 'off', None) and not self.parked():
                 time.sleep(0.1)
 
     def stop_scaler(self):
@@ -289,6 +289,13 @@ class Services(object):
             return True     # parked on purpose (POOL_IDLE_RELEASE_S)
         booted, _total = (int(v) for v in fields[:2])
         return booted >= self.pool
+
+    def parked(self):
+        """The pool parked on purpose (deep idle): no generation to wait
+        for until a key wakes it."""
+        value = self.redis.get('kiosk:pool')
+        fields = value.split() if value else []
+        return len(fields) > 3 and fields[3] == '1'
 
     def node_state(self):
         value = self.redis.get('kiosk:pool')

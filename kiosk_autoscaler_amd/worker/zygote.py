@@ -220,10 +220,23 @@ class ZygoteClient(object):
 # zygote process
 # ---------------------------------------------------------------------------
 def _preload(backend):
-    """Everything a worker imports, without a single HIP call."""
+    """Everything a worker imports, without a single HIP call -- RCCL
+    included: its dlopen registers its 573 MB fat binary, which in a process
+    with a HIP context holds the runtime for ~1.1 s (5 s on a cold page
+    cache) and here, before any HIP call, costs ~1 ms; every forked worker
+    inherits the registration (MI355X: the child's RCCL library init 5204 ->
+    26 ms, its HIP init unchanged, no thread in the zygote;
+    profiles/r4_defaults/zygote_probe.jsonl)."""
     from . import main as worker_main
     worker_main._preload(backend)           # native module (+ torch)
     worker_main._preimport(backend)         # runtime, events, models, plug-in
+    if backend == 'hip' and os.environ.get('FENCE', 'auto') not in (
+            'none', 'off', '0', 'shm', 'store', 'gloo'):
+        from ..ops import native
+        try:
+            native.load().fence_dlopen()
+        except Exception:  # pylint: disable=broad-except
+            pass    # no RCCL here: each worker's agent reports it
     from ..parallel import nodefence  # noqa: F401
     from ..redisq import RedisClient  # noqa: F401
     import logging  # noqa: F401

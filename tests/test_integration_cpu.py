@@ -30,7 +30,9 @@ def settings_for(server, **overrides):
     env = {'REDIS_HOST': server.host, 'REDIS_PORT': str(server.port),
            'QUEUES': 'predict', 'RESOURCE_NAME': 'worker',
            'MAX_PODS': '1', 'WORKER_BACKEND': 'cpu', 'WARM_POOL': '1',
-           'FENCE': 'store', 'INTERVAL': '1', 'REDIS_INTERVAL': '0'}
+           'FENCE': 'store', 'INTERVAL': '1', 'REDIS_INTERVAL': '0',
+           # a resident pool unless a test parks it (default: 0.05 s)
+           'POOL_IDLE_RELEASE_S': '0'}
     env.update({k: str(v) for k, v in overrides.items()})
     return Settings(Config(environ=env, use_files=False))
 
