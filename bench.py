@@ -214,7 +214,6 @@ class Services(object):
             'GPU_IDS': os.environ.get('BENCH_GPU_IDS') or
             ','.join(str(i) for i in range(n_gpus)),
             'WORKER_BACKEND': args.backend, 'WARM_POOL': str(pool),
-            'WARM_POOL_MODE': args.pool_mode,
             'WORKER_RECYCLE': '0' if args.no_recycle else '1',
             'FENCE': args.fence,
             'MODEL': '%dx%dx%d' % (args.dim, args.hidden, args.layers),
@@ -499,10 +498,6 @@ def parse_args():
                    help='opt-in fast poll while at zero workers (changes the '
                         "reference's INTERVAL semantics; reported separately)")
     p.add_argument('--resource-type', default='deployment')
-    p.add_argument('--pool-mode', default='device',
-                   help="standby preinit: 'device' (HIP context + code "
-                        "objects: fastest READY, holds the GPU) or 'import' "
-                        "(imports only: holds nothing)")
     p.add_argument('--no-recycle', action='store_true',
                    help='drained workers exit (a fresh standby replaces '
                         'them) instead of returning to the pool')
@@ -678,7 +673,7 @@ def base_line(args, episodes, elapsed):
             'max_pods': args.gpus, 'keys_per_pod': args.kpp,
             'policy': args.policy, 'resource_type': args.resource_type,
             'idle_interval_s': args.idle_interval,
-            'warm_pool_mode': args.pool_mode,
+            'warm_pool_mode': 'device',
             'worker_recycle': not args.no_recycle,
             # deep idle (standbys exit after this many idle seconds; 0 =
             # kept) and the arrival wake's queue-read period: the values

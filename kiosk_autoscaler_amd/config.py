@@ -138,7 +138,7 @@ REFERENCE_DEFAULTS = (
 )
 
 #: MI355X-native additions (SURVEY §5.6 "New knobs").  Round 4 pruned them
-#: from 39 to 25: merged spellings (``SCALE_POLICY``
+#: from 39 to 24: merged spellings (``SCALE_POLICY``
 #: carries the strict policy's delay, ``MODEL`` the three model sizes,
 #: ``FENCE_FALLBACK`` its threshold, ``METRICS_PORT`` its address,
 #: ``WORKER_TIMEOUT`` the start bound) and former knobs that became
@@ -153,10 +153,9 @@ EXTRA_DEFAULTS = (
     ('GPUMGR', str, 'embedded'),            # embedded | unix:<path> | k8s
     ('WORKER_MODULE', str, 'kiosk_autoscaler_amd.worker.main'),
     ('WORKER_BACKEND', str, 'auto'),        # auto | hip | cpu
-    ('WARM_POOL', int, -1),                 # standby processes (-1 = MAX_PODS)
-    # device (HIP context + code objects + queue + prebuilt engine) |
-    # context (HIP context only: no HBM)
-    ('WARM_POOL_MODE', str, 'device'),
+    # standby processes (-1 = MAX_PODS): HIP context, code objects, queue,
+    # prebuilt engine, RCCL node communicator
+    ('WARM_POOL', int, -1),
     # s with no demand after which the standbys exit (0 = keep them): the
     # node then holds no GPU, like the reference at zero replicas; a key's
     # arrival wakes the pool ahead of the scale-up tick (below); each wake
@@ -194,6 +193,9 @@ EXTRA_DEFAULTS = (
 #: attributes for the code that reads them.
 CONSTANTS = {
     'DEBUG': True,                 # the reference always logs at DEBUG
+    # standbys hold their GPU (context, queue, engine, RCCL); the context-
+    # only and import-only modes were dominated by deep idle (round 4)
+    'WARM_POOL_MODE': 'device',
     'STATE_TTL': 3600,             # s the persisted manager state lives
     'WARM_START': True,            # N1 always runs
     'WORKER_ZYGOTE': True,         # spawns fork from the pre-imported zygote

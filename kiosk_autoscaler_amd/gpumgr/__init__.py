@@ -111,9 +111,6 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
             per_key=settings.HBM_PER_KEY_BYTES)
     template = template_for(settings, backend, kpp)
     template.env.update(extra_env or {})
-    if settings.WARM_POOL_MODE not in ('device', 'context'):
-        raise ValueError('WARM_POOL_MODE must be device or context, got %r'
-                         % settings.WARM_POOL_MODE)
     pool = settings.WARM_POOL
     if pool < 0:
         pool = min(max(settings.MAX_PODS, 0), len(slots))

@@ -3,15 +3,13 @@
 Two start modes (both spawned by :mod:`kiosk_autoscaler_amd.gpumgr`):
 
 * **standby** (``--pin JSON``, no ``--assign``): pinned to its GPU before
-  anything loads, import the native kernel module (not PyTorch) and --
-  with ``WARM_POOL_MODE=device``, the default -- create the HIP context,
-  load every code object and size the LDS ring (``preinit_device``).  Such a
-  standby **holds its GPU** (context + code objects + a hardware queue,
-  ~1.3 GiB of HBM with the node communicator, no weights); the benchmark
-  reports that time as ``standby_gpu_s`` and the HBM as
-  ``standby_pool_boot_hbm_mib``.  ``WARM_POOL_MODE=context`` opens the HIP
-  context only (no queue, no RCCL: no HBM); ``import`` stops after the
-  imports and holds no GPU.
+  anything loads, import the native kernel module (not PyTorch), create the
+  HIP context, load every code object and size the LDS ring
+  (``preinit_device``), then build the engine (weights, forward and
+  warm-start graphs) before the node agent starts and pays RCCL's one-time
+  load.  Such a standby **holds its GPU** (the benchmark reports that time
+  as ``standby_gpu_s``); with deep idle (``POOL_IDLE_RELEASE_S``) only from
+  just before the tick that assigns it until just after its scale-down.
   Report ``standby`` and block on the command pipe.
 * **cold** (``--assign JSON``): start immediately.  The HIP context and
   the code objects are created on a helper thread (``preinit_device``
@@ -382,25 +380,6 @@ def main(argv=None):
         except Exception as err:  # pylint: disable=broad-except
             channel.emit('error', message='preinit failed: %s' % err)
             return 4
-    elif pin and pin.get('preinit') == 'context' and backend == 'hip':
-        # the HIP context alone: no hardware queue (the first kernel launch
-        # creates one, ~0.5 GiB of device-side state) and no RCCL, so this
-        # standby holds no HBM (profiles/r2_hbm_hold/).  CONTEXT_PRELOAD=1
-        # (opt-in) also loads the code objects without a launch: measured
-        # +314 MiB of HBM for -3 ms of actuation (profiles/r2_context_preload/),
-        # so by default the assignment pays queue, code objects and engine
-        from ..ops import native
-        try:
-            t0 = time.monotonic_ns()
-            mod = native.load()
-            mod.mem_info()
-            preinit = {'context_open': t0, 'context_done': time.monotonic_ns()}
-            if os.environ.get('CONTEXT_PRELOAD', '0') == '1':
-                preinit.update(mod.preload_modules(0))
-        except Exception as err:  # pylint: disable=broad-except
-            channel.emit('error', message='preinit failed: %s' % err)
-            return 4
-
     if pin is not None and not args.assign:
         _preimport(backend)
         _preconnect()

@@ -357,79 +357,6 @@ def test_gpu_cold_spawn_opens_the_device_in_parallel(resp_server):
         manager.stop()
 
 
-def test_pool_mode_is_validated():
-    from kiosk_autoscaler_amd.config import Config, Settings
-    env = {'RESOURCE_NAME': 'x', 'WORKER_BACKEND': 'cpu',
-           'WARM_POOL_MODE': 'devcie'}
-    with pytest.raises(ValueError, match='WARM_POOL_MODE'):
-        gpumgr.build_manager(Settings(Config(environ=env, use_files=False)))
-
-
-@pytest.mark.gpu
-def test_gpu_context_standby_holds_no_hbm_and_serves(resp_server):
-    """MI355X, ``WARM_POOL_MODE=context``: the standby opens its HIP context
-    (and measures free HBM through it) but creates no hardware queue and no
-    RCCL state, so the device's used VRAM does not move while it waits; an
-    assignment then builds the queue, code objects and engine and serves."""
-    import time
-    from kiosk_autoscaler_amd.bench import gpu_util
-    from kiosk_autoscaler_amd.config import Config, Settings
-    from kiosk_autoscaler_amd.redisq import StrictRedis
-    from kiosk_autoscaler_amd.utils.events import EventLog
-    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
-           'QUEUES': 'predict', 'RESOURCE_NAME': 'ctx', 'MAX_PODS': '1',
-           'WORKER_BACKEND': 'hip', 'WARM_POOL': '1',
-           'WARM_POOL_MODE': 'context', 'WORKER_RECYCLE': '0',
-           'FENCE': 'none', 'REDIS_INTERVAL': '0', 'GPU_IDS': '0',
-           'MODEL': '1024x4096x2',
-           'ROWS_PER_KEY': '256',
-           'POOL_IDLE_RELEASE_S': '0'}
-    s = Settings(Config(environ=env, use_files=False))
-    client = StrictRedis(host=resp_server.host, port=resp_server.port,
-                         decode_responses=True)
-    events = EventLog(source='test')
-    events.keep = True
-
-    def until(predicate, timeout):
-        deadline = time.monotonic() + timeout
-        while time.monotonic() < deadline:
-            value = predicate()
-            if value:
-                return value
-            time.sleep(0.02)
-        raise AssertionError('timed out')
-
-    def vram():
-        snap = gpu_util.vram_snapshot()
-        return max(snap.values()) if snap else None
-    before = vram()
-    manager = gpumgr.build_manager(s, redis_client=client,
-                                   events=events).start()
-    try:
-        booted = until(lambda: [e for e in events.records
-                                if e['ev'] == 'standby_ready'], 120)
-        assert 'context_done' in (booted[0].get('preinit') or {})
-        standby = list(manager.standbys.values())[0]
-        assert standby.hbm_free, 'free HBM measured through the context'
-        held = vram()
-        if before is not None and held is not None:
-            assert held - before < 64, (before, held)   # MiB: no queue
-        client.hset('predict:x0', mapping={'status': 'new', 'rows': 256})
-        client.lpush('predict', 'predict:x0')
-        manager.patch_namespaced_deployment(
-            'ctx', 'default', {'spec': {'replicas': 1}})
-        until(lambda: client.hget('predict:x0', 'status') == 'done', 120)
-        assigned = [e for e in events.records if e['ev'] == 'worker_assigned']
-        assert assigned and assigned[0]['from_pool']
-        manager.patch_namespaced_deployment(
-            'ctx', 'default', {'spec': {'replicas': 0}})
-        until(lambda: not [w for r in manager.resources.values()
-                           for w in r.workers.values()
-                           if w.state != 'exited'], 60)
-    finally:
-        manager.stop()
-
-
 def test_pool_parks_after_idle_and_refills_on_demand(resp_server):
     """``POOL_IDLE_RELEASE_S``: after that long without demand the standbys
     exit (the node holds no GPU, like the reference at zero replicas); the
@@ -812,14 +739,13 @@ def test_gpu_arrival_woken_standby_prebuilds(resp_server):
     ('device', 0.0, None),      # long-lived GPU standbys: RCCL (FENCE)
     ('device', 3.0, None),      # deep idle: RCCL too (VERDICT r3 missing 3)
     ('device', 600.0, None),
-    ('context', 0.0, 'shm'),    # standbys without a GPU queue / HBM
 ])
 def test_node_transport_follows_pool_mode(mode, park, expected):
     """The node communicator runs over RCCL wherever its ranks hold the GPU
     -- a pool that parks included: each wake's generation is built after
-    READY and its RCCL load stalls no launch of the worker (round 4) --
-    and over the native shared-memory transport where the standbys hold no
-    GPU queue."""
+    READY and its RCCL load stalls no launch of the worker (round 4; the
+    context-only pool mode, whose standbys held no GPU queue and fenced
+    over shared memory, is gone)."""
     slots = [gpus.GpuSlot(i, str(i)) for i in range(2)]
     tpl = gpumgr.WorkerTemplate(queues=['q'], backend='hip')
     manager = gpumgr.GpuManager(slots, pool_size=2, pool_template=tpl,
