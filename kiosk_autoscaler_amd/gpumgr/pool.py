@@ -462,6 +462,7 @@ class PoolMixin(object):
             self.events.emit('standby_prebuilt', pid=proc.pid, slot=proc.slot,
                              ms=message.get('ms'),
                              hbm_bytes=message.get('hbm_bytes'),
+                             stages=message.get('stages'),
                              error=message.get('error'))
             return
         if message.get('ev') == 'standby':

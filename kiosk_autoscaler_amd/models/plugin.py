@@ -80,6 +80,12 @@ class PluginEngine(object):
                              % (len(outputs), len(jobs)))
         return [dict(o or {}) for o in outputs], ms
 
+    def hbm_bytes(self):
+        """Device bytes the user engine holds (its ``hbm_bytes()``, if it
+        has one): what the standby reports as released / reusable."""
+        hook = getattr(self.user, 'hbm_bytes', None)
+        return int(hook()) if callable(hook) else 0
+
     def close(self):
         user, self.user = self.user, None
         self.engine = None

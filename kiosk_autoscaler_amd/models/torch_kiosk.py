@@ -36,6 +36,51 @@ from ..ops import native
 _WARM_ITERS = 4096
 
 
+_ALIGN = 256
+
+
+def _aligned(nbytes):
+    return (nbytes + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+def _nbytes(shape, dtype):
+    import torch
+    count = 1
+    for d in shape:
+        count *= int(d)
+    return count * torch.empty((), dtype=dtype).element_size()
+
+
+def _span(specs):
+    return sum(_aligned(_nbytes(shape, dtype)) for _, shape, dtype in specs)
+
+
+def _layer_bytes(dim, hidden):
+    """One layer's w1, b1, w2, b2 as :func:`ops.model_weights` lays them."""
+    import torch
+    return _span([('w1', (hidden, dim), torch.bfloat16),
+                  ('b1', (hidden,), torch.float32),
+                  ('w2', (dim, hidden), torch.bfloat16),
+                  ('b2', (dim,), torch.float32)])
+
+
+class _Carver(object):
+    """Hands out 256-B aligned typed views of one uint8 device tensor."""
+
+    def __init__(self, arena):
+        self.arena = arena
+        self.offset = 0
+
+    def __call__(self, shape, dtype):
+        n = _nbytes(shape, dtype)
+        if self.offset + n > self.arena.numel():
+            raise RuntimeError('arena overflow: %d + %d > %d'
+                               % (self.offset, n, self.arena.numel()))
+        view = self.arena[self.offset:self.offset + n].view(dtype)
+        self.offset += _aligned(n)
+        return view.view(tuple(int(d) for d in shape))
+
+
 class TorchKioskEngine(object):
     name = 'torch-kiosk'
 
@@ -61,33 +106,55 @@ class TorchKioskEngine(object):
         # LDS limits, code objects, launch handles: once, outside capture
         self.mod.prepare_kernels()
         self.stream = torch.cuda.Stream()
+        rows, dim, hidden = self.max_rows, self.dim, self.hidden
+        ws = max(self.mod.gemm_workspace_bytes(rows, hidden, dim),
+                 self.mod.gemm_workspace_bytes(rows, dim, hidden))
+        self.workspace_bytes = ws
+        f32, i32, i64 = torch.float32, torch.int32, torch.int64
+        bf16 = torch.bfloat16
+        # one device allocation for everything (as the built-in engine's
+        # arena): the small buffers that start zeroed first, so one fill
+        # clears them, then the weights and the activations
+        small = [('partials', (self.mod.sum_blocks,), f32),
+                 ('seed_dev', (1,), i64),
+                 ('warm_record', (self._cus() * 8,), i32)]
+        big = [('x', (rows, dim), bf16),          # input / ping
+               ('y', (rows, dim), bf16),          # pong
+               ('h', (rows, hidden), bf16),
+               ('workspace', (max(1, ws // 4),), f32)]
+        weight_bytes = _layer_bytes(dim, hidden) * self.layers
+        total = (_span(small) + weight_bytes + _span(big))
         with torch.cuda.stream(self.stream):
-            self.weights = ops.model_weights(self.dim, self.hidden,
-                                             self.layers, self.seed)
-            rows, dim, hidden = self.max_rows, self.dim, self.hidden
-            bf16 = dict(dtype=torch.bfloat16, device=self.device)
-            self.x = torch.empty((rows, dim), **bf16)    # input / ping
-            self.y = torch.empty((rows, dim), **bf16)    # pong
-            self.h = torch.empty((rows, hidden), **bf16)
-            self.partials = torch.zeros(self.mod.sum_blocks,
-                                        dtype=torch.float32,
-                                        device=self.device)
-            ws = max(self.mod.gemm_workspace_bytes(rows, hidden, dim),
-                     self.mod.gemm_workspace_bytes(rows, dim, hidden))
-            self.workspace = torch.empty(max(1, ws // 4), dtype=torch.float32,
-                                         device=self.device)
-            self.workspace_bytes = ws
-            self.seed_dev = torch.zeros(1, dtype=torch.int64,
-                                        device=self.device)
-            self.warm_record = torch.zeros(
-                (self._cus() * 8,), dtype=torch.int32, device=self.device)
-        self.seed_host = torch.zeros(1, dtype=torch.int64).pin_memory()
+            self.arena = torch.empty(total, dtype=torch.uint8,
+                                     device=self.device)
+            if stage:
+                stage('arena_allocated')
+            carve = _Carver(self.arena)
+            for name, shape, dtype in small:
+                setattr(self, name, carve(shape, dtype))
+            self.arena[:carve.offset].zero_()
+            self.weights = ops.model_weights(dim, hidden, self.layers,
+                                             self.seed, alloc=carve)
+            for name, shape, dtype in big:
+                setattr(self, name, carve(shape, dtype))
+        if stage:
+            stage('weights_enqueued')
+        self.seed_host = torch.zeros(1, dtype=i64).pin_memory()
+        # the forward's partial sums land here inside the graph: the key's
+        # checksum needs no torch kernel (a kernel launch would wait while
+        # RCCL loads on the node agent's thread; a graph launch does not)
+        self.partials_host = torch.zeros(self.mod.sum_blocks,
+                                         dtype=f32).pin_memory()
+        if stage:
+            stage('host_pinned')
         self.stream.synchronize()
         if stage:
             stage('weights_on_device')
         self.graphs = {}               # rows -> (CUDAGraph, output tensor)
         self.warm_graph = None
         self._capture(self.max_rows)
+        if stage:
+            stage('forward_captured')
         self._capture_warm()
         if stage:
             stage('graphs_ready')
@@ -124,29 +191,40 @@ class TorchKioskEngine(object):
         out = cur[:rows]
         mod.partial_sums(out.data_ptr(), out.numel(),
                          self.partials.data_ptr(), stream)
+        self.partials_host.copy_(self.partials, non_blocking=True)
         return out
 
+    def _record(self, enqueue):
+        """Capture ``enqueue()`` on the engine's stream.  Directly through
+        ``capture_begin``/``capture_end``: ``torch.cuda.graph`` would also
+        empty the caching allocator (nothing here allocates), and the
+        capture is thread-local (as the built-in engine's), so the node
+        agent's thread may call HIP meanwhile."""
+        graph = self.torch.cuda.CUDAGraph()
+        self.stream.synchronize()
+        with self.torch.cuda.stream(self.stream):
+            graph.capture_begin(capture_error_mode='thread_local')
+            try:
+                result = enqueue()
+            finally:
+                graph.capture_end()
+        return graph, result
+
     def _capture(self, rows):
-        torch = self.torch
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(self.stream):
-            with torch.cuda.graph(graph, stream=self.stream):
-                out = self._enqueue_forward(rows)
-        self.graphs[rows] = (graph, out)
+        self.graphs[rows] = self._record(lambda: self._enqueue_forward(rows))
         return self.graphs[rows]
 
     def _capture_warm(self):
-        torch = self.torch
         w1 = self.weights[0][0]
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(self.stream):
-            with torch.cuda.graph(graph, stream=self.stream):
-                self.warm_record.zero_()
-                self.mod.warmstart_raw(
-                    w1.data_ptr(), w1.numel(), self.warm_record.data_ptr(),
-                    self._cus(), _WARM_ITERS, self.mod.gemm_ring_lds_bytes,
-                    torch.cuda.current_stream().cuda_stream)
-        self.warm_graph = graph
+
+        def enqueue():
+            stream = self.torch.cuda.current_stream().cuda_stream
+            self.warm_record.zero_()
+            self.mod.warmstart_raw(
+                w1.data_ptr(), w1.numel(), self.warm_record.data_ptr(),
+                self._cus(), _WARM_ITERS, self.mod.gemm_ring_lds_bytes,
+                stream)
+        self.warm_graph = self._record(enqueue)[0]
 
     # -- plug-in contract ---------------------------------------------------
     def warmstart(self):
@@ -192,10 +270,19 @@ class TorchKioskEngine(object):
                     break
                 self.forward(rows, seed)
                 passes += 1
-            total = float(self.partials.double().sum().item())
-            out.append({'output_sum': '%.6e' % total, 'passes': passes,
-                        'engine': self.name})
+            out.append({'output_sum': '%.6e' % self.checksum(),
+                        'passes': passes, 'engine': self.name})
         return out
+
+    def checksum(self):
+        """The last forward's output sum: its per-block partials added in
+        block order in double, as the built-in engine does
+        (``Engine::forward``, ``csrc/runtime/engine.cpp``).  Call after the
+        stream is synchronised."""
+        total = 0.0
+        for value in self.partials_host.tolist():
+            total += value
+        return total
 
     def output(self, rows, seed):
         """The forward's ``[rows, dim]`` output as a fresh tensor (tests)."""
@@ -204,15 +291,14 @@ class TorchKioskEngine(object):
         return y.clone()
 
     def hbm_bytes(self):
-        return int(sum(t.numel() * t.element_size()
-                       for layer in self.weights for t in layer) +
-                   sum(t.numel() * t.element_size()
-                       for t in (self.x, self.y, self.h, self.workspace)))
+        return int(self.arena.numel()) if self.arena is not None else 0
 
     def close(self):
         self.graphs = {}
         self.warm_graph = None
         self.weights = None
         self.x = self.y = self.h = self.workspace = None
+        self.partials = self.seed_dev = self.warm_record = None
+        self.arena = None
         self.torch.cuda.synchronize()
         self.torch.cuda.empty_cache()

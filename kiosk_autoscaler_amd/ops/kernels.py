@@ -115,17 +115,22 @@ def checksum(t):
     return float(partials.double().sum().item())
 
 
-def model_weights(dim, hidden, layers, seed, device='cuda'):
-    """Regenerate the Engine's weights (same seeds and bounds) as tensors."""
+def model_weights(dim, hidden, layers, seed, device='cuda', alloc=None):
+    """Regenerate the Engine's weights (same seeds and bounds) as tensors.
+    ``alloc(shape, dtype)`` places them (e.g. in one arena); default
+    ``torch.empty`` on ``device``."""
     import torch
+    if alloc is None:
+        def alloc(shape, dtype):
+            return torch.empty(shape, dtype=dtype, device=device)
     bd, bh = 1.0 / math.sqrt(dim), 1.0 / math.sqrt(hidden)
     weights = []
     for layer in range(layers):
         s = seed * 1000003 + 16 * layer
-        w1 = torch.empty((hidden, dim), dtype=torch.bfloat16, device=device)
-        b1 = torch.empty(hidden, dtype=torch.float32, device=device)
-        w2 = torch.empty((dim, hidden), dtype=torch.bfloat16, device=device)
-        b2 = torch.empty(dim, dtype=torch.float32, device=device)
+        w1 = alloc((hidden, dim), torch.bfloat16)
+        b1 = alloc((hidden,), torch.float32)
+        w2 = alloc((dim, hidden), torch.bfloat16)
+        b2 = alloc((dim,), torch.float32)
         init_uniform_(w1, s + 1, -bd, bd)
         init_uniform_(b1, s + 2, -bd, bd)
         init_uniform_(w2, s + 3, -bh, bh)

@@ -226,6 +226,10 @@ def _prebuild_engine(backend, pin, channel):
     from .runtime import WorkerConfig
     spec = pin.get('prebuild') or {}
     t0 = time.monotonic_ns()
+    stages = {}
+
+    def stage(name, t=None):
+        stages[name] = round(((t or time.monotonic_ns()) - t0) / 1e6, 3)
     try:
         template = {}
         if spec.get('keys_per_pod'):
@@ -234,12 +238,13 @@ def _prebuild_engine(backend, pin, channel):
             'worker_id': 'standby', 'kind': spec.get('kind', 'deployment'),
             'slot': pin.get('slot', 0), 'gpu': pin.get('gpu', ''),
             'template': template})
-        engine = _cached_engine(backend, cfg, None)
+        engine = _cached_engine(backend, cfg, stage)
+        stage('engine_built')
         if os.environ.get('WARM_START', '1').lower() not in (
                 '0', 'false', 'no', 'off'):
             engine.warmstart()
         channel.emit('prebuilt', ms=(time.monotonic_ns() - t0) / 1e6,
-                     hbm_bytes=_cached_engine_bytes())
+                     hbm_bytes=_cached_engine_bytes(), stages=stages)
     except Exception as err:  # pylint: disable=broad-except
         _drop_cached_engines()
         channel.emit('prebuilt', ms=(time.monotonic_ns() - t0) / 1e6,

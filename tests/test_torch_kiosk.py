@@ -70,9 +70,14 @@ def test_bit_identical_to_the_native_engine(cuda):
     native_engine = mod.Engine(0, dim, hidden, layers, rows, 21)
     try:
         ours = engine.output(rows, 9)
-        native_engine.forward(rows, 1, 9)
+        result = native_engine.forward(rows, 1, 9)
         theirs = kernels.engine_output(native_engine, rows)
         assert torch.equal(ours, theirs)
+        # the key's checksum: the same partials summed in the same order,
+        # without a torch kernel on the serving path
+        assert engine.checksum() == result['checksum']
+        served = engine.infer([{'rows': rows, 'seed': 9, 'service_ms': 0}])
+        assert served[0]['output_sum'] == '%.6e' % result['checksum']
     finally:
         native_engine.close()
         engine.close()
