@@ -26,6 +26,80 @@ hipStream_t stream_of(unsigned long long s) {
   return reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(s));
 }
 
+// DLPack (the legacy, unversioned ABI every torch build reads): a device
+// buffer of ours handed to torch without a copy.  Only the structs the
+// exchange needs; the layout is DLPack's.
+struct DLDevice { int32_t device_type; int32_t device_id; };
+struct DLDataType { uint8_t code; uint8_t bits; uint16_t lanes; };
+struct DLTensor {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor*);
+};
+constexpr int32_t kDLROCM = 10;
+constexpr uint8_t kDLUInt = 1;
+
+struct DeviceBuffer {
+  DLManagedTensor managed{};
+  int64_t shape[1] = {0};
+  int64_t strides[1] = {1};
+};
+
+void free_device_buffer(DLManagedTensor* t) {
+  auto* buf = static_cast<DeviceBuffer*>(t->manager_ctx);
+  if (buf->managed.dl_tensor.data) hipFree(buf->managed.dl_tensor.data);
+  delete buf;
+}
+
+// `nbytes` of device memory from hipMalloc as a uint8 DLPack capsule:
+// torch.utils.dlpack.from_dlpack() makes it a tensor that frees it when
+// the last view dies.  A PyTorch engine's arena comes from here because
+// the caching allocator's first segment of a size this large took ~110 ms
+// (profiles/r4_boot) against well under 1 ms for hipMalloc itself.
+py::capsule device_buffer(size_t nbytes, int device) {
+  auto* buf = new DeviceBuffer();
+  void* data = nullptr;
+  hipError_t err;
+  {
+    py::gil_scoped_release release;
+    err = hipSetDevice(device);
+    if (err == hipSuccess) err = hipMalloc(&data, nbytes);
+  }
+  if (err != hipSuccess) {
+    delete buf;
+    check_hip(err, "hipMalloc(device_buffer)");
+  }
+  buf->shape[0] = static_cast<int64_t>(nbytes);
+  DLTensor& t = buf->managed.dl_tensor;
+  t.data = data;
+  t.device = {kDLROCM, device};
+  t.ndim = 1;
+  t.dtype = {kDLUInt, 8, 1};
+  t.shape = buf->shape;
+  t.strides = buf->strides;
+  t.byte_offset = 0;
+  buf->managed.manager_ctx = buf;
+  buf->managed.deleter = free_device_buffer;
+  // a capsule nobody consumed (renamed "used_dltensor" once torch took
+  // ownership) frees the buffer itself
+  return py::capsule(&buf->managed, "dltensor", [](PyObject* cap) {
+    if (PyCapsule_IsValid(cap, "dltensor")) {
+      auto* m = static_cast<DLManagedTensor*>(
+          PyCapsule_GetPointer(cap, "dltensor"));
+      if (m && m->deleter) m->deleter(m);
+    }
+  });
+}
+
 py::dict warm_to_dict(const kiosk::WarmStartResult& r) {
   py::dict d;
   d["blocks"] = r.blocks;
@@ -181,6 +255,10 @@ PYBIND11_MODULE(_kiosk_hip, m) {
       py::arg("device") = 0);
   m.def("release_kept_stream", &kiosk::release_kept_stream,
         py::call_guard<py::gil_scoped_release>());
+  // the stream preinit_device warmed (its hardware queue already set up)
+  m.def("take_stream", &kiosk::take_stream, py::arg("device") = 0);
+  m.def("return_stream", &kiosk::return_stream, py::arg("handle"),
+        py::arg("device") = 0, py::call_guard<py::gil_scoped_release>());
   m.def(
       "preload_modules",
       [](int device) {
@@ -217,6 +295,20 @@ PYBIND11_MODULE(_kiosk_hip, m) {
                     "hipDeviceGetPCIBusId");
         }
         return std::string(buf);
+      },
+      py::arg("device") = 0);
+  m.def("device_buffer", &device_buffer, py::arg("nbytes"),
+        py::arg("device") = 0);
+  // compute units of a device: one attribute query (torch's
+  // get_device_properties fills every property first, ~0.1 s on MI355X)
+  m.def(
+      "device_cus",
+      [](int device) {
+        int cus = 0;
+        check_hip(hipDeviceGetAttribute(
+                      &cus, hipDeviceAttributeMultiprocessorCount, device),
+                  "hipDeviceGetAttribute");
+        return cus;
       },
       py::arg("device") = 0);
   m.def("synchronize", [] { check_hip(hipDeviceSynchronize(), "sync"); },

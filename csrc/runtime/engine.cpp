@@ -74,6 +74,16 @@ void keep_stream(hipStream_t s, int device) {
 }
 }  // namespace
 
+unsigned long long take_stream(int device) {
+  return static_cast<unsigned long long>(
+      reinterpret_cast<uintptr_t>(take_kept_stream(device)));
+}
+
+void return_stream(unsigned long long handle, int device) {
+  keep_stream(reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(handle)),
+              device);
+}
+
 void release_kept_stream() {
   hipStream_t s = nullptr;
   int device = -1;
@@ -99,11 +109,13 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   check_hip(gemm_prepare(), "gemm_prepare");
   check_hip(misc_prepare(), "misc_prepare");
   check_hip(warmstart_prepare(), "warmstart_prepare");
+  stages.emplace_back("preinit_prepared", monotonic_ns());
   hipStream_t stream = take_kept_stream(device);
   if (!stream) {
     check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking),
               "hipStreamCreate");
   }
+  stages.emplace_back("preinit_stream", monotonic_ns());
   // 128x128 operands + bias + output + sums + warm-start record
   const size_t elems = 128 * 128;
   char* scratch = nullptr;
@@ -125,6 +137,8 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
             "preinit init");
   check_hip(launch_init_uniform_f32(bias, 128, 2, -1.f, 1.f, stream),
             "preinit init f32");
+  check_hip(hipStreamSynchronize(stream), "preinit first sync");
+  stages.emplace_back("preinit_first_launch", monotonic_ns());
   for (int epi = 0; epi < 3; ++epi) {
     check_hip(launch_gemm(a, b, c, bias, r, 128, 128, 128, epi, stream),
               "preinit gemm");

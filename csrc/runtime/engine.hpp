@@ -24,6 +24,11 @@ long long monotonic_ns();
 // took it): the standby's exit path, so teardown does not depend on process
 // exit.
 void release_kept_stream();
+// The kept stream for a caller outside Engine (the PyTorch engine wraps it
+// in torch.cuda.ExternalStream): 0 if none is kept for `device`.  The
+// caller owns it until it hands it back with return_stream.
+unsigned long long take_stream(int device);
+void return_stream(unsigned long long handle, int device);
 std::vector<std::pair<std::string, long long>> preinit_device(int device);
 // `context` standby: HIP context + every kernel's code object, no launch (so
 // no hardware queue and no HBM beyond the code objects).

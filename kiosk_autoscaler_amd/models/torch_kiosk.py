@@ -105,7 +105,20 @@ class TorchKioskEngine(object):
         self.seed = int(cfg.seed)
         # LDS limits, code objects, launch handles: once, outside capture
         self.mod.prepare_kernels()
-        self.stream = torch.cuda.Stream()
+        if stage:
+            stage('kernels_prepared')
+        # the stream the standby's preinit_device warmed: a new stream's
+        # first launch sets up a hardware queue (~0.1 s on MI355X,
+        # profiles/r4_boot); handed back on close for the next engine
+        self._device_index = torch.cuda.current_device()
+        self._stream_handle = self.mod.take_stream(self._device_index)
+        if self._stream_handle:
+            self.stream = torch.cuda.ExternalStream(self._stream_handle,
+                                                    device=self.device)
+        else:
+            self.stream = torch.cuda.Stream()
+        if stage:
+            stage('stream_ready')
         rows, dim, hidden = self.max_rows, self.dim, self.hidden
         ws = max(self.mod.gemm_workspace_bytes(rows, hidden, dim),
                  self.mod.gemm_workspace_bytes(rows, dim, hidden))
@@ -124,9 +137,16 @@ class TorchKioskEngine(object):
                ('workspace', (max(1, ws // 4),), f32)]
         weight_bytes = _layer_bytes(dim, hidden) * self.layers
         total = (_span(small) + weight_bytes + _span(big))
+        if stage:
+            stage('sized')
         with torch.cuda.stream(self.stream):
-            self.arena = torch.empty(total, dtype=torch.uint8,
-                                     device=self.device)
+            # hipMalloc'ed by the native module and handed over by DLPack:
+            # the caching allocator's first segment this large took ~110 ms
+            # of a ~0.3 s standby boot (profiles/r4_boot); the tensor frees
+            # the buffer when its last view dies
+            from torch.utils.dlpack import from_dlpack
+            self.arena = from_dlpack(self.mod.device_buffer(
+                total, torch.cuda.current_device()))
             if stage:
                 stage('arena_allocated')
             carve = _Carver(self.arena)
@@ -161,8 +181,11 @@ class TorchKioskEngine(object):
 
     # -- construction -----------------------------------------------------
     def _cus(self):
-        props = self.torch.cuda.get_device_properties(self.device)
-        return int(props.multi_processor_count)
+        # one attribute query: torch's get_device_properties costs ~0.1 s
+        # on its first call (profiles/r4_boot)
+        if not hasattr(self, '_cu_count'):
+            self._cu_count = int(self.mod.device_cus(self._device_index))
+        return self._cu_count
 
     def _enqueue_forward(self, rows):
         """The forward on the current stream (captured, never run eagerly
@@ -294,6 +317,10 @@ class TorchKioskEngine(object):
         return int(self.arena.numel()) if self.arena is not None else 0
 
     def close(self):
+        if self.stream is None:
+            return
+        # nothing of ours may still run when the arena's hipFree comes
+        self.stream.synchronize()
         self.graphs = {}
         self.warm_graph = None
         self.weights = None
@@ -302,3 +329,7 @@ class TorchKioskEngine(object):
         self.arena = None
         self.torch.cuda.synchronize()
         self.torch.cuda.empty_cache()
+        if self._stream_handle:
+            self.mod.return_stream(self._stream_handle, self._device_index)
+            self._stream_handle = 0
+        self.stream = None

@@ -103,6 +103,40 @@ def test_warmstart_and_forward_are_graph_launches(cuda):
         engine.close()
 
 
+def test_engine_reuses_the_preinit_stream_and_a_dlpack_arena(cuda):
+    """Standby boot path: the engine wraps the stream preinit_device warmed
+    (no new hardware queue) and hands it back on close; its arena is one
+    hipMalloc handed over by DLPack and freed with the engine."""
+    from kiosk_autoscaler_amd.models.torch_kiosk import TorchKioskEngine
+    from kiosk_autoscaler_amd.ops import native
+    mod = native.load()
+    mod.preinit_device(0)
+    free0 = mod.mem_info()[0]
+    stages = {}
+    engine = TorchKioskEngine(_cfg(1024, 4096, 2, 512),
+                              lambda name: stages.setdefault(name, 1))
+    handle = engine._stream_handle
+    try:
+        assert handle and engine.stream.cuda_stream == handle
+        assert {'stream_ready', 'arena_allocated', 'graphs_ready'} <= set(
+            stages)
+        assert engine.hbm_bytes() == engine.arena.numel()
+        assert free0 - mod.mem_info()[0] >= engine.hbm_bytes()
+        engine.warmstart()
+        out = engine.infer([{'rows': 512, 'seed': 4, 'service_ms': 0}])
+        assert out[0]['passes'] == 1
+    finally:
+        engine.close()
+    engine.close()                       # idempotent
+    torch.cuda.synchronize()
+    # the arena is freed (up to the allocator's rounding) ...
+    assert mod.mem_info()[0] > free0 - (64 << 20)
+    # ... and the stream is kept again for the next engine
+    again = mod.take_stream(0)
+    assert again == handle
+    mod.return_stream(again, 0)
+
+
 def test_torch_worker_serves_keys_through_the_manager(resp_server):
     """A real PyTorch-ROCm worker process (zygote-forked, torch imported,
     native kernels on torch's allocator and stream) scales up, serves keys

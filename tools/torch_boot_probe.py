@@ -21,9 +21,15 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(use_torch, model):
+def child(use_torch, model, rocm_runtime=False):
     t_start = time.perf_counter()
-    row = {'torch': use_torch}
+    row = {'torch': use_torch, 'rocm_runtime': rocm_runtime}
+    if rocm_runtime:
+        # the image's HIP / HSA runtime (same SONAMEs as torch's bundled
+        # copies, which the loader then never opens)
+        import ctypes
+        for lib in ('libhsa-runtime64.so.1', 'libamdhip64.so.7'):
+            ctypes.CDLL('/opt/rocm/lib/' + lib, mode=ctypes.RTLD_GLOBAL)
 
     def mark(name):
         row[name] = round((time.perf_counter() - t_start) * 1e3, 2)
@@ -62,21 +68,28 @@ def child(use_torch, model):
     t0 = time.perf_counter()
     engine.warmstart()
     row['ready_ms'] = round((time.perf_counter() - t0) * 1e3, 3)
+    if use_torch:
+        import torch
+        a = torch.randn(512, 512, device='cuda', dtype=torch.bfloat16)
+        row['torch_matmul_ok'] = bool(torch.isfinite((a @ a).float()).all())
+        with open('/proc/self/maps') as maps:
+            row['hip_runtime'] = sorted({line.split()[-1] for line in maps
+                                         if 'libamdhip64' in line})
     engine.close()
     print(json.dumps(row), flush=True)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--child', choices=('torch', 'native'))
+    ap.add_argument('--child', choices=('torch', 'native', 'torch72'))
     ap.add_argument('--repeat', type=int, default=3)
     ap.add_argument('--model', default='4096x16384x4')
     args = ap.parse_args()
     if args.child:
-        child(args.child == 'torch', args.model)
+        child(args.child != 'native', args.model, args.child == 'torch72')
         return 0
     for _ in range(args.repeat):
-        for kind in ('native', 'torch'):
+        for kind in ('native', 'torch', 'torch72'):
             out = subprocess.run(
                 [sys.executable, os.path.abspath(__file__), '--child', kind,
                  '--model', args.model],
