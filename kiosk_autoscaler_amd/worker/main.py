@@ -45,6 +45,18 @@ def _die_with_parent():
         pass
 
 
+def _stack_dump_on_sigusr1():
+    """``kill -USR1 <pid>`` prints every thread's Python stack to the
+    worker's stderr (the manager's log): how a worker stuck in a state is
+    diagnosed without a debugger."""
+    try:
+        import faulthandler
+        import signal
+        faulthandler.register(signal.SIGUSR1, all_threads=True)
+    except (ImportError, AttributeError, RuntimeError, ValueError):
+        pass
+
+
 def _preload(backend):
     """Import everything heavy *without* touching the GPU.  The HIP worker
     needs only the native module (engine, fence): no torch import unless
@@ -334,6 +346,7 @@ def main(argv=None):
     if args.standalone:
         return _standalone(args.backend)
     _die_with_parent()
+    _stack_dump_on_sigusr1()
     # ordered for the cold spawn: pin, load the native module and start
     # opening the device first; logging, the channel and the runtime
     # modules load while the helper thread creates the HIP context

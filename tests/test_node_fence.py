@@ -909,10 +909,20 @@ def test_two_resources_share_the_node_communicator(resp_server):
                                       ['members']) == 1), timeout=30)
             except AssertionError:
                 import pprint
+                status = manager.status()
                 with open('/tmp/two_debug.txt', 'w') as f:
-                    pprint.pprint(manager.status(), stream=f)
+                    pprint.pprint(status, stream=f)
                     for e in events.records:
                         f.write('EV %r\n' % (e,))
+                # stacks of workers stuck before READY, on their stderr
+                for res in status['resources']:
+                    for w in res['workers']:
+                        if w['state'] == 'starting' and w.get('pid'):
+                            try:
+                                os.kill(w['pid'], signal.SIGUSR1)
+                            except OSError:
+                                pass
+                time.sleep(0.5)
                 raise
         members = [json.loads(client.get('kiosk:active:default:%s' % n))
                    ['members'][0] for n in ('a', 'b')]
