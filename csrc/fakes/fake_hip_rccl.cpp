@@ -45,6 +45,8 @@
 #include <string>
 #include <thread>
 
+#include <unistd.h>
+
 #include "runtime/shmcomm.hpp"
 
 #define FAKE_API extern "C" __attribute__((visibility("default")))
@@ -141,7 +143,13 @@ FakeComm* new_comm(std::unique_ptr<kiosk::ShmComm> shm) {
   auto* c = new FakeComm();
   c->shm = std::move(shm);
   const std::string m = mode();
-  c->init_fails = m == "init_error";
+  // init_error_while:<path>: inits fail while that file exists (a test
+  // lets RCCL recover after the node fell back to shared memory)
+  static const std::string kWhile = "init_error_while:";
+  c->init_fails =
+      m == "init_error" ||
+      (m.compare(0, kWhile.size(), kWhile) == 0 &&
+       access(m.c_str() + kWhile.size(), F_OK) == 0);
   c->init_hangs = m == "init_hang";
   c->finalize_hangs = m == "finalize_hang";
   g_live_comms++;

@@ -434,6 +434,9 @@ class NodeFenceAgent(object):
                  uid_timeout=None, transport_factory=None, preload=False):
         self.slot = int(slot)
         self.transport = transport
+        # the configured transport: a generation that names none (the RCCL
+        # retry after a fallback, gpumgr/nodecomm.py) goes back to it
+        self.home_transport = transport
         # kind -> transport, for a manager-requested switch (the fallback
         # after failed RCCL generations, gpumgr/nodecomm.py)
         self.transport_factory = transport_factory or (
@@ -552,7 +555,10 @@ class NodeFenceAgent(object):
         timeout = float(message.get('timeout') or 0.0) or None
         self._drop()
         wanted = message.get('transport')
-        if wanted and wanted != self.transport.name:
+        if not wanted:
+            # no override: the configured transport, also after a fallback
+            self.transport = self.home_transport
+        elif wanted != self.transport.name:
             try:
                 self.transport = self.transport_factory(wanted)
             except Exception as err:  # pylint: disable=broad-except

@@ -247,6 +247,13 @@ def test_agent_switches_transport_when_the_manager_asks():
     assert ready['ok'] and ready['transport'] == 'store'
     assert ('connect', 3, 0, 2, 'u3') in made
     assert not any(c[0] == 'connect' for c in native.calls)  # RCCL unused
+    # the RCCL retry after a fallback names no transport: the agent goes
+    # back to its configured one (it stayed on the fallback before)
+    agent.submit({'cmd': 'comm_init', 'gen': 4, 'rank': 0, 'nranks': 1})
+    ready = chan.next('comm_ready')
+    assert ready['transport'] == 'rccl' and agent.transport is \
+        agent.home_transport
+    assert any(c[0] == 'connect' for c in native.calls)
     assert agent.close()
 
 
@@ -989,6 +996,43 @@ def test_hung_rccl_init_at_eight_ranks_falls_back(resp_server, tmp_path):
     done = [e for e in events.records if e['ev'] == 'fence_done']
     assert done and all(e['transport'] == 'shm' and e['n'] == 8
                         for e in done)
+
+
+@pytest.mark.slow
+def test_rccl_is_retried_after_the_fallback(resp_server, tmp_path):
+    """VERDICT r3 missing 3: after two failed RCCL generations the node
+    runs on shared memory, and once it is idle it tries RCCL again -- with
+    the same processes, which must then leave the fallback transport (the
+    agents used to stay on it when the retry named no transport)."""
+    fail = tmp_path / 'rccl_fails'
+    fail.write_text('1')
+    s, client, events, manager, scaler = _node_stack(
+        resp_server, 'rccl-fake', tmp_path,
+        extra={'FAKE_RCCL_MODE': 'init_error_while:%s' % fail},
+        node={'rccl_retry_s': 1.0, 'first_init_timeout': 5.0})
+    try:
+        wait_for(lambda: [e for e in events.records
+                          if e['ev'] == 'node_comm_fallback'], timeout=60)
+        wait_for(lambda: manager.node.ready and
+                 manager.node.transport == 'shm', timeout=30)
+        pids = sorted(p.pid for _, p in manager.node.members)
+        fail.unlink()                  # RCCL works again
+        retry = wait_for(lambda: [e for e in events.records
+                                  if e['ev'] == 'node_comm_retry'],
+                         timeout=30)[0]
+        wait_for(lambda: manager.node.ready and manager.node.gen > retry[
+            'gen'] - 1 and manager.node.transport == 'rccl', timeout=30)
+        assert sorted(p.pid for _, p in manager.node.members) == pids
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 1}})
+        wait_for(lambda: _converged(manager, client) and
+                 len(_ready_ids(manager)) == 1, timeout=30)
+    finally:
+        manager.stop(timeout=15)
+    readies = [e for e in events.records if e['ev'] == 'node_comm_ready']
+    assert readies[-1]['transport'] == 'rccl'
+    done = [e for e in events.records if e['ev'] == 'fence_done']
+    assert done and done[-1]['transport'] == 'rccl'
 
 
 @pytest.mark.slow
