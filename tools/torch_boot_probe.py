@@ -21,15 +21,9 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(use_torch, model, rocm_runtime=False):
+def child(use_torch, model):
     t_start = time.perf_counter()
-    row = {'torch': use_torch, 'rocm_runtime': rocm_runtime}
-    if rocm_runtime:
-        # the image's HIP / HSA runtime (same SONAMEs as torch's bundled
-        # copies, which the loader then never opens)
-        import ctypes
-        for lib in ('libhsa-runtime64.so.1', 'libamdhip64.so.7'):
-            ctypes.CDLL('/opt/rocm/lib/' + lib, mode=ctypes.RTLD_GLOBAL)
+    row = {'torch': use_torch}
 
     def mark(name):
         row[name] = round((time.perf_counter() - t_start) * 1e3, 2)
@@ -81,15 +75,15 @@ def child(use_torch, model, rocm_runtime=False):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--child', choices=('torch', 'native', 'torch72'))
+    ap.add_argument('--child', choices=('torch', 'native'))
     ap.add_argument('--repeat', type=int, default=3)
     ap.add_argument('--model', default='4096x16384x4')
     args = ap.parse_args()
     if args.child:
-        child(args.child != 'native', args.model, args.child == 'torch72')
+        child(args.child == 'torch', args.model)
         return 0
     for _ in range(args.repeat):
-        for kind in ('native', 'torch', 'torch72'):
+        for kind in ('native', 'torch'):
             out = subprocess.run(
                 [sys.executable, os.path.abspath(__file__), '--child', kind,
                  '--model', args.model],
