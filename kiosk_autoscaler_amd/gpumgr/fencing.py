@@ -53,19 +53,14 @@ class FencingMixin(object):
             self.events.emit('fence_comm', requested='node', used='epoch')
         if self.fence_comm != 'node':
             return
-        # standbys that hold no GPU (context / import) run it over the
-        # native shared-memory transport instead of RCCL, which would need
-        # a hardware queue and ~0.8 GiB of HBM per GPU
-        # (profiles/r2_hbm_hold).  A pool that parks (deep idle) stays on
-        # RCCL: each wake's generation is built after the woken worker is
-        # READY, its engine was built before its agent joined, so RCCL's
-        # one-time load on the agent's thread holds up no launch on the
-        # READY path (profiles/r4_collision), and a generation of fresh
-        # processes gets the first-generation budget
+        # RCCL for every GPU pool, one that parks (deep idle) included: each
+        # wake's generation is built after the woken worker is READY, its
+        # engine was built before its agent joined, so RCCL's one-time load
+        # on the agent's thread holds up no launch on the READY path
+        # (profiles/r4_collision), and a generation of fresh processes gets
+        # the first-generation budget.  ``fence_transport`` (FENCE) picks
+        # another transport explicitly.
         transport = fence_transport
-        if transport is None and self.pool_template.backend == 'hip' and \
-                self.pool_mode != 'device':
-            transport = 'shm'
         self.node = NodeComm(self, fence_timeout=min(fence_timeout, 30.0),
                              init_timeout=fence_init_timeout,
                              fallback=fence_fallback,
