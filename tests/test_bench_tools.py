@@ -331,8 +331,13 @@ def test_bench_tick_inproc_runs():
 def test_gpu_bench_contract(tmp_path):
     """MI355X: the driver's bench contract end to end at a tiny scale --
     one JSON line, the timed steps, every key served, the RCCL node
-    communicator, the managed device named, HBM figures in range."""
-    env = dict(os.environ, PYTHONPATH=ROOT, KIOSK_BENCH_OUT=str(tmp_path))
+    communicator, the managed device named, HBM figures in range.  A
+    resident pool: with the deep-idle default each wake builds its RCCL
+    generation after READY (~2 s), longer than these 1 s bursts keep a
+    worker, so no fence would complete (the driver-scale run,
+    profiles/r4_defaults, fences over RCCL in deep idle)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, KIOSK_BENCH_OUT=str(tmp_path),
+               POOL_IDLE_RELEASE_S='0')
     proc = subprocess.run(
         [sys.executable, os.path.join(ROOT, 'bench.py'), '--steps', '2',
          '--warmup', '1', '--interval', '1', '--on', '1', '--lam-per-gpu',
