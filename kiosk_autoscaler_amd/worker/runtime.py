@@ -65,9 +65,16 @@ class WorkerConfig(object):
             'keys_per_pod', _env_int(env, 'KEYS_PER_POD', 1))))
         batch_default = self.keys_per_pod if self.kind == 'job' else 1
         self.batch = max(1, _env_int(env, 'WORKER_BATCH', batch_default))
-        self.dim = _env_int(env, 'MODEL_DIM', 4096)
-        self.hidden = _env_int(env, 'MODEL_HIDDEN', 16384)
-        self.layers = _env_int(env, 'MODEL_LAYERS', 4)
+        # MODEL=DIMxHIDDENxLAYERS (the autoscaler knob; a standalone worker
+        # reads it too); the manager passes the parsed MODEL_DIM /
+        # MODEL_HIDDEN / MODEL_LAYERS, which win
+        dim, hidden, layers = 4096, 16384, 4
+        if env.get('MODEL'):
+            dim, hidden, layers = (int(v) for v in
+                                   str(env['MODEL']).lower().split('x'))
+        self.dim = _env_int(env, 'MODEL_DIM', dim)
+        self.hidden = _env_int(env, 'MODEL_HIDDEN', hidden)
+        self.layers = _env_int(env, 'MODEL_LAYERS', layers)
         self.rows = _env_int(env, 'ROWS_PER_KEY', 2048)
         self.passes = _env_int(env, 'PASSES_PER_KEY', 1)
         self.seed = _env_int(env, 'MODEL_SEED', 1234)

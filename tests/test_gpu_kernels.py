@@ -235,7 +235,11 @@ def test_fence_warmup_and_preinit(mod):
     ms = mod.fence_warmup(60.0)
     assert ms > 0
     stages = mod.preinit_device(0)
-    assert list(stages) == ['preinit_enter', 'preinit_context', 'preinit_done']
+    names = list(stages)
+    assert names[:2] == ['preinit_enter', 'preinit_context'] and \
+        names[-1] == 'preinit_done'
+    assert {'preinit_prepared', 'preinit_stream'} <= set(names)
+    assert list(stages.values()) == sorted(stages.values())
 
 
 def test_preload_modules_stamps(mod):

@@ -256,3 +256,15 @@ def test_standby_prebuild_builds_the_engine_the_assignment_reuses(
         assert 'no device' in chan.out[-1]['error'] and not wm._ENGINES
     finally:
         wm._drop_cached_engines()
+
+
+def test_worker_config_reads_model_and_prefers_the_parsed_sizes():
+    """A standalone worker reads the autoscaler's MODEL knob; the
+    manager's parsed MODEL_DIM / MODEL_HIDDEN / MODEL_LAYERS win."""
+    cfg = rt.WorkerConfig({'MODEL': '512x2048x2'}, {'worker_id': 'w'})
+    assert (cfg.dim, cfg.hidden, cfg.layers) == (512, 2048, 2)
+    cfg = rt.WorkerConfig({'MODEL': '512x2048x2', 'MODEL_DIM': '1024'},
+                          {'worker_id': 'w'})
+    assert (cfg.dim, cfg.hidden, cfg.layers) == (1024, 2048, 2)
+    cfg = rt.WorkerConfig({}, {'worker_id': 'w'})
+    assert (cfg.dim, cfg.hidden, cfg.layers) == (4096, 16384, 4)
