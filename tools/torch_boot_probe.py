@@ -23,7 +23,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def child(use_torch, model):
     t_start = time.perf_counter()
-    row = {'torch': use_torch}
+    row = {'torch': use_torch,
+           'torch_stream_first': bool(os.environ.get(
+               'PROBE_TORCH_STREAM_FIRST'))}
 
     def mark(name):
         row[name] = round((time.perf_counter() - t_start) * 1e3, 2)
@@ -34,6 +36,20 @@ def child(use_torch, model):
     from kiosk_autoscaler_amd.ops import native
     mod = native.load(torch_first=use_torch)
     mark('native_loaded')
+    if use_torch and os.environ.get('PROBE_TORCH_STREAM_FIRST'):
+        # which pays the first hardware queue: torch's own stream, created
+        # before preinit_device creates the native one?
+        import torch
+        torch.cuda.init()
+        mark('torch_cuda_init')
+        torch.empty(1, device='cuda').zero_()
+        torch.cuda.synchronize()
+        mark('torch_null_stream_op')
+        side = torch.cuda.Stream()
+        with torch.cuda.stream(side):
+            torch.empty(1, device='cuda').zero_()
+        side.synchronize()
+        mark('torch_side_stream_op')
     stages = dict(mod.preinit_device(0))
     base = stages['preinit_enter']
     row['preinit'] = {k: round((v - base) / 1e6, 2) for k, v in stages.items()}
@@ -83,10 +99,11 @@ def main():
         child(args.child == 'torch', args.model)
         return 0
     for _ in range(args.repeat):
-        for kind in ('native', 'torch'):
+        for kind, first in (('native', ''), ('torch', ''), ('torch', '1')):
+            env = dict(os.environ, PROBE_TORCH_STREAM_FIRST=first)
             out = subprocess.run(
                 [sys.executable, os.path.abspath(__file__), '--child', kind,
-                 '--model', args.model],
+                 '--model', args.model], env=env,
                 stdout=subprocess.PIPE, timeout=300, check=True)
             sys.stdout.write(out.stdout.decode())
             sys.stdout.flush()
