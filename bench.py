@@ -826,12 +826,17 @@ def managed_bdfs(n_gpus):
     """PCI addresses of the GPUs the run manages (None if not found)."""
     if os.environ.get('KIOSK_AMDSMI', '1') == '0':
         return None
+    # BENCH_GPU_IDS (rehearsal): several slots on one device; each device
+    # is sampled once
+    ids = os.environ.get('BENCH_GPU_IDS') or \
+        ','.join(str(i) for i in range(n_gpus))
+    unique = sorted(set(i.strip() for i in ids.split(',') if i.strip()),
+                    key=int)
     try:
         from kiosk_autoscaler_amd.gpumgr import gpus
-        slots = gpus.discover(','.join(str(i) for i in range(n_gpus)),
-                              env={}, cpu_slots=0)
+        slots = gpus.discover(','.join(unique), env={}, cpu_slots=0)
         found = [s.pci for s in slots if getattr(s, 'pci', None)]
-        if len(found) == n_gpus:
+        if len(found) == len(unique):
             return found
     except Exception:  # pylint: disable=broad-except
         pass
@@ -846,7 +851,9 @@ def verified_bdfs(redis, n_gpus):
     except (ValueError, TypeError):
         return None
     found = [s['pci'] for s in slots if s.get('verified') and s.get('pci')]
-    return found if len(found) == n_gpus else None
+    if len(found) != n_gpus:
+        return None
+    return sorted(set(found), key=found.index)    # one entry per device
 
 
 def start_util_sampler(n_gpus, bdfs=None):
