@@ -62,9 +62,9 @@ void free_device_buffer(DLManagedTensor* t) {
 
 // `nbytes` of device memory from hipMalloc as a uint8 DLPack capsule:
 // torch.utils.dlpack.from_dlpack() makes it a tensor that frees it when
-// the last view dies.  A PyTorch engine's arena comes from here because
-// the caching allocator's first segment of a size this large took ~110 ms
-// (profiles/r4_boot) against well under 1 ms for hipMalloc itself.
+// the last view dies.  The PyTorch engine's arena comes from here: one
+// allocation outside torch's caching allocator, so closing the engine
+// returns the HBM to the device instead of to a cached segment.
 py::capsule device_buffer(size_t nbytes, int device) {
   auto* buf = new DeviceBuffer();
   void* data = nullptr;

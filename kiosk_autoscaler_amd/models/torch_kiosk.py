@@ -107,9 +107,10 @@ class TorchKioskEngine(object):
         self.mod.prepare_kernels()
         if stage:
             stage('kernels_prepared')
-        # the stream the standby's preinit_device warmed: a new stream's
-        # first launch sets up a hardware queue (~0.1 s on MI355X,
-        # profiles/r4_boot); handed back on close for the next engine
+        # the stream the standby's preinit_device warmed (it paid the
+        # process's first hardware-queue set-up, ~85 ms in torch's HIP
+        # runtime, profiles/r4_boot); handed back on close for the next
+        # engine
         self._device_index = torch.cuda.current_device()
         self._stream_handle = self.mod.take_stream(self._device_index)
         if self._stream_handle:
@@ -140,10 +141,10 @@ class TorchKioskEngine(object):
         if stage:
             stage('sized')
         with torch.cuda.stream(self.stream):
-            # hipMalloc'ed by the native module and handed over by DLPack:
-            # the caching allocator's first segment this large took ~110 ms
-            # of a ~0.3 s standby boot (profiles/r4_boot); the tensor frees
-            # the buffer when its last view dies
+            # one hipMalloc by the native module, handed over by DLPack: the
+            # arena lives outside torch's caching allocator (no rounding, no
+            # cached segment left after close); the tensor frees the buffer
+            # when its last view dies
             from torch.utils.dlpack import from_dlpack
             self.arena = from_dlpack(self.mod.device_buffer(
                 total, torch.cuda.current_device()))
