@@ -830,8 +830,10 @@ def managed_bdfs(n_gpus):
     # is sampled once
     ids = os.environ.get('BENCH_GPU_IDS') or \
         ','.join(str(i) for i in range(n_gpus))
-    unique = sorted(set(i.strip() for i in ids.split(',') if i.strip()),
-                    key=int)
+    unique = []
+    for gpu_id in (i.strip() for i in ids.split(',')):
+        if gpu_id and gpu_id not in unique:
+            unique.append(gpu_id)
     try:
         from kiosk_autoscaler_amd.gpumgr import gpus
         slots = gpus.discover(','.join(unique), env={}, cpu_slots=0)
