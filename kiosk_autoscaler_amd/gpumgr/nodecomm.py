@@ -200,18 +200,28 @@ class NodeComm(object):
             time.monotonic() - since < self.first_init_timeout
 
     def candidates(self):
-        """``[(slot, proc)]`` over every managed slot, or ``None`` while one
-        of them has no live process with a node agent -- or while a worker
-        is still starting: a generation's RCCL init on a process that is
+        """``[(slot, proc)]`` over every slot that has a process, or
+        ``None`` while one of those processes is not a live node agent yet
+        (booting, paying RCCL's load, retiring) -- or while a worker is
+        still starting: a generation's RCCL init on a process that is
         building its engine competes with it (a PyTorch engine started 1.9 s
         after a deep-idle wake instead of 0.4 s), and the fence must stay
-        off the scale-up's critical path.  A slot whose
-        serving worker was quarantined (its agent stopped answering) is left
-        out until that worker has drained and exited."""
+        off the scale-up's critical path.  A slot that a
+        deep-idle pool sized to the queued keys leaves empty on purpose
+        (``PoolMixin.pool_sized_to_demand``) is left out: a process that
+        appears on it later joins by a regrow.  Otherwise every slot must
+        have one (a resident pool waits for a replacement instead of
+        building a generation that a regrow would replace seconds later).
+        A slot whose serving worker was
+        quarantined (its agent stopped answering) is left out until that
+        worker has drained and exited."""
         bound = self._bound()
+        sized = getattr(self.m, 'pool_sized_to_demand', lambda: False)()
         out = []
         for slot in self.m.slots:
             proc = bound.get(slot.index)
+            if proc is None and sized:
+                continue        # left empty on purpose: joins by a regrow
             if proc is not None and \
                     getattr(proc, 'node_quarantined', False) and \
                     self._alive(proc):

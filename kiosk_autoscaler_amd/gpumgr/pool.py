@@ -15,7 +15,8 @@ import subprocess
 import time
 
 from .nodecomm import NODE_EVENTS
-from .process import EXITED, ManagedProcess, Pipe, bare_worker
+from .process import (DRAINING, EXITED, ManagedProcess, Pipe,
+                      bare_worker)
 
 logger = logging.getLogger('GpuManager')
 
@@ -39,6 +40,7 @@ class PoolMixin(object):
         # the pool stays empty until the next scale-up (0 = never)
         self.pool_idle_release_s = float(pool_idle_release_s or 0.0)
         self.pool_parked = False
+        self.pool_parks = 0
         self._last_demand = time.monotonic()
         self.pool_wake_poll_s = float(pool_wake_poll_s or 0.0)
         self.pool_wake_hold_s = float(pool_wake_hold_s or 0.0)
@@ -54,6 +56,10 @@ class PoolMixin(object):
         # ends (a scale to zero implies empty queues, stranded keys aside),
         # so a key landing before the first check still counts as arrived
         self._queued = {}
+        # keys waiting in the managed queues at the last reading: a
+        # deep-idle pool keeps a standby per KEYS_PER_POD of them
+        self._waiting = 0
+        self._next_waiting_check = 0.0
         self.arrival_wakes = 0
         # worker zygote (worker/zygote.py): spawns fork from a process that
         # imported the worker (and torch, for a plug-in) without the GPU
@@ -240,13 +246,88 @@ class PoolMixin(object):
             if changed:
                 self._publish_pool()
             return
+        have = len(self.standbys)
+        target = self._standby_target(time.monotonic(), have)
         for slot in self._free_slots()[:self.pool_size]:
+            if have >= target:
+                break
             if slot.index not in self.standbys:
                 self.standbys[slot.index] = self._spawn(
                     self.pool_template, 'standby', slot=slot)
+                have += 1
                 changed = True
         if changed:
             self._publish_pool()
+
+    def _standby_target(self, now, have=0):
+        """How many standbys the pool keeps.  A resident pool
+        (``POOL_IDLE_RELEASE_S=0``): ``pool_size``, one per free slot.  A
+        deep-idle pool that is awake: one per KEYS_PER_POD keys waiting in
+        the managed queues beyond what idle workers will pull -- the
+        scale-ups the next tick can make -- and at least one while an
+        arrival's wake is held for its tick.  Standbys
+        the first tick would not assign would otherwise hold their GPU
+        (context, prebuilt engine) through the whole burst; later waiting
+        keys get theirs ahead of the tick that scales for them, and a
+        drained worker stays as a standby until the park.  At N = 1 nothing
+        changes: the one slot is the worker's."""
+        if not self.pool_sized_to_demand():
+            # resident, or the boot pool (every slot's device verified,
+            # then parked)
+            return self.pool_size
+        kpp = min([max(1, int(r.template.keys_per_pod or 1))
+                   for r in self.resources.values()] or [1])
+        # workers that will pull a waiting key themselves: running and not
+        # busy (a starting one included), not draining
+        idle = sum(1 for r in self.resources.values()
+                   for w in r.workers.values()
+                   if w.state not in (EXITED, DRAINING) and not w.busy)
+
+        def need():
+            n = max(0, -(-self._waiting_keys(now) // kpp) - idle)
+            if now < self._wake_until:
+                n = max(n, 1)
+            return min(self.pool_size, n)
+        target = need()
+        if target > have:
+            # a spawn on a reading taken before a worker pulled its key
+            # (its ``busy`` is what called us) would overshoot: re-read
+            self._next_waiting_check = 0.0
+            target = need()
+        return target
+
+    def pool_sized_to_demand(self):
+        """The pool leaves slots empty on purpose (deep idle after the boot
+        pool parked): the node communicator spans the slots that have a
+        process instead of waiting for all of them."""
+        return self.pool_idle_release_s > 0 and self.pool_parks > 0
+
+    def _waiting_keys(self, now):
+        """Keys waiting in the managed queues (one pipelined LLEN per queue,
+        at most every ``pool_wake_poll_s``; the last reading in between)."""
+        if now >= self._next_waiting_check:
+            self._next_waiting_check = now + max(self.pool_wake_poll_s, 0.02)
+            lengths = self._queue_lengths()
+            if lengths is not None:
+                self._waiting = sum(lengths.values())
+        return self._waiting
+
+    def _queue_lengths(self):
+        """``{queue: LLEN}`` over every managed queue, or None."""
+        if self.redis is None:
+            return None
+        queues = sorted(set(q for r in self.resources.values()
+                            for q in r.template.queues))
+        if not queues:
+            return {}
+        try:
+            pipe = self.redis.pipeline(transaction=False)
+            for queue in queues:
+                pipe.llen(queue)
+            return dict(zip(queues, (int(n or 0) for n in pipe.execute())))
+        except Exception as err:  # pylint: disable=broad-except
+            logger.debug('queue length check failed: %s', err)
+            return None
 
     def _park_pool(self):
         """Deep idle (``POOL_IDLE_RELEASE_S``): with no declared or live
@@ -313,6 +394,7 @@ class PoolMixin(object):
                 now < self._wake_until):
             return False
         self.pool_parked = True
+        self.pool_parks += 1
         released = 0
         for index, proc in list(self.standbys.items()):
             if proc.popen.poll() is None:
@@ -376,18 +458,12 @@ class PoolMixin(object):
                 now < self._next_arrival_check:
             return False
         self._next_arrival_check = now + self.pool_wake_poll_s
-        queues = sorted(set(q for r in self.resources.values()
-                            for q in r.template.queues))
-        if not queues:
+        lengths = self._queue_lengths()
+        if not lengths:
             return False
-        try:
-            pipe = self.redis.pipeline(transaction=False)
-            for queue in queues:
-                pipe.llen(queue)
-            lengths = dict(zip(queues, (int(n or 0) for n in pipe.execute())))
-        except Exception as err:  # pylint: disable=broad-except
-            logger.debug('arrival check failed: %s', err)
-            return False
+        queues = sorted(lengths)
+        self._waiting = sum(lengths.values())
+        self._next_waiting_check = now + self.pool_wake_poll_s
         before, self._queued = self._queued, lengths
         grown = [q for q in queues if lengths[q] > before.get(q, 0)]
         if grown:

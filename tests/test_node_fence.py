@@ -1296,9 +1296,11 @@ def test_arrival_woken_pool_builds_its_generation_after_ready(resp_server,
         parked_at = len(events.records)
         client.hset('predict:a', mapping={'status': 'new', 'rows': 8})
         client.lpush('predict', 'predict:a')
-        wait_for(lambda: len(manager.standbys) == 2 and all(
+        # one key: one standby (the pool is sized to the waiting keys)
+        wait_for(lambda: len(manager.standbys) == 1 and all(
             p.booted for p in manager.standbys.values()), timeout=60)
         time.sleep(0.3)
+        assert len(manager.standbys) == 1
         later = events.records[parked_at:]
         assert not [e for e in later if e['ev'] == 'node_comm_init']
         manager.patch_namespaced_deployment('worker', 'default',
@@ -1313,6 +1315,55 @@ def test_arrival_woken_pool_builds_its_generation_after_ready(resp_server,
         assert ready is not None and init is not None and init > ready
     finally:
         manager.stop(timeout=15)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize('transport', ['shm', 'rccl-fake'])
+def test_woken_pool_is_sized_to_the_waiting_keys(resp_server, tmp_path,
+                                                transport):
+    """Deep idle at N > 1: an arrival wakes one standby per KEYS_PER_POD
+    waiting keys, not one per slot (the others would hold their GPU through
+    the burst).  More keys, more standbys.  The node communicator spans the
+    slots that have a process, fences the scale-up, and a process that
+    appears on another slot joins by a regrow."""
+    s, client, events, manager, scaler = _node_stack(
+        resp_server, transport, tmp_path, MAX_PODS='4', WARM_POOL='4',
+        POOL_IDLE_RELEASE_S='0.3', POOL_WAKE_POLL_S='0.02')
+    try:
+        wait_for(lambda: manager.pool_parked and not manager.standbys,
+                 timeout=60)
+        for i in range(2):
+            client.hset('predict:w%d' % i, mapping={'status': 'new',
+                                                    'rows': 8})
+            client.lpush('predict', 'predict:w%d' % i)
+        wait_for(lambda: len(manager.standbys) == 2 and all(
+            p.booted for p in manager.standbys.values()), timeout=60)
+        time.sleep(0.3)
+        assert len(manager.standbys) == 2          # not 4
+        client.hset('predict:w2', mapping={'status': 'new', 'rows': 8})
+        client.lpush('predict', 'predict:w2')
+        wait_for(lambda: len(manager.standbys) == 3, timeout=30)
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 2}})
+        wait_for(lambda: _converged(manager, client) and
+                 len(_ready_ids(manager)) == 2, timeout=60)
+        assert manager.node.ready and not manager.node.full
+        assert len(manager.node.members) == 3
+        # a fourth process joins the communicator by a regrow
+        gens = manager.node.generations
+        client.hset('predict:w3', mapping={'status': 'new', 'rows': 8,
+                                           'service_ms': 3000})
+        client.lpush('predict', 'predict:w3')
+        manager.patch_namespaced_deployment('worker', 'default',
+                                            {'spec': {'replicas': 4}})
+        wait_for(lambda: manager.node.ready and manager.node.full and
+                 manager.node.generations > gens, timeout=60)
+        wait_for(lambda: _converged(manager, client) and
+                 len(_ready_ids(manager)) == 4, timeout=60)
+    finally:
+        manager.stop(timeout=15)
+    assert not any(e['failed'] for e in events.records
+                   if e['ev'] == 'node_comm_break')
 
 
 @pytest.mark.slow
