@@ -131,6 +131,7 @@ class Services(object):
         # HBM reference points: before any process of the run exists, and
         # once the standby pool (and its node communicator) has booted
         self.vram0 = self.vram_pool = None
+        self.hbm_baseline_source = 'before the run'
         bdfs = managed_bdfs(self.n) if args.backend == 'hip' else None
         self.bdfs = bdfs
         if bdfs:
@@ -691,10 +692,27 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
     events = drain_redis(svc.redis)
     summary = metrics.summarize(events, episodes) if episodes else None
     hbm = None
+    baseline, pool_boot = svc.vram0, svc.vram_pool
+    def parked_empty():
+        return svc.parked() and \
+            (svc.redis.get('kiosk:pool') or '').split()[:2] == ['0', '0']
+    if baseline is None and svc.bdfs:
+        deadline = time.monotonic() + 3.0
+        while not parked_empty() and time.monotonic() < deadline:
+            time.sleep(0.1)
+    if baseline is None and svc.bdfs and parked_empty():
+        # the pre-run reading was someone else's memory draining (a box
+        # read 232 GB used at start): the device with the pool parked and
+        # no worker -- nothing of this run on it -- is the baseline instead
+        baseline = gpu_util.vram_snapshot(svc.bdfs) or None
+        pool_boot = None
+        if baseline:
+            svc.hbm_baseline_source = 'parked pool after the run'
+            log('HBM baseline from the parked pool: %s' % baseline)
     if episodes and sampler is not None and hasattr(sampler, 'vram'):
         hbm = metrics.hbm_hold(events, sampler.vram(),
                                episodes[0]['t_first'], episodes[-1]['t_end'],
-                               baseline=svc.vram0, pool_boot=svc.vram_pool)
+                               baseline=baseline, pool_boot=pool_boot)
     ref = reference_sim(episodes, events, args, same_grid=True)
     ref_ideal = reference_sim(episodes, events, args, same_grid=False)
     # context only (never vs_baseline): the same trace and ticks with the
@@ -756,6 +774,9 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         # engine -- which includes this rank's own torch context)
         'standby_pool_boot_hbm_mib': _r((hbm or {}).get('pool_boot_mib'), 1),
         'idle_node_hbm_mib': _r((hbm or {}).get('idle_mib_median'), 1),
+        'idle_node_hbm_baseline': (svc.hbm_baseline_source
+                                   if (hbm or {}).get('baseline_mib')
+                                   is not None else 'none (absolute)'),
         # ENGINE_IDLE_RELEASE_S tier: idle HBM once the kept engine is freed
         'idle_node_hbm_released_mib': _r((hbm or {}).get(
             'idle_released_mib_median'), 1),
