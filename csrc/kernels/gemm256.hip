@@ -797,6 +797,267 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gemm256_kernel(
 // tile rows per group of the 256-row kernels' tile order (gemm_set_group_m)
 int g_group_m = 4;
 
+
+// ---------------------------------------------------------------------------
+// 4-wave 256x256 tile on v_mfma_f32_32x32x16_bf16 (gemm_set_mfma32).  The
+// ring, the DMA rate (8 pieces per half-step), the swizzle and the counted
+// waits are the 4-wave kernel's above; a half-step
+// runs 32 MFMAs of 32x32x16 instead of 64 of 16x16x32.  Each keeps the
+// matrix pipe busy for 32 cycles, so a wave held by an LDS-DMA issue stalls
+// the pipe for less of it (profiles/r4_mfma_dma: the same schedule on
+// register operands runs 7 % faster).  Per wave a 128x128 output in 4x4
+// tiles of 32x32 (16 AGPRs each); per 32-deep half-step two k-substeps of
+// 16.  Operands swapped as in the 4-wave kernel (C^T in the accumulators):
+// lane l holds, of tile (i, j), output row (l & 31) and the columns
+// 8b + 4(l >> 5) + 0..3, b = 0..3, of the tile's 32.  Fragment reads:
+// row (l & 31), 16-B chunk 2ks + (l >> 5) (+4 in a step's upper half):
+// 16 distinct bank groups in every ds_read_b128 lane group under the
+// ring's (r >> 1) & 7 swizzle.
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+__device__ __forceinline__ void mfma32_agpr(f32x16& acc, const bf16x8& a,
+                                            const bf16x8& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
+               : "+a"(acc)
+               : "v"(a), "v"(b));
+}
+
+__device__ __forceinline__ void mfma32_agpr_first(f32x16& acc,
+                                                  const bf16x8& a,
+                                                  const bf16x8& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0"
+               : "=a"(acc)
+               : "v"(a), "v"(b));
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm256m32_kernel(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+    uint16_t* __restrict__ C, const float* __restrict__ bias,
+    const uint16_t* __restrict__ R, int M, int N, int K, int lda,
+    int group_m) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int split = static_cast<int>(blockIdx.y);
+  A += static_cast<size_t>(split) * K;
+  B += static_cast<size_t>(split) * K;
+  const int tiles_n = N / 256;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int ntiles = tiles_m * tiles_n;
+  int m0 = 0, n0 = 0;
+  {
+    const int wg = xcd_remap(static_cast<int>(blockIdx.x), ntiles);
+    const int per_group = group_m * tiles_n;
+    const int group = wg / per_group;
+    const int first_m = group * group_m;
+    const int gsize = min(tiles_m - first_m, group_m);
+    const int in_group = wg - group * per_group;
+    m0 = (first_m + in_group % gsize) * BM;
+    n0 = (in_group / gsize) * 256;
+  }
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lane = static_cast<int>(threadIdx.x & 63);
+  constexpr int kUnit = BM * 128;
+  const int steps = K / 64;
+  f32x16 acc[4][4];
+
+  int voff_a[8], voff_b[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int r = (wave * 8 + p) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int ra = m0 + r < M ? m0 + r : M - 1;
+    const int rb = n0 + r < N ? n0 + r : N - 1;
+    voff_a[p] = (ra * lda + c * 8) * 2;
+    voff_b[p] = (rb * lda + c * 8) * 2;
+  }
+  const auto rsrc_a = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(A), 0, 0x7fffffff, 0x00020000);
+  const auto rsrc_b = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(B), 0, 0x7fffffff, 0x00020000);
+  // piece p of group g = operand (g & 1: B) of 64-deep step g >> 1, clamped
+  // to the last step past the end (same pipeline shape every step)
+  auto dma = [&](int g, int p) {
+    const int t = min(g >> 1, steps - 1);
+    char* lds = smem + (g % 5) * kUnit + (wave * 8 + p) * 1024;
+    if (g & 1)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_b, (lds_void_t*)lds, 16,
+                                               voff_b[p], t * 128, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)lds, 16,
+                                               voff_a[p], t * 128, 0, 0);
+  };
+  const int fr = lane & 31;
+  const int sw = (fr >> 1) & 7;
+  const int hk = lane >> 5;
+  const int row_a = (wm * 128 + fr) * 128, row_b = (wn * 128 + fr) * 128;
+  // [upper half][k-substep] -> this lane's byte offset in a unit
+  int off_a[2][2], off_b[2][2];
+#pragma unroll
+  for (int hi = 0; hi < 2; ++hi)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ((hi * 4 + ks * 2 + hk) ^ sw) << 4;
+      off_a[hi][ks] = row_a + chunk;
+      off_b[hi][ks] = row_b + chunk;
+    }
+  // fragment r of a half: r < 8 -> B (k-substep r >> 2, tile r & 3), else A
+  auto read = [&](auto hh, int t, int r, bf16x8 (&wb)[2][4],
+                  bf16x8 (&xa)[2][4]) {
+    constexpr int kHi = decltype(hh)::value;
+    const int ks = (r >> 2) & 1, idx = r & 3;
+    if (r < 8) {
+      const char* base = smem + __builtin_amdgcn_readfirstlane(
+                                    ((2 * t + 1) % 5) * kUnit) +
+                         off_b[kHi][ks];
+      wb[ks][idx] = *reinterpret_cast<const bf16x8*>(base + idx * 4096);
+    } else {
+      const char* base = smem + __builtin_amdgcn_readfirstlane(
+                                    ((2 * t) % 5) * kUnit) +
+                         off_a[kHi][ks];
+      xa[ks][idx] = *reinterpret_cast<const bf16x8*>(base + idx * 4096);
+    }
+  };
+  auto half = [&](auto first, auto odd, int t, const bf16x8 (&wb)[2][4],
+                  const bf16x8 (&xa)[2][4], bf16x8 (&wb_next)[2][4],
+                  bf16x8 (&xa_next)[2][4]) {
+    constexpr bool kOdd = decltype(odd)::value;
+    const int h = 2 * t + kOdd;
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(kOdd ? 8 : 16));
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const int tn = kOdd ? t + 1 : t;
+    using HH = std::integral_constant<int, kOdd ? 0 : 1>;
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int ks = u >> 4, i = (u >> 2) & 3, j = u & 3;
+      if constexpr (decltype(first)::value) {
+        if (ks == 0)
+          mfma32_agpr_first(acc[i][j], wb[ks][j], xa[ks][i]);
+        else
+          mfma32_agpr(acc[i][j], wb[ks][j], xa[ks][i]);
+      } else {
+        mfma32_agpr(acc[i][j], wb[ks][j], xa[ks][i]);
+      }
+      // a DMA piece every 4 MFMAs; the 16 reads of the next half-step in
+      // the first 24 MFMAs (two of every three), so the last one has 8
+      // MFMAs (~256 cycles) to land before the next half's lgkmcnt(0)
+      if (u % 4 == 1) dma(h + 4, u / 4);
+      if (u < 24 && u % 3 != 2) read(HH(), tn, (u / 3) * 2 + u % 3, wb_next,
+                                     xa_next);
+    }
+  };
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma(g, p);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(16));
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  bf16x8 wb0[2][4], xa0[2][4], wb1[2][4], xa1[2][4];
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    read(std::integral_constant<int, 0>(), 0, r, wb0, xa0);
+  half(std::true_type(), std::false_type(), 0, wb0, xa0, wb1, xa1);
+  half(std::false_type(), std::true_type(), 0, wb1, xa1, wb0, xa0);
+  for (int t = 1; t < steps; ++t) {
+    half(std::false_type(), std::false_type(), t, wb0, xa0, wb1, xa1);
+    half(std::false_type(), std::true_type(), t, wb1, xa1, wb0, xa0);
+  }
+  // drain the tail DMAs before the workgroup's LDS can be released
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  mfma_drain();
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));
+
+  auto pack2 = [](float lo, float hi) {
+    return f32_to_bf16(lo) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
+  };
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 128 + i * 32 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int n = n0 + wn * 128 + j * 32 + b * 8 + hk * 4;
+        float v[4] = {acc[i][j][4 * b], acc[i][j][4 * b + 1],
+                      acc[i][j][4 * b + 2], acc[i][j][4 * b + 3]};
+        if (EPI == EPI_PARTIAL) {
+          float* P = reinterpret_cast<float*>(C) +
+                     static_cast<size_t>(split) * M * N;
+          *reinterpret_cast<float4*>(P + static_cast<size_t>(m) * N + n) =
+              float4{v[0], v[1], v[2], v[3]};
+          continue;
+        }
+        if (EPI != EPI_NONE) {
+          const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+          v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+        }
+        if (EPI == EPI_BIAS_GELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+        }
+        if (EPI == EPI_BIAS_RESIDUAL) {
+          const uint2 res = *reinterpret_cast<const uint2*>(
+              R + static_cast<size_t>(m) * N + n);
+          v[0] += bf16_to_f32(res.x & 0xffff);
+          v[1] += bf16_to_f32(res.x >> 16);
+          v[2] += bf16_to_f32(res.y & 0xffff);
+          v[3] += bf16_to_f32(res.y >> 16);
+        }
+        *reinterpret_cast<uint2*>(C + static_cast<size_t>(m) * N + n) =
+            uint2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
+    }
+    // one row of tiles at a time: bounds the AGPR -> VGPR copies
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// 0: the 16x16x32 4-wave kernel; 1: gemm256m32_kernel wherever the 4-wave
+// one-tile kernel runs (plain, fused epilogues, split-K partials)
+int g_mfma32 = 0;
+
+template <int EPI>
+hipError_t configure_m32() {
+  hipError_t err = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&gemm256m32_kernel<EPI>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256, 4>::kLdsBytes);
+  return err == hipSuccess ? prepare_kernel(&gemm256m32_kernel<EPI>) : err;
+}
+
+hipError_t launch_m32(const uint16_t* A, const uint16_t* B, uint16_t* C,
+                      const float* bias, const uint16_t* R, int M, int N,
+                      int K, int lda, int splits, int epilogue,
+                      hipStream_t stream) {
+  const int blocks = ((M + BM - 1) / BM) * (N / 256);
+  const dim3 grid(blocks, splits), block(256);
+  constexpr int lds = Geo<256, 4>::kLdsBytes;
+  switch (epilogue) {
+    case EPI_NONE:
+      return launch_kernel(&gemm256m32_kernel<EPI_NONE>, grid, block, lds,
+                           stream, A, B, C, bias, R, M, N, K, lda, g_group_m);
+    case EPI_BIAS_GELU:
+      return launch_kernel(&gemm256m32_kernel<EPI_BIAS_GELU>, grid, block,
+                           lds, stream, A, B, C, bias, R, M, N, K, lda,
+                           g_group_m);
+    case EPI_BIAS_RESIDUAL:
+      return launch_kernel(&gemm256m32_kernel<EPI_BIAS_RESIDUAL>, grid, block,
+                           lds, stream, A, B, C, bias, R, M, N, K, lda,
+                           g_group_m);
+    case EPI_PARTIAL:
+      return launch_kernel(&gemm256m32_kernel<EPI_PARTIAL>, grid, block, lds,
+                           stream, A, B, C, bias, R, M, N, K, lda, g_group_m);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
 template <int EPI, int BN, int W>
 hipError_t configure256() {
   hipError_t err = hipFuncSetAttribute(
@@ -820,6 +1081,11 @@ hipError_t launch256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                      const float* bias, const uint16_t* R, int M, int N,
                      int K, int lda, int splits, int epilogue,
                      hipStream_t stream) {
+  if constexpr (BN == 256 && W == 4) {
+    if (g_mfma32)
+      return launch_m32(A, B, C, bias, R, M, N, K, lda, splits, epilogue,
+                        stream);
+  }
   const int blocks = ((M + BM - 1) / BM) * (N / BN);
   const dim3 grid(blocks, splits), block(64 * W);
   const int lds = Geo<BN, W>::kLdsBytes;
@@ -999,6 +1265,10 @@ hipError_t gemm256_prepare() {
   if (err == hipSuccess) err = configure_persist<EPI_BIAS_RESIDUAL>();
   if (err == hipSuccess) err = configure256_all<128, 8>();
   if (err == hipSuccess) err = configure256_all<256, 4>();
+  if (err == hipSuccess) err = configure_m32<EPI_NONE>();
+  if (err == hipSuccess) err = configure_m32<EPI_BIAS_GELU>();
+  if (err == hipSuccess) err = configure_m32<EPI_BIAS_RESIDUAL>();
+  if (err == hipSuccess) err = configure_m32<EPI_PARTIAL>();
   if (err == hipSuccess) err = configure_fused4<EPI_NONE>();
   if (err == hipSuccess) err = configure_fused4<EPI_BIAS_GELU>();
   if (err == hipSuccess) err = configure_fused4<EPI_BIAS_RESIDUAL>();
@@ -1083,6 +1353,9 @@ void gemm_set_group_m(int rows) { g_group_m = rows < 1 ? 1 : rows; }
 int gemm_group_m() { return g_group_m; }
 
 void gemm_set_splitk_fused(int mode) { g_splitk_fused = mode ? 1 : 0; }
+
+void gemm_set_mfma32(int on) { g_mfma32 = on ? 1 : 0; }
+int gemm_mfma32() { return g_mfma32; }
 int gemm_splitk_fused() { return g_splitk_fused; }
 
 // the fused 4-wave split-K path: two 64-deep-aligned slices, 32-bit

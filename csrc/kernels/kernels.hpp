@@ -77,6 +77,10 @@ size_t gemm256_splitk_workspace(int M, int N, int K);
 // slice, or (default, faster here) partial planes + the reduce kernel
 void gemm_set_splitk_fused(int mode);   // 0 reduce kernel, 1 in-launch
 int gemm_splitk_fused();
+// 1: the 4-wave one-tile kernel runs on v_mfma_f32_32x32x16_bf16
+// (gemm256m32_kernel, profiles/r4_mfma_dma); 0: on 16x16x32
+void gemm_set_mfma32(int on);
+int gemm_mfma32();
 // tile rows per group in the 256-row kernels' tile order (default 4)
 void gemm_set_group_m(int rows);
 int gemm_group_m();

@@ -143,6 +143,8 @@ PYBIND11_MODULE(_kiosk_hip, m) {
         "tile rows per group of the 256-row GEMM tile order (A/B knob)");
   m.def("gemm_group_m", &kiosk::gemm_group_m);
   m.def("gemm_splitk_fused", &kiosk::gemm_splitk_fused);
+  m.def("gemm_set_mfma32", &kiosk::gemm_set_mfma32, py::arg("on"));
+  m.def("gemm_mfma32", &kiosk::gemm_mfma32);
   m.attr("sum_blocks") = kiosk::kSumBlocks;
 
   m.def("gemm_shape_ok", &kiosk::gemm_shape_ok);

@@ -421,6 +421,62 @@ def _check_splitk(mod, kernels, M, N, K, epilogue):
     assert torch.equal(auto, c)          # auto picks split-K here
 
 
+@pytest.mark.parametrize('M,N,K', [(256, 256, 64), (300, 512, 192),
+                                   (777, 768, 192), (2048, 1024, 4096),
+                                   (1, 256, 64)])
+@pytest.mark.parametrize('epilogue', ['none', 'gelu', 'residual'])
+def test_gemm256_mfma32_kernel(mod, M, N, K, epilogue):
+    """gemm_set_mfma32(1): the 4-wave tile on v_mfma_f32_32x32x16_bf16
+    (gemm256m32_kernel) against the fp32 reference -- ragged M, one row,
+    a single 64-deep step -- and close to the 16x16x32 kernel (same
+    products, K summed in 16- instead of 32-deep MFMA steps)."""
+    from kiosk_autoscaler_amd.ops import kernels
+    a = rand_bf16(M, K, seed=41)
+    b = rand_bf16(N, K, scale=0.1, seed=42)
+    bias = torch.randn(N, device='cuda')
+    res = rand_bf16(M, N, seed=43)
+    ref = a.float() @ b.float().t()
+    if epilogue != 'none':
+        ref = ref + bias
+    if epilogue == 'gelu':
+        ref = gelu_tanh(ref)
+    if epilogue == 'residual':
+        ref = ref + res.float()
+    c16 = kernels.gemm(a, b, bias=bias, residual=res, epilogue=epilogue,
+                       variant='256w4')
+    mod.gemm_set_mfma32(1)
+    try:
+        c32 = kernels.gemm(a, b, bias=bias, residual=res, epilogue=epilogue,
+                           variant='256w4')
+    finally:
+        mod.gemm_set_mfma32(0)
+    torch.testing.assert_close(c32.float(), ref, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(c32.float(), c16.float(), atol=2e-2,
+                               rtol=1e-2)
+
+
+@pytest.mark.parametrize('epilogue', ['gelu', 'residual'])
+def test_gemm256_mfma32_splitk_and_forward_shapes(mod, epilogue):
+    """The worker's two GEMMs on the 32x32x16 kernel: the up-projection
+    (2048x16384x4096: 512 tiles, two per CU) and the split-K
+    down-projection (2048x4096x16384: fp32 partial planes + the reduce)."""
+    from kiosk_autoscaler_amd.ops import kernels
+    for M, N, K in ((2048, 16384, 4096), (2048, 4096, 16384)):
+        a = rand_bf16(M, K, seed=51)
+        b = rand_bf16(N, K, scale=0.02, seed=52)
+        bias = torch.randn(N, device='cuda')
+        res = rand_bf16(M, N, seed=53)
+        ref = a.float() @ b.float().t() + bias
+        ref = gelu_tanh(ref) if epilogue == 'gelu' else ref + res.float()
+        mod.gemm_set_mfma32(1)
+        try:
+            c = kernels.gemm(a, b, bias=bias, residual=res,
+                             epilogue=epilogue)
+        finally:
+            mod.gemm_set_mfma32(0)
+        torch.testing.assert_close(c.float(), ref, atol=3e-2, rtol=2e-2)
+
+
 def test_splitk_dispatch(mod):
     assert mod.gemm_pick_variant(2048, 4096, 16384, True) == 4
     assert mod.gemm_pick_variant(2048, 4096, 16384, False) == 3

@@ -29,6 +29,9 @@ def main():
                         help='comma-separated tile-row group sizes of the '
                              '256-row kernels: each adds <name>_gm<G> arms '
                              'of the 4-wave kernels (A/B in one process)')
+    parser.add_argument('--mfma32', action='store_true',
+                        help='add <name>_m32 arms of the 4-wave kernels on '
+                             'v_mfma_f32_32x32x16_bf16 (gemm_set_mfma32)')
     args = parser.parse_args()
     group_ms = [int(g) for g in args.group_m.split(',') if g]
     default_gm = mod.gemm_group_m()
@@ -121,6 +124,15 @@ def main():
                         fn()
                         mod.gemm_set_group_m(default_gm)
                     fns['%s_gm%d' % (base, gm)] = arm
+        if args.mfma32:
+            for base in ('native_gelu_auto', 'native256w4', 'native256w4_gelu',
+                         'native256splitk'):
+                if base in fns:
+                    def arm32(fn=fns[base]):
+                        mod.gemm_set_mfma32(1)
+                        fn()
+                        mod.gemm_set_mfma32(0)
+                    fns[base + '_m32'] = arm32
         if args.only:
             keep = set(args.only.split(','))
             fns = {k: v for k, v in fns.items() if k in keep}
