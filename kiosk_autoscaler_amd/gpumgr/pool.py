@@ -247,8 +247,9 @@ class PoolMixin(object):
                 self._publish_pool()
             return
         have = len(self.standbys)
-        target = self._standby_target(time.monotonic(), have)
-        for slot in self._free_slots()[:self.pool_size]:
+        free = self._free_slots()[:self.pool_size]
+        target = self._standby_target(time.monotonic(), have, len(free))
+        for slot in free:
             if have >= target:
                 break
             if slot.index not in self.standbys:
@@ -259,7 +260,7 @@ class PoolMixin(object):
         if changed:
             self._publish_pool()
 
-    def _standby_target(self, now, have=0):
+    def _standby_target(self, now, have=0, room=None):
         """How many standbys the pool keeps.  A resident pool
         (``POOL_IDLE_RELEASE_S=0``): ``pool_size``, one per free slot.  A
         deep-idle pool that is awake: one per KEYS_PER_POD keys waiting in
@@ -283,11 +284,13 @@ class PoolMixin(object):
                    for w in r.workers.values()
                    if w.state not in (EXITED, DRAINING) and not w.busy)
 
+        cap = self.pool_size if room is None else min(self.pool_size, room)
+
         def need():
             n = max(0, -(-self._waiting_keys(now) // kpp) - idle)
             if now < self._wake_until:
                 n = max(n, 1)
-            return min(self.pool_size, n)
+            return min(cap, n)
         target = need()
         if target > have:
             # a spawn on a reading taken before a worker pulled its key

@@ -774,3 +774,55 @@ def test_orphaned_zombies_are_reaped_by_pid():
     assert manager._reap_orphans(now=1.0) == []        # scan interval
     assert stray.pid in manager._reap_orphans(now=10.0)
     assert not os.path.exists('/proc/%d' % stray.pid)
+
+
+def test_deep_idle_standby_target_follows_waiting_keys():
+    """A deep-idle pool keeps one standby per KEYS_PER_POD keys waiting
+    beyond what idle workers will pull (capped by the slots a standby can
+    take); a resident or not-yet-parked pool keeps pool_size.  A target
+    above what the pool holds re-reads the queues once, not on every poll
+    when no slot is free."""
+    import types
+    from kiosk_autoscaler_amd.gpumgr.controller import GpuManager
+    calls = []
+
+    class _Pipe(object):
+        def __init__(self, lengths):
+            self.lengths, self.queued = lengths, []
+
+        def llen(self, queue):
+            self.queued.append(queue)
+
+        def execute(self):
+            calls.append(list(self.queued))
+            return [self.lengths[q] for q in self.queued]
+
+    class _Redis(object):
+        lengths = {'q': 5}
+
+        def pipeline(self, transaction=False):
+            return _Pipe(self.lengths)
+    slots = [gpus.GpuSlot(i, str(i)) for i in range(4)]
+    tpl = gpumgr.WorkerTemplate(queues=['q'], backend='cpu')
+    manager = GpuManager(slots, pool_size=4, pool_template=tpl,
+                         pool_idle_release_s=0.5, redis_client=_Redis())
+    res = types.SimpleNamespace(
+        template=types.SimpleNamespace(keys_per_pod=2, queues=['q']),
+        workers={})
+    manager.resources = {('deployment', 'default', 'w'): res}
+    assert manager._standby_target(0.0) == 4          # the boot pool
+    manager.pool_parks = 1
+    assert manager.pool_sized_to_demand()
+    assert manager._standby_target(10.0) == 3          # ceil(5 / 2)
+    res.workers = {'a': types.SimpleNamespace(state='ready', busy=False)}
+    manager._next_waiting_check = 0.0
+    assert manager._standby_target(20.0) == 2          # one idle worker
+    res.workers['a'].busy = True
+    manager._next_waiting_check = 0.0
+    assert manager._standby_target(30.0) == 3
+    # no room: the target is capped, and no forced re-read happens
+    n = len(calls)
+    assert manager._standby_target(30.01, have=0, room=0) == 0
+    assert len(calls) == n
+    manager.pool_idle_release_s = 0.0
+    assert manager._standby_target(40.0) == 4          # resident pool
