@@ -249,6 +249,9 @@ class PoolMixin(object):
         have = len(self.standbys)
         free = self._free_slots()[:self.pool_size]
         target = self._standby_target(time.monotonic(), have, len(free))
+        if have > target and self._retire_excess(have - target):
+            changed = True
+            have = len(self.standbys)
         for slot in free:
             if have >= target:
                 break
@@ -298,6 +301,32 @@ class PoolMixin(object):
             self._next_waiting_check = 0.0
             target = need()
         return target
+
+    def _retire_excess(self, excess, now=None):
+        """A pool sized to demand retires standbys it holds beyond its
+        target once they have waited a tick's hold (``pool_wake_hold_s``)
+        unassigned -- typically drained workers recycled mid-burst, which
+        would otherwise hold their GPU (context, engine) until the burst
+        ends.  Oldest-idle first; True if any was retired."""
+        if not self.pool_sized_to_demand() or excess <= 0:
+            return False
+        now = time.monotonic() if now is None else now
+        hold = max(self.pool_wake_hold_s, self.pool_idle_release_s)
+        idle = sorted((proc.standby_since, index)
+                      for index, proc in self.standbys.items()
+                      if proc.booted and proc.standby_since is not None and
+                      now - proc.standby_since > hold)
+        retired = 0
+        for _, index in idle[:excess]:
+            proc = self.standbys.pop(index)
+            if proc.popen.poll() is None:
+                proc.pipe.send({'cmd': 'exit'})
+                self.retiring.append(proc)
+            retired += 1
+        if retired:
+            self.events.emit('standby_retired', standbys=retired,
+                             reason='beyond demand')
+        return retired > 0
 
     def pool_sized_to_demand(self):
         """The pool leaves slots empty on purpose (deep idle after the boot
@@ -553,6 +582,7 @@ class PoolMixin(object):
                 self._wake_boots.append(
                     (time.monotonic_ns() - proc.t_spawn) / 1e9)
             proc.booted = True
+            proc.standby_since = time.monotonic()
             proc.hbm_free = message.get('hbm_free')
             if message.get('pci'):
                 if not self._check_device(proc, message.get('pci')):

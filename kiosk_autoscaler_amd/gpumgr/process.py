@@ -114,6 +114,7 @@ class ManagedProcess(object):
         self.hbm_free = None    # free HBM bytes the standby measured
         self.woken = False      # spawned by an arrival wake (prebuilds)
         self.engine_cached = False  # standby holds a built engine
+        self.standby_since = None   # monotonic s of its last 'standby'
 
     @property
     def pid(self):

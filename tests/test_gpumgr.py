@@ -826,3 +826,33 @@ def test_deep_idle_standby_target_follows_waiting_keys():
     assert len(calls) == n
     manager.pool_idle_release_s = 0.0
     assert manager._standby_target(40.0) == 4          # resident pool
+
+
+def test_sized_pool_retires_standbys_idle_beyond_demand():
+    """A deep-idle pool sized to demand retires the standbys it holds beyond
+    its target once they waited a tick's hold unassigned (drained workers
+    recycled mid-burst), oldest first -- never a resident pool's, never one
+    still booting or idle for less than the hold."""
+    import types
+    from kiosk_autoscaler_amd.gpumgr.controller import GpuManager
+    slots = [gpus.GpuSlot(i, str(i)) for i in range(4)]
+    tpl = gpumgr.WorkerTemplate(queues=['q'], backend='cpu')
+    manager = GpuManager(slots, pool_size=4, pool_template=tpl,
+                         pool_idle_release_s=0.5, pool_wake_hold_s=8.5)
+    sent = []
+
+    def proc(since, booted=True):
+        return types.SimpleNamespace(
+            booted=booted, standby_since=since,
+            popen=types.SimpleNamespace(poll=lambda: None),
+            pipe=types.SimpleNamespace(send=sent.append))
+    manager.standbys = {0: proc(100.0), 1: proc(95.0), 2: proc(109.0),
+                        3: proc(None, booted=False)}
+    assert not manager._retire_excess(2, now=110.0)    # boot pool: resident
+    manager.pool_parks = 1
+    assert manager._retire_excess(2, now=110.0)
+    # 1 (idle 15 s) then 0 (10 s); 2 (1 s) and the booting 3 stay
+    assert sorted(manager.standbys) == [2, 3]
+    assert sent == [{'cmd': 'exit'}, {'cmd': 'exit'}]
+    assert len(manager.retiring) == 2
+    assert not manager._retire_excess(2, now=110.0)    # none idle long enough
