@@ -17,6 +17,9 @@ def main():
     parser.add_argument('--shapes', default='2048x16384x4096,2048x4096x16384')
     parser.add_argument('--variants', default='256,256x128,128')
     parser.add_argument('--iters', type=int, default=10)
+    parser.add_argument('--mfma32', action='store_true',
+                        help='run each 256w4 variant again on the 32x32x16 '
+                             'kernel (gemm_set_mfma32; its own kernel name)')
     args = parser.parse_args()
     import torch
     from kiosk_autoscaler_amd.ops import kernels
@@ -33,6 +36,15 @@ def main():
                 kernels.gemm(a, b, out=out, variant=variant)
             torch.cuda.synchronize()
             print('%s %s done' % (spec, variant), flush=True)
+            if args.mfma32 and variant == '256w4':
+                from kiosk_autoscaler_amd.ops import native
+                mod = native.load()
+                mod.gemm_set_mfma32(1)
+                for _ in range(args.iters):
+                    kernels.gemm(a, b, out=out, variant=variant)
+                torch.cuda.synchronize()
+                mod.gemm_set_mfma32(0)
+                print('%s %s mfma32 done' % (spec, variant), flush=True)
 
 
 if __name__ == '__main__':
