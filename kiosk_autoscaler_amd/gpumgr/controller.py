@@ -10,15 +10,15 @@ this module plays API server + controller + kubelet:
 * **Workers** are OS processes, one per GPU, pinned with
   ``HIP_VISIBLE_DEVICES`` and CPU affinity to the GPU's NUMA-local cores.
   The lowest free GPU index is allocated first.
-* **Warm pool**: ``pool_size`` standby processes, each pinned to its GPU
-  at spawn, have imported the native kernel module (not PyTorch).  With
-  ``WARM_POOL_MODE=device`` (the default) they have also created the HIP
-  context and loaded every code object, so **a standby holds its GPU**
-  (context and code objects, no weights; the benchmark reports this as
-  ``standby_gpu_s``); with ``import`` they stop before HIP and hold none.
-  A scale-up hands a standby its assignment over a pipe, taking process
-  start, imports and the HIP init (0.27 s together) off the critical path
-  (SURVEY §7.4 item 4).  Standbys do not count as replicas.
+* **Warm pool** (:mod:`.pool`): standby processes, each pinned to its GPU
+  at spawn, have imported the native kernel module (not PyTorch, unless a
+  plug-in needs it), created the HIP context, loaded every code object and
+  prebuilt the engine with its warm-start graph, so **a standby holds its
+  GPU** (the benchmark reports this as ``standby_gpu_s``).  A scale-up
+  hands a standby its assignment over a pipe, and READY is one graph
+  launch.  Deep idle parks the pool when demand ends
+  and wakes it, sized to the waiting keys, ahead of the tick that scales
+  for them.  Standbys do not count as replicas.
 * **READY** (``status.available_replicas``) means the worker has its
   weights in HBM and has run the warm-start kernel.
 * **Scale-down** drains: the worker finishes its in-flight key and exits.
@@ -32,9 +32,10 @@ this module plays API server + controller + kubelet:
 * **Membership fence**: whenever the READY set changes the manager starts a
   fence epoch (coalesced: one in flight at a time); the set is agreed with
   a 72-B RCCL all-reduce over xGMI and rank 0 acknowledges.  With a standby
-  per GPU the communicator is persistent (:mod:`.nodecomm`: built once over
-  every slot's process, rebuilt only when one dies); otherwise each epoch
-  bootstraps its own over the READY workers.  The fenced set is published
+  per GPU the communicator is persistent (:mod:`.nodecomm`, orchestrated
+  by :mod:`.fencing`: built over the slots' processes, shrunk when one
+  exits, regrown when one appears); otherwise each epoch bootstraps its own
+  over the READY workers.  The fenced set is published
   to Redis (``kiosk:active:<ns>:<name>``).
 """
 import collections
