@@ -200,6 +200,19 @@ PYBIND11_MODULE(_kiosk_hip, m) {
       py::arg("ptr"), py::arg("n"), py::arg("seed_ptr"), py::arg("lo") = -1.0f,
       py::arg("hi") = 1.0f, py::arg("stream") = 0,
       py::call_guard<py::gil_scoped_release>());
+  // hipMemsetAsync (a runtime blit kernel, already loaded with the first
+  // stream): the PyTorch engine clears its buffers with it, so its boot
+  // loads no torch fill kernel from libtorch_hip's code objects
+  m.def(
+      "memset_async",
+      [](unsigned long long p, int value, size_t nbytes,
+         unsigned long long stream) {
+        check_hip(hipMemsetAsync(ptr<void>(p), value, nbytes,
+                                 stream_of(stream)),
+                  "hipMemsetAsync");
+      },
+      py::arg("ptr"), py::arg("value"), py::arg("nbytes"),
+      py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("prepare_kernels",
         [] {
           check_hip(kiosk::gemm_prepare(), "gemm_prepare");

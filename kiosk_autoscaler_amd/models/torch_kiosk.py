@@ -86,11 +86,13 @@ class TorchKioskEngine(object):
 
     @staticmethod
     def warm_device():
-        """Standby boot (``worker/main.py``): torch's CUDA context and
-        caching allocator plus our launch handles -- no hipBLASLt handle
-        (this engine never calls a torch matmul)."""
+        """Standby boot (``worker/main.py``): torch's lazy CUDA init plus
+        our launch handles -- no hipBLASLt handle (this engine never calls
+        a torch matmul) and no torch kernel: the engine clears its buffers
+        with ``hipMemsetAsync``, so no torch code object is loaded on the
+        boot path (profiles/r4_comgr)."""
         import torch
-        torch.empty(1, device='cuda').zero_()
+        torch.cuda.init()
         native.load().prepare_kernels()
 
     def __init__(self, cfg, stage=None):
@@ -153,7 +155,8 @@ class TorchKioskEngine(object):
             carve = _Carver(self.arena)
             for name, shape, dtype in small:
                 setattr(self, name, carve(shape, dtype))
-            self.arena[:carve.offset].zero_()
+            self.mod.memset_async(self.arena.data_ptr(), 0, carve.offset,
+                                  self.stream.cuda_stream)
             self.weights = ops.model_weights(dim, hidden, self.layers,
                                              self.seed, alloc=carve)
             for name, shape, dtype in big:
@@ -243,7 +246,8 @@ class TorchKioskEngine(object):
 
         def enqueue():
             stream = self.torch.cuda.current_stream().cuda_stream
-            self.warm_record.zero_()
+            self.mod.memset_async(self.warm_record.data_ptr(), 0,
+                                  self.warm_record.numel() * 4, stream)
             self.mod.warmstart_raw(
                 w1.data_ptr(), w1.numel(), self.warm_record.data_ptr(),
                 self._cus(), _WARM_ITERS, self.mod.gemm_ring_lds_bytes,

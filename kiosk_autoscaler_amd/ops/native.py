@@ -8,6 +8,12 @@ process would each own the device).  The worker never uses torch: it loads
 the extension with ``torch_first=False`` and runs on ROCm's own runtime (the
 one the extension was compiled against), which takes the ~1.5 s torch
 import -- minutes on a fresh node -- off standby boot and cold spawns.
+A torch process gets ROCm's own code-object compiler (comgr) instead of
+torch's bundled copy (:func:`prefer_rocm_comgr`): the HIP runtime compiles
+its blit kernels through comgr when the process creates its first stream,
+and torch's comgr caches only the back half of that compile, so every
+PyTorch standby paid ~60 ms of OpenCL front end at boot
+(``profiles/r4_stream``).
 RCCL is *not* a link-time dependency: the fence code ``dlopen``s a full RCCL
 (``KIOSK_RCCL_LIB``, default ROCm's, which has ``ncclCommShrink``) with
 ``RTLD_LOCAL``.
@@ -21,6 +27,7 @@ compiled for the host against the shared-memory fake HIP + RCCL
 (``tools/build_native.py --fake-hip``), so the production fence path runs in
 N CPU processes.  It has no kernels and no engine.
 """
+import ctypes
 import glob
 import importlib
 import os
@@ -63,6 +70,33 @@ def _load_fake():
     return importlib.import_module('_kiosk_fence_cpu')
 
 
+def prefer_rocm_comgr():
+    """Map ROCm's ``libamd_comgr.so`` before torch loads its own.
+
+    Torch's ``libamdhip64.so`` needs ``libamd_comgr.so`` (unversioned) via
+    an ``$ORIGIN`` RPATH.  A library already loaded *under that name* meets
+    the dependency, so a bare-name ``dlopen`` (resolved by the loader cache
+    to ``/opt/rocm``) puts ROCm 7.2's comgr under torch's HIP runtime; the
+    HIP and HSA runtimes stay torch's own (one of each per process).
+    ROCm's comgr caches the whole blit-kernel compile on disk
+    (``AMD_COMGR_CACHE``, on by default), torch's 7.0 copy only its code
+    generation: a torch process's first stream drops from ~85 ms to
+    ~20 ms.  No-op once torch is imported; returns the path mapped, or
+    None."""
+    if 'torch' in sys.modules:
+        return None
+    try:
+        ctypes.CDLL('libamd_comgr.so', mode=ctypes.RTLD_GLOBAL)
+    except OSError:
+        return None
+    try:
+        with open('/proc/self/maps') as maps:
+            paths = {line.split()[-1] for line in maps if 'comgr' in line}
+    except OSError:
+        return None
+    return sorted(paths)[0] if paths else None
+
+
 def load(torch_first=True):
     """Import and return the native module (cached; the first call decides
     the load order).  ``torch_first=False`` is for processes that never
@@ -77,6 +111,7 @@ def load(torch_first=True):
         raise NativeUnavailable('native module _kiosk_hip is not built; '
                                 + BUILD_HINT)
     if torch_first:
+        prefer_rocm_comgr()
         try:
             import torch  # noqa: F401  -- must precede the extension
         except ImportError:

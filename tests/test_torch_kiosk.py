@@ -3,7 +3,10 @@
 numerics against the fp32 PyTorch reference, bit-equality with the
 built-in native engine, one-graph-launch warm start and forward, and the
 engine serving keys through a real worker process on MI355X."""
+import json
 import os
+import subprocess
+import sys
 import time
 
 import pytest
@@ -135,6 +138,53 @@ def test_engine_reuses_the_preinit_stream_and_a_dlpack_arena(cuda):
     again = mod.take_stream(0)
     assert again == handle
     mod.return_stream(again, 0)
+
+
+_COMGR_CHILD = r'''
+import json, sys
+sys.path.insert(0, sys.argv[1])
+from kiosk_autoscaler_amd.ops import native, kernels
+mod = native.load(torch_first=True)        # the worker's load order
+import torch
+from kiosk_autoscaler_amd.models.torch_kiosk import TorchKioskEngine
+from kiosk_autoscaler_amd.worker.runtime import WorkerConfig
+stages = dict(mod.preinit_device(0))
+cfg = WorkerConfig({'MODEL_DIM': '1024', 'MODEL_HIDDEN': '4096',
+                    'MODEL_LAYERS': '2', 'ROWS_PER_KEY': '512',
+                    'MODEL_SEED': '21'}, {'worker_id': 'w'})
+engine = TorchKioskEngine(cfg)
+ours = engine.output(512, 9)
+ref_engine = mod.Engine(0, 1024, 4096, 2, 512, 21)
+ref_engine.forward(512, 1, 9)
+same = bool(torch.equal(ours, kernels.engine_output(ref_engine, 512)))
+# torch's own blit kernels and BLAS after the comgr swap
+a = torch.full((256, 256), 0.25, device='cuda', dtype=torch.bfloat16)
+blas = float((a @ a).float().sum().cpu())
+ref_engine.close()
+engine.close()
+maps = [l.split()[-1] for l in open('/proc/self/maps')]
+print(json.dumps({
+    'same': same, 'blas': blas,
+    'stream_ms': (stages['preinit_stream'] - stages['preinit_prepared']) / 1e6,
+    'comgr': sorted({m for m in maps if 'comgr' in m}),
+    'hip': sorted({m for m in maps if 'libamdhip64' in m})}))
+'''
+
+
+def test_worker_load_order_runs_rocm_comgr_under_torch(cuda):
+    """``native.load(torch_first=True)`` (the PyTorch worker's load order)
+    maps ROCm's comgr under torch's own HIP runtime: the engine still
+    serves the built-in engine's bytes, torch's blit kernels and BLAS still
+    work, and the first stream no longer pays torch's uncached blit-kernel
+    front end (profiles/r4_stream)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, '-c', _COMGR_CHILD, root],
+                         stdout=subprocess.PIPE, timeout=120, check=True)
+    row = json.loads(out.stdout.decode().strip().splitlines()[-1])
+    print(row)
+    assert row['same'] and row['blas'] == 256 * 256 * 256 * 0.0625
+    assert len(row['comgr']) == 1 and row['comgr'][0].startswith('/opt/rocm')
+    assert len(row['hip']) == 1 and 'torch' in row['hip'][0]
 
 
 def test_torch_worker_serves_keys_through_the_manager(resp_server):

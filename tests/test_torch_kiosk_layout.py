@@ -2,6 +2,11 @@
 (models/torch_kiosk.py): the carver hands out aligned, non-overlapping
 typed views, and the size the engine reserves for the weights is exactly
 what :func:`ops.kernels.model_weights` takes from it."""
+import json
+import os
+import subprocess
+import sys
+
 import pytest
 
 torch = pytest.importorskip('torch')
@@ -54,3 +59,30 @@ def test_weight_reservation_matches_model_weights_allocation():
                      ((dim,), torch.float32)]
     size = sum(tk._aligned(tk._nbytes(s, d)) for s, d in order)
     assert size == tk._layer_bytes(dim, hidden)
+
+
+def test_rocm_comgr_replaces_torchs_bundled_copy():
+    """``native.prefer_rocm_comgr`` before ``import torch``: one comgr is
+    mapped, ROCm's, and torch's HIP runtime is still torch's own (no second
+    HIP runtime).  After torch is imported it is a no-op."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    child = (
+        'import json, sys\n'
+        'sys.path.insert(0, sys.argv[1])\n'
+        'from kiosk_autoscaler_amd.ops import native\n'
+        'first = native.prefer_rocm_comgr()\n'
+        'import torch\n'
+        'again = native.prefer_rocm_comgr()\n'
+        'maps = [l.split()[-1] for l in open("/proc/self/maps")]\n'
+        'print(json.dumps({"first": first, "again": again,\n'
+        '  "comgr": sorted({m for m in maps if "comgr" in m}),\n'
+        '  "hip": sorted({m for m in maps if "libamdhip64" in m})}))\n')
+    out = subprocess.run([sys.executable, '-c', child, root],
+                         stdout=subprocess.PIPE, timeout=300, check=True)
+    row = json.loads(out.stdout.decode().strip().splitlines()[-1])
+    if row['first'] is None:
+        pytest.skip('no ROCm comgr in the loader cache')
+    assert row['comgr'] == [row['first']]
+    assert row['first'].startswith('/opt/rocm')
+    assert row['again'] is None
+    assert len(row['hip']) == 1 and 'torch' in row['hip'][0]

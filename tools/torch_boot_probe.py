@@ -29,13 +29,15 @@ def child(use_torch, model):
 
     def mark(name):
         row[name] = round((time.perf_counter() - t_start) * 1e3, 2)
-    if use_torch:
-        import torch  # noqa: F401
-        mark('torch_imported')
     sys.path.insert(0, ROOT)
     from kiosk_autoscaler_amd.ops import native
+    # the worker's order: native.load imports torch (after mapping ROCm's
+    # comgr, ``prefer_rocm_comgr``), then the extension
     mod = native.load(torch_first=use_torch)
     mark('native_loaded')
+    with open('/proc/self/maps') as maps:
+        row['comgr'] = sorted({line.split()[-1] for line in maps
+                               if 'comgr' in line})
     if use_torch and os.environ.get('PROBE_TORCH_STREAM_FIRST'):
         # which pays the first hardware queue: torch's own stream, created
         # before preinit_device creates the native one?
