@@ -686,6 +686,27 @@ def base_line(args, episodes, elapsed):
     }
 
 
+def _low_vram_baseline(svc, sampler, reads=10):
+    """Per-device VRAM with nothing of this run on it, read after the run:
+    the lowest of ``reads`` snapshots 0.1 s apart (a process that just
+    exited can still be freeing; one snapshot read 2.6 GB over the run's
+    own idle samples, ``profiles/r4_torch_default``), and never above the
+    lowest sample taken during the run (too low a baseline only overstates
+    the idle figure)."""
+    low = {}
+    for i in range(reads):
+        snap = gpu_util.vram_snapshot(svc.bdfs) or {}
+        for bdf, mib in snap.items():
+            low[bdf] = min(mib, low.get(bdf, mib))
+        if i + 1 < reads:
+            time.sleep(0.1)
+    if sampler is not None and hasattr(sampler, 'vram'):
+        for bdf, samples in (sampler.vram().get('device') or {}).items():
+            if bdf in low and samples:
+                low[bdf] = min(low[bdf], min(m for _, m in samples))
+    return low or None
+
+
 def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
     from kiosk_autoscaler_amd.bench import metrics, sim
     from kiosk_autoscaler_amd.utils.events import drain_redis
@@ -704,7 +725,7 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         # the pre-run reading was someone else's memory draining (a box
         # read 232 GB used at start): the device with the pool parked and
         # no worker -- nothing of this run on it -- is the baseline instead
-        baseline = gpu_util.vram_snapshot(svc.bdfs) or None
+        baseline = _low_vram_baseline(svc, sampler)
         pool_boot = None
         if baseline:
             svc.hbm_baseline_source = 'parked pool after the run'

@@ -396,3 +396,27 @@ def test_pmc_summary_mfma_busy_over_active(tmp_path):
     assert mod.durations(dirs) == {'k': 200000.0}
     assert data['k']['GRBM_GUI_ACTIVE'] == 8 * cycles    # not 16x
     assert abs(mod.derive(data['k'])['mfma_busy_over_active'] - 1.0) < 1e-9
+
+
+def test_post_run_hbm_baseline_is_the_lowest_reading(monkeypatch):
+    """bench.py's after-the-run HBM baseline: the lowest of several
+    snapshots (a just-exited process may still be freeing) and never above
+    the run's own lowest sample, so idle HBM over it cannot go negative."""
+    import importlib.util
+    import types
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location(
+        'bench_main', os.path.join(root, 'bench.py'))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    reads = iter([{'a': 3000.0, 'b': 500.0}, {'a': 420.0, 'b': 510.0}] +
+                 [{'a': 430.0, 'b': 505.0}] * 8)
+    monkeypatch.setattr(bench.gpu_util, 'vram_snapshot',
+                        lambda bdfs=None: next(reads))
+    monkeypatch.setattr(bench.time, 'sleep', lambda s: None)
+    sampler = types.SimpleNamespace(vram=lambda: {'device': {
+        'a': [(1, 900.0), (2, 415.0)], 'b': [(1, 700.0)]}})
+    svc = types.SimpleNamespace(bdfs=['a', 'b'])
+    assert bench._low_vram_baseline(svc, sampler) == {'a': 415.0, 'b': 500.0}
+    reads = iter([{}] * 10)
+    assert bench._low_vram_baseline(svc, None) is None
