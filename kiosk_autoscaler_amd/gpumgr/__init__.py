@@ -6,6 +6,7 @@ returns the actuator the Autoscaler talks to -- the process-wide embedded
 manager, or a client for an out-of-process daemon (``GPUMGR=unix:PATH``).
 """
 import os
+import tempfile
 
 from .controller import GpuManager, WorkerTemplate
 from .daemon import GpuManagerClient, ManagerServer
@@ -41,6 +42,38 @@ def resolve_backend(requested, slots):
     return 'hip' if any(s.kind == 'gpu' for s in slots) else 'cpu'
 
 
+def comgr_cache_env(environ=None):
+    """Where a worker's HIP runtime caches its blit-kernel build.
+
+    Every HIP process compiles the runtime's blit kernels through comgr at
+    its first stream: ~150 ms cold, ~15-20 ms from comgr's on-disk cache
+    (``$XDG_CACHE_HOME/comgr``, else ``~/.cache/comgr``;
+    profiles/r4_comgr).  That is on every standby's boot, so when the
+    default directory is not writable (a read-only home in a container)
+    the workers get a private one under the temp dir.  Returns the env to
+    add ({} when the default works or the operator chose)."""
+    environ = os.environ if environ is None else environ
+    if environ.get('AMD_COMGR_CACHE_DIR') or \
+            environ.get('AMD_COMGR_CACHE') == '0':
+        return {}
+    base = environ.get('XDG_CACHE_HOME') or os.path.join(
+        environ.get('HOME') or os.path.expanduser('~'), '.cache')
+    default = os.path.join(base, 'comgr')
+    try:
+        os.makedirs(default, exist_ok=True)
+        if os.access(default, os.W_OK | os.X_OK):
+            return {}
+    except OSError:
+        pass
+    fallback = os.path.join(tempfile.gettempdir(),
+                            'kiosk-comgr-%d' % os.getuid())
+    try:
+        os.makedirs(fallback, mode=0o700, exist_ok=True)
+    except OSError:
+        return {}
+    return {'AMD_COMGR_CACHE_DIR': fallback}
+
+
 def worker_env(settings, keys_per_pod=None):
     """Environment every worker of this autoscaler inherits."""
     env = {
@@ -63,6 +96,7 @@ def worker_env(settings, keys_per_pod=None):
     # standby measured (utils.hbm.size_from_free)
     env['HBM_PER_KEY_BYTES'] = settings.HBM_PER_KEY_BYTES
     env['HBM_FREE_RESERVE_BYTES'] = settings.HBM_FREE_RESERVE_BYTES
+    env.update(comgr_cache_env())
     # worker-side settings that are not autoscaler knobs: the engine
     # plug-in, per-key work shape, and test / debugging hooks
     for passthrough in ('WORKER_ENGINE', 'WORKER_IMPORT_TORCH',

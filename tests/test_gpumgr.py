@@ -1,6 +1,7 @@
 """GPU manager units: discovery, resource views, daemon transport, requeue,
 worker env pinning.  (End-to-end process tests: test_integration_cpu.py.)"""
 import os
+import tempfile
 import time
 
 import pytest
@@ -856,3 +857,25 @@ def test_sized_pool_retires_standbys_idle_beyond_demand():
     assert sent == [{'cmd': 'exit'}, {'cmd': 'exit'}]
     assert len(manager.retiring) == 2
     assert not manager._retire_excess(2, now=110.0)    # none idle long enough
+
+
+def test_workers_get_a_writable_comgr_cache(tmp_path):
+    """The HIP runtime's blit-kernel build is cached by comgr under the
+    home directory; with a read-only home the workers get a private cache
+    under the temp dir, and an operator's choice is left alone."""
+    from kiosk_autoscaler_amd.gpumgr import comgr_cache_env
+    home = tmp_path / 'home'
+    home.mkdir()
+    assert comgr_cache_env({'HOME': str(home)}) == {}
+    assert (home / '.cache' / 'comgr').is_dir()
+    # a home where ~/.cache cannot be a directory (stands in for a read-only
+    # one, which root would write anyway)
+    ro = tmp_path / 'ro'
+    ro.mkdir()
+    (ro / '.cache').write_text('not a directory')
+    env = comgr_cache_env({'HOME': str(ro)})
+    assert env['AMD_COMGR_CACHE_DIR'].startswith(tempfile.gettempdir())
+    assert os.path.isdir(env['AMD_COMGR_CACHE_DIR'])
+    assert comgr_cache_env({'HOME': str(ro), 'AMD_COMGR_CACHE_DIR': '/x'}) \
+        == {}
+    assert comgr_cache_env({'HOME': str(ro), 'AMD_COMGR_CACHE': '0'}) == {}
