@@ -102,6 +102,9 @@ def main():
     ap.add_argument('--kinds', default='native,torch,torch_rocm_comgr')
     ap.add_argument('--variants', default='default,cache_off,cache_dir')
     ap.add_argument('--repeat', type=int, default=3)
+    ap.add_argument('--gap', type=float, default=0.0,
+                    help='seconds between children (the previous one\'s '
+                         'teardown)')
     ap.add_argument('--cache-root', default='/tmp/comgr_probe')
     args = ap.parse_args()
     if args.child:
@@ -114,7 +117,10 @@ def main():
                 ('cache_off', {'AMD_COMGR_CACHE': '0'}),
                 ('cache_dir', {'AMD_COMGR_CACHE': '1',
                                'AMD_COMGR_CACHE_DIR': None}),
-                ('no_packet_capture', {'DEBUG_CLR_GRAPH_PACKET_CAPTURE': '0'})]
+                ('no_packet_capture', {'DEBUG_CLR_GRAPH_PACKET_CAPTURE': '0'}),
+                # context-creation knobs of the HSA runtime
+                ('sdma_off', {'HSA_ENABLE_SDMA': '0'}),
+                ('rocr_visible', {'ROCR_VISIBLE_DEVICES': '0'})]
     wanted = args.variants.split(',')
     for kind in args.kinds.split(','):
         for name, extra in variants:
@@ -134,7 +140,8 @@ def main():
                      kind], env=env, stdout=subprocess.PIPE, timeout=120,
                     check=True)
                 row = json.loads(out.stdout.decode().strip().splitlines()[-1])
-                row.update(kind=kind, variant=name, run=i)
+                row.update(kind=kind, variant=name, run=i, gap_s=args.gap)
+                time.sleep(args.gap)
                 if cache_dir:
                     row['cache_files'] = cache_files(cache_dir)
                 print(json.dumps(row), flush=True)
