@@ -103,7 +103,8 @@ def worker_env(settings, keys_per_pod=None):
                         'PASSES_PER_KEY', 'WORKER_BATCH', 'MODEL_SEED',
                         'JOB_IDLE_EXIT_S', 'POLL_BLOCK_S', 'WORKER_EVENTS',
                         'KIOSK_RCCL_LIB', 'KIOSK_FAULTS', 'KIOSK_ROCTX',
-                        'KIOSK_SHM_DIR', 'KIOSK_NATIVE', 'MOCK_WORK_MS',
+                        'KIOSK_SHM_DIR', 'KIOSK_NATIVE', 'KIOSK_TORCH_COMGR',
+                        'MOCK_WORK_MS',
                         'FAKE_RCCL_DIR', 'FAKE_RCCL_MODE',
                         'FAKE_RCCL_INIT_MS', 'FAKE_RCCL_LOAD_MS',
                         'WORKER_MAX_RECYCLES',

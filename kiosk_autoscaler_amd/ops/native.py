@@ -81,9 +81,11 @@ def prefer_rocm_comgr():
     ROCm's comgr caches the whole blit-kernel compile on disk
     (``AMD_COMGR_CACHE``, on by default), torch's 7.0 copy only its code
     generation: a torch process's first stream drops from ~85 ms to
-    ~20 ms.  No-op once torch is imported; returns the path mapped, or
-    None."""
-    if 'torch' in sys.modules:
+    ~20 ms.  No-op once torch is imported, or with
+    ``KIOSK_TORCH_COMGR=bundled`` (keep torch's copy); returns the path
+    mapped, or None."""
+    if 'torch' in sys.modules or \
+            os.environ.get('KIOSK_TORCH_COMGR') == 'bundled':
         return None
     try:
         ctypes.CDLL('libamd_comgr.so', mode=ctypes.RTLD_GLOBAL)

@@ -86,3 +86,10 @@ def test_rocm_comgr_replaces_torchs_bundled_copy():
     assert row['first'].startswith('/opt/rocm')
     assert row['again'] is None
     assert len(row['hip']) == 1 and 'torch' in row['hip'][0]
+
+
+def test_bundled_comgr_opt_out(monkeypatch):
+    from kiosk_autoscaler_amd.ops import native
+    monkeypatch.setenv('KIOSK_TORCH_COMGR', 'bundled')
+    monkeypatch.delitem(sys.modules, 'torch', raising=False)
+    assert native.prefer_rocm_comgr() is None
