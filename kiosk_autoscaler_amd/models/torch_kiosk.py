@@ -88,9 +88,9 @@ class TorchKioskEngine(object):
     def warm_device():
         """Standby boot (``worker/main.py``): torch's lazy CUDA init plus
         our launch handles -- no hipBLASLt handle (this engine never calls
-        a torch matmul) and no torch kernel: the engine clears its buffers
-        with ``hipMemsetAsync``, so no torch code object is loaded on the
-        boot path (profiles/r4_comgr)."""
+        a torch matmul) and no torch fill: the engine clears its buffers
+        with ``hipMemsetAsync`` (profiles/r4_comgr; torch's CUDAGraph
+        capture still issues four small int64 fills of its own)."""
         import torch
         torch.cuda.init()
         native.load().prepare_kernels()

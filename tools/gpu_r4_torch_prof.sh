@@ -3,7 +3,7 @@
 # (tools/profile_torch_engine.py): an unprofiled timing run, then the
 # kernel trace + stats.
 set -o pipefail
-OUT=gpurun_out/r4_torch_prof
+OUT=${OUT:-gpurun_out/r4_torch_prof}
 mkdir -p $OUT
 timeout -k 10 120 python tools/profile_torch_engine.py > $OUT/unprofiled.json \
     2> $OUT/unprofiled.err || { tail -20 $OUT/unprofiled.err; exit 1; }
