@@ -88,7 +88,8 @@ def ensure_built(kernels):
     sys.path.insert(0, os.path.join(ROOT, 'tools'))
     import build_native
     need = not os.path.exists(build_native.KREDIS) or (
-        kernels and not os.path.exists(build_native.EXT_PATH))
+        kernels and not (os.path.exists(build_native.EXT_PATH) and
+                         os.path.exists(build_native.RCCL_SLIM)))
     if need:
         log('building native components')
         build_native.build(jobs=8, kernels=kernels)
@@ -646,6 +647,12 @@ def _setting(name):
     return cast(value) if value not in (None, '') else default
 
 
+def _engine_name(backend):
+    from kiosk_autoscaler_amd.models import engine_name, engine_spec
+    spec = engine_spec(_setting('WORKER_ENGINE'), backend)
+    return engine_name(spec) if backend == 'hip' else (spec or 'cpu-mock')
+
+
 def base_line(args, episodes, elapsed):
     steps = len(episodes)
     return {
@@ -681,6 +688,9 @@ def base_line(args, episodes, elapsed):
             # scale.py runs with (environment, else the config default)
             'pool_idle_release_s': _setting('POOL_IDLE_RELEASE_S'),
             'pool_wake_poll_s': _setting('POOL_WAKE_POLL_S'),
+            # the engine the workers run (WORKER_ENGINE; torch-kiosk = the
+            # PyTorch-ROCm engine on our gfx950 kernels)
+            'engine': _engine_name(args.backend),
         },
         'steps_requested': args.steps,
     }
@@ -840,6 +850,22 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
                                       'gpu_mapping_mismatch'),
         'fence_transport': ','.join(fence['fence_transport']) or None,
         'fence_max_ranks': fence['fence_max_ranks'],
+        # READY -> first fence that agreed on the worker: how long the
+        # published set (available_replicas, kiosk:active) trailed READY
+        'fence_lag_mean_s': _r(summary['fence_lag']['fence_lag_mean_s']),
+        'fence_lag_max_s': _r(summary['fence_lag']['fence_lag_max_s']),
+        'fence_lag_unfenced': summary['fence_lag']['fence_lag_unfenced'],
+        'fence_lag_by_ranks': {
+            n: {k: _r(v) for k, v in row.items()}
+            for n, row in summary['fence_lag']['fence_lag_by_ranks'].items()},
+        'rccl_lib': rccl_lib_summary(events),
+        # per rank count: generations, RCCL's init breakdown, transport per
+        # peer (P2P = xGMI; others flagged), all-reduce time; the largest
+        # generation's rank -> slot / PCI device table
+        'rccl_generations': summary['generations'],
+        # what the workers actually ran (their READY warm-start reports)
+        'engines_seen': sorted({str(e.get('backend')) for e in events
+                                if e.get('ev') == 'warmstart'}),
         'fence': {k: _r(v) for k, v in fence.items()
                   if k not in ('fence_transport', 'fence_max_ranks')},
         # declared targets, multi-queue inflation, concurrent workers /
@@ -907,6 +933,20 @@ def start_util_sampler(n_gpus, bdfs=None):
     sampler = gpu_util.UtilSampler(0.1, bdfs or managed_bdfs(n_gpus))
     sampler.start()
     return sampler
+
+
+def rccl_lib_summary(events):
+    """Which RCCL the workers loaded (``rccl_lib`` event of the manager's
+    start): the one-ISA slim copy or the stock library, and why."""
+    last = None
+    for e in events:
+        if e.get('ev') == 'rccl_lib':
+            last = e
+    if last is None:
+        return None
+    return {'slim': last.get('slim'), 'cached': last.get('cached'),
+            'ms': _r(last.get('ms'), 1), 'error': last.get('error'),
+            'code_object_bytes': last.get('code_object_bytes')}
 
 
 def _r(value, nd=4):

@@ -22,6 +22,17 @@
 // FAKE_RCCL_MODE (read at each call): ok | init_error | init_hang |
 // allreduce_hang | finalize_hang.
 //
+// What grows with the rank count on a real node (bootstrap all-gathers, IPC
+// handle exchange, topology search) is modelled by FAKE_RCCL_INIT_PER_RANK_MS:
+// every init settles no sooner than nranks x that after it started, so an
+// 8-rank CPU rehearsal builds slower generations than a 1-rank one.  With
+// NCCL_DEBUG=INFO and NCCL_DEBUG_FILE (``%h`` / ``%p`` expanded) the fake
+// writes the INFO lines the node agent parses from the real library
+// (parallel/rccl_info.py): ``Init COMPLETE`` with a bus id, ``Init timings``,
+// the graph ``Pattern`` line and, at a communicator's first all-reduce (RCCL
+// connects lazily), one ``Channel`` line per ring peer, ``via`` the
+// transport named by FAKE_RCCL_TRANSPORT (default P2P/IPC).
+//
 // The device hold measured on MI355X (profiles/r4_collision) is modelled
 // too: a process-wide "HIP runtime lock" that RCCL holds while its fat
 // binary registers -- the first ncclGetUniqueId of the process, for
@@ -34,8 +45,11 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -45,6 +59,7 @@
 #include <string>
 #include <thread>
 
+#include <strings.h>
 #include <unistd.h>
 
 #include "runtime/shmcomm.hpp"
@@ -60,6 +75,13 @@ std::string mode() {
 
 struct FakeComm {
   std::unique_ptr<kiosk::ShmComm> shm;
+  int rank = 0;
+  int nranks = 1;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  std::chrono::steady_clock::time_point ready_at = t0;   // per-rank cost
+  long load_ms = 0;            // its code-object load (first comm only)
+  bool logged_init = false;
+  bool logged_channels = false;
   int polls_left = 3;        // ncclInProgress this many times, then settle
   std::atomic<bool> loading{false};   // its code-object load holds the lock
   bool init_fails = false;
@@ -97,6 +119,79 @@ std::atomic<int> g_loading_comms{0};   // comms whose code-object load runs
 long env_ms(const char* name) {
   const char* v = std::getenv(name);
   return v ? std::atol(v) : 0;
+}
+
+std::string busid(int rank) {
+  char buf[16];
+  std::snprintf(buf, sizeof(buf), "%x", 0x10000 * (rank + 1));
+  return buf;
+}
+
+// One INFO line to NCCL_DEBUG_FILE, in RCCL's format.
+void fake_log(const std::string& text) {
+  const char* level = std::getenv("NCCL_DEBUG");
+  const char* pattern = std::getenv("NCCL_DEBUG_FILE");
+  if (!level || !pattern || strcasecmp(level, "INFO") != 0) return;
+  char host[64] = {0};
+  gethostname(host, sizeof(host) - 1);
+  if (char* dot = std::strchr(host, '.')) *dot = '\0';   // RCCL's %h
+  std::string path;
+  for (const char* p = pattern; *p; ++p) {
+    if (p[0] == '%' && p[1] == 'h') {
+      path += host;
+      ++p;
+    } else if (p[0] == '%' && p[1] == 'p') {
+      path += std::to_string(getpid());
+      ++p;
+    } else {
+      path += *p;
+    }
+  }
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
+  if (FILE* f = std::fopen(path.c_str(), "a")) {
+    std::fprintf(f, "%s:%d:%d [0] NCCL INFO %s\n", host, getpid(),
+                 static_cast<int>(gettid()), text.c_str());
+    std::fclose(f);
+  }
+}
+
+void log_init_complete(FakeComm* c) {
+  using namespace std::chrono;
+  const double total =
+      duration<double>(steady_clock::now() - c->t0).count();
+  const double kernels = c->load_ms / 1e3;
+  char line[512];
+  std::snprintf(line, sizeof(line),
+                "ncclCommInitRankConfig_impl comm %p rank %d nranks %d "
+                "cudaDev 0 nvmlDev 0 busId %s commId 0x%llx - Init COMPLETE",
+                static_cast<void*>(c), c->rank, c->nranks,
+                busid(c->rank).c_str(),
+                static_cast<unsigned long long>(reinterpret_cast<uintptr_t>(c)));
+  fake_log(line);
+  std::snprintf(line, sizeof(line),
+                "Pattern 4, crossNic 0, nChannels 1, bw 40.000000/40.000000, "
+                "type XGMI/PIX, sameChannels 1");
+  fake_log(line);
+  std::snprintf(line, sizeof(line),
+                "Init timings - ncclCommInitRankConfig_impl: rank %d nranks %d "
+                "total %.2f (kernels %.2f, alloc 0.00, bootstrap %.2f, "
+                "allgathers 0.00, topo 0.00, graphs 0.00, connections 0.00, "
+                "rest 0.00)",
+                c->rank, c->nranks, total, kernels,
+                std::max(0.0, total - kernels));
+  fake_log(line);
+}
+
+void log_channels(FakeComm* c) {
+  if (c->nranks < 2) return;
+  const char* via = std::getenv("FAKE_RCCL_TRANSPORT");
+  const int peer = (c->rank + 1) % c->nranks;
+  char line[256];
+  std::snprintf(line, sizeof(line), "Channel 00/0 : %d[%s] -> %d[%s] via %s",
+                c->rank, busid(c->rank).c_str(), peer, busid(peer).c_str(),
+                via && *via ? via : "P2P/IPC");
+  fake_log(line);
 }
 
 void hold_runtime_lock(long ms) {
@@ -267,12 +362,17 @@ FAKE_API ncclResult_t ncclCommInitRankConfig(ncclComm_t* comm, int nranks,
   {
     std::lock_guard<std::mutex> lock(g_mu);
     c = new_comm(std::move(shm));
+    c->rank = rank;
+    c->nranks = nranks;
+    c->ready_at = c->t0 + std::chrono::milliseconds(
+                              env_ms("FAKE_RCCL_INIT_PER_RANK_MS") * nranks);
   }
   *comm = reinterpret_cast<ncclComm_t>(c);
   const long load_ms = env_ms("FAKE_RCCL_INIT_MS");
   if (load_ms > 0 && !g_kernels_loaded.exchange(true)) {
     // the first communicator of the process loads RCCL's code object on
     // RCCL's init thread, holding the runtime lock; the init settles after
+    c->load_ms = load_ms;
     c->loading = true;
     g_loading_comms++;
     std::thread([c, load_ms] {
@@ -296,8 +396,14 @@ FAKE_API ncclResult_t ncclCommGetAsyncError(ncclComm_t comm,
     *state = ncclInProgress;
   } else if (c->init_fails) {
     *state = ncclInvalidUsage;
+  } else if (std::chrono::steady_clock::now() < c->ready_at) {
+    *state = ncclInProgress;     // bootstrap cost, growing with nranks
   } else {
     *state = c->shm->poll_ready() ? ncclSuccess : ncclInProgress;
+    if (*state == ncclSuccess && !c->logged_init) {
+      c->logged_init = true;
+      log_init_complete(c);
+    }
   }
   return ncclSuccess;
 }
@@ -342,6 +448,10 @@ FAKE_API ncclResult_t ncclAllReduce(const void* send, void* recv,
   op.count = static_cast<int>(count);
   op.hang = mode() == "allreduce_hang";   // a peer that never joins
   std::lock_guard<std::mutex> lock(g_mu);
+  if (!c->logged_channels) {
+    c->logged_channels = true;    // RCCL connects at the first collective
+    log_channels(c);
+  }
   c->polls_left = 0;
   s->ops.push_back(op);
   progress(s);
@@ -362,6 +472,12 @@ FAKE_API ncclResult_t ncclCommShrink(ncclComm_t comm, int* excluded,
   } catch (const std::exception&) {
     return ncclInvalidArgument;
   }
-  *out = reinterpret_cast<ncclComm_t>(new_comm(std::move(child)));
+  FakeComm* next = new_comm(std::move(child));
+  int below = 0;
+  for (int i = 0; i < count; ++i) below += excluded[i] < c->rank;
+  next->rank = c->rank - below;
+  next->nranks = c->nranks - count;
+  next->logged_init = true;      // a shrink logs no init of its own
+  *out = reinterpret_cast<ncclComm_t>(next);
   return ncclInProgress;
 }

@@ -322,6 +322,110 @@ def fence_stats(events):
     }
 
 
+def generation_stats(events):
+    """Node-communicator generations by rank count, as RCCL reported them
+    (``node_comm_ready`` rank tables, ``node_comm_info`` per-rank
+    connections; parallel/rccl_info.py): how many, their init time and
+    RCCL's own phase breakdown, the transport per peer (``P2P`` = xGMI on
+    an MI355X node) with non-GPU peers and non-XGMI graph links counted,
+    and the fence all-reduce time at that rank count.  ``largest`` is the
+    last generation with the most ranks: rank -> slot, PCI device, bus id
+    and init breakdown."""
+    inits = [e for e in events if e.get('ev') == 'node_comm_ready' and
+             e.get('mode', 'init') != 'shrink']
+    infos = [e for e in events if e.get('ev') == 'node_comm_info']
+    fences = [e for e in events if e.get('ev') == 'fence_done']
+    by_n = collections.defaultdict(lambda: {
+        'count': 0, 'init_ms': [], 'phases': collections.defaultdict(list),
+        'transports': collections.Counter(), 'link_types': set(),
+        'non_gpu_peers': 0, 'non_xgmi_links': 0, 'allreduce_us': []})
+    for e in inits:
+        row = by_n[str(int(e.get('n') or 0))]
+        row['count'] += 1
+        row['init_ms'].append(float(e.get('init_ms') or 0.0))
+        for rank in e.get('ranks') or ():
+            for phase, ms in (rank.get('init') or {}).items():
+                row['phases'][phase].append(float(ms))
+    for e in infos:
+        row = by_n[str(int(e.get('n') or 0))]
+        row['transports'].update(e.get('transports') or {})
+        row['link_types'].update(e.get('link_types') or ())
+        row['non_gpu_peers'] += bool(e.get('non_gpu_peer'))
+        row['non_xgmi_links'] += bool(e.get('non_xgmi_links')) and \
+            int(e.get('n') or 0) > 1
+    for e in fences:
+        if e.get('allreduce_us') is not None:
+            by_n[str(int(e.get('n') or 0))]['allreduce_us'].append(
+                float(e['allreduce_us']))
+    out = {}
+    for n, row in sorted(by_n.items(), key=lambda kv: int(kv[0])):
+        if not row['count'] and not row['allreduce_us']:
+            continue
+        out[n] = {
+            'count': row['count'],
+            'init_ms_mean': _mean(row['init_ms']),
+            'init_ms_max': max(row['init_ms']) if row['init_ms'] else None,
+            'phases_ms_mean': {k: _mean(v) for k, v in
+                               sorted(row['phases'].items())},
+            'transports': dict(row['transports']),
+            'link_types': sorted(row['link_types']),
+            'non_gpu_peers': row['non_gpu_peers'],
+            'non_xgmi_links': row['non_xgmi_links'],
+            'allreduce_us_mean': _mean(row['allreduce_us']),
+        }
+    largest = None
+    if inits:
+        top = max(inits, key=lambda e: (int(e.get('n') or 0), e.get('t', 0)))
+        largest = {'gen': top.get('gen'), 'n': top.get('n'),
+                   'ranks': top.get('ranks') or []}
+    return {'by_ranks': out, 'largest': largest}
+
+
+def fence_lag(events, t_lo=None, t_hi=None):
+    """READY -> fenced: for every worker that came up (``worker_up``), the
+    time until the first completed fence whose agreed membership includes
+    it (``fence_done``), i.e. how long ``available_replicas`` and
+    ``kiosk:active`` trailed the worker's READY.  By
+    the rank count of that fence; workers that exited before any fence
+    included them are counted as ``unfenced``.  Only workers that came up
+    in [t_lo, t_hi] count (the timed cycles)."""
+    ups = {}
+    exits = {}
+    fences = []
+    for e in sorted(events, key=lambda e: e.get('t', 0)):
+        ev = e.get('ev')
+        if ev == 'worker_up' and (t_lo is None or t_lo <= e['t']) and \
+                (t_hi is None or e['t'] <= t_hi):
+            ups.setdefault(e.get('worker'), e['t'])
+        elif ev == 'worker_exit':
+            exits.setdefault(e.get('worker'), e['t'])
+        elif ev == 'fence_done' and e.get('members') is not None:
+            fences.append((e['t'], set(e.get('members') or ()),
+                           int(e.get('n') or 0)))
+    lags = []
+    by_n = collections.defaultdict(list)
+    unfenced = 0
+    for worker, t_up in ups.items():
+        hit = next(((t, n) for t, members, n in fences
+                    if t >= t_up and worker in members), None)
+        if hit is None or (worker in exits and hit[0] > exits[worker]):
+            unfenced += 1
+            continue
+        lag = (hit[0] - t_up) / 1e9
+        lags.append(lag)
+        by_n[str(hit[1])].append(lag)
+    return {
+        'fence_lag_mean_s': _mean(lags),
+        'fence_lag_p50_s': _pct(lags, 0.5),
+        'fence_lag_max_s': max(lags) if lags else None,
+        'fence_lag_count': len(lags),
+        'fence_lag_unfenced': unfenced,
+        'fence_lag_by_ranks': {
+            n: {'count': len(v), 'mean_s': sum(v) / len(v), 'max_s': max(v)}
+            for n, v in sorted(by_n.items())},
+    }
+
+
 def decision_stats(events):
     """What the policy declared and what ran (config 3): the
     largest target, the ticks whose target exceeded the keys they counted
@@ -388,6 +492,8 @@ def summarize(events, episodes):
         'keys': sum(p['keys'] for p in per),
         'keys_done': sum(p['keys_done'] for p in per),
         'fence': fence_stats(events),
+        'fence_lag': fence_lag(events, t_lo, t_hi),
+        'generations': generation_stats(events),
         'decisions': decision_stats(events),
         'episodes': per,
     }

@@ -153,6 +153,9 @@ EXTRA_DEFAULTS = (
     ('GPUMGR', str, 'embedded'),            # embedded | unix:<path> | k8s
     ('WORKER_MODULE', str, 'kiosk_autoscaler_amd.worker.main'),
     ('WORKER_BACKEND', str, 'auto'),        # auto | hip | cpu
+    # the model the workers serve: torch-kiosk (PyTorch-ROCm on our gfx950
+    # kernels) | builtin (torch-free) | torch-mlp | package.module:factory
+    ('WORKER_ENGINE', str, 'torch-kiosk'),
     # standby processes (-1 = MAX_PODS): HIP context, code objects, queue,
     # prebuilt engine, RCCL node communicator
     ('WARM_POOL', int, -1),
@@ -164,7 +167,7 @@ EXTRA_DEFAULTS = (
     # with POOL_IDLE_RELEASE_S: s between queue-length reads while no worker
     # runs; a new key refills a parked pool just before the scale-up tick
     # (the decision still waits for the tick; 0 = wake at the scale-up only)
-    ('POOL_WAKE_POLL_S', float, 0.05),
+    ('POOL_WAKE_POLL_S', float, 0.02),
     # auto (rccl with device standbys, shm otherwise; store on CPU) | rccl
     # | shm | store | gloo | none
     ('FENCE', str, 'auto'),

@@ -74,8 +74,9 @@ def comgr_cache_env(environ=None):
     return {'AMD_COMGR_CACHE_DIR': fallback}
 
 
-def worker_env(settings, keys_per_pod=None):
+def worker_env(settings, keys_per_pod=None, backend='hip'):
     """Environment every worker of this autoscaler inherits."""
+    from ..models import engine_spec
     env = {
         'REDIS_HOST': settings.REDIS_HOST, 'REDIS_PORT': settings.REDIS_PORT,
         'REDIS_INTERVAL': settings.REDIS_INTERVAL,
@@ -97,9 +98,16 @@ def worker_env(settings, keys_per_pod=None):
     env['HBM_PER_KEY_BYTES'] = settings.HBM_PER_KEY_BYTES
     env['HBM_FREE_RESERVE_BYTES'] = settings.HBM_FREE_RESERVE_BYTES
     env.update(comgr_cache_env())
+    # the engine (WORKER_ENGINE: torch-kiosk by default on GPU slots; ''
+    # selects the built-in engine, which the worker reads as unset)
+    # (the process environment wins, as for the other worker-side settings
+    # passed through below)
+    env['WORKER_ENGINE'] = engine_spec(
+        os.environ.get('WORKER_ENGINE',
+                       getattr(settings, 'WORKER_ENGINE', None)), backend)
     # worker-side settings that are not autoscaler knobs: the engine
     # plug-in, per-key work shape, and test / debugging hooks
-    for passthrough in ('WORKER_ENGINE', 'WORKER_IMPORT_TORCH',
+    for passthrough in ('WORKER_IMPORT_TORCH',
                         'PASSES_PER_KEY', 'WORKER_BATCH', 'MODEL_SEED',
                         'JOB_IDLE_EXIT_S', 'POLL_BLOCK_S', 'WORKER_EVENTS',
                         'KIOSK_RCCL_LIB', 'KIOSK_FAULTS', 'KIOSK_ROCTX',
@@ -118,11 +126,11 @@ def template_for(settings, backend=None, keys_per_pod=None):
     """The worker template (pod-template analog) of an autoscaler's
     resource, from its settings."""
     kpp = keys_per_pod or settings.KEYS_PER_POD
+    backend = backend or settings.WORKER_BACKEND
     return WorkerTemplate(queues=settings.queues,
                           module=settings.WORKER_MODULE,
-                          env=worker_env(settings, kpp),
-                          backend=backend or settings.WORKER_BACKEND,
-                          keys_per_pod=kpp)
+                          env=worker_env(settings, kpp, backend),
+                          backend=backend, keys_per_pod=kpp)
 
 
 def build_manager(settings, redis_client=None, events=None, slots=None,

@@ -298,6 +298,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                 if stale:
                     logger.warning('Removed %d stale node-communicator '
                                    'segment(s): %s', len(stale), stale)
+                self._configure_rccl()
             with self.lock:
                 self._start_zygote()
                 self._refill_pool()
@@ -305,6 +306,58 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                                             name='gpumgr', daemon=True)
             self._thread.start()
         return self
+
+    def _configure_rccl(self):
+        """Before the zygote and the first standby exist: point every worker
+        at the one-ISA copy of RCCL (``parallel/rccl_lib.py``), so a fresh
+        process's first generation does not inflate 5.3 GB of device code
+        for other GPUs (1.75 s -> 0.36 s on MI355X, profiles/r5_fence_lag).
+        Only for GPU slots with the RCCL transport; the fake-HIP CPU stack
+        keeps its own library."""
+        if os.environ.get('FENCE', 'auto') not in ('auto', 'rccl', '') or \
+                self.node.transport_override not in (None, 'rccl'):
+            return None
+        # (traced for the fake RCCL of the CPU stack too: same log lines)
+        self._configure_rccl_trace()
+        if os.environ.get('KIOSK_NATIVE') == 'fake' or \
+                not any(getattr(s, 'kind', 'gpu') == 'gpu'
+                        for s in self.slots):
+            return None      # the fake-HIP CPU stack keeps its own library
+        from ..parallel import rccl_lib
+        info = rccl_lib.configure(log=logger)
+        self.events.emit('rccl_lib', lib=info.get('lib'),
+                         slim=info.get('slim'), cached=info.get('cached'),
+                         ms=info.get('ms'), error=info.get('error'),
+                         code_object_bytes=info.get('slim_code_object_bytes'))
+        return info
+
+    def _configure_rccl_trace(self):
+        """Every worker's RCCL writes its INFO log to a file of its own
+        (``parallel/rccl_info.py``): its node agent reports RCCL's init
+        breakdown and the transport per peer of each generation
+        (``node_comm_ready`` / ``node_comm_info`` events).  The files go to
+        ``RCCL_TRACE_DIR`` (kept) or a temporary directory removed at stop;
+        ``RCCL_TRACE=0`` or an operator's own ``NCCL_DEBUG`` turns it off."""
+        from ..parallel import rccl_info
+        directory = os.environ.get('RCCL_TRACE_DIR')
+        temporary = not directory
+        try:
+            if temporary:
+                import tempfile
+                directory = tempfile.mkdtemp(prefix='kiosk-rccl-')
+            else:
+                os.makedirs(directory, exist_ok=True)
+        except OSError as err:
+            logger.warning('RCCL trace directory: %s', err)
+            return
+        env = rccl_info.trace_env(directory)
+        if not env:
+            if temporary:
+                os.rmdir(directory)
+            return
+        os.environ.update(env)
+        self._rccl_trace_env = env        # removed again at stop
+        self._rccl_trace_tmp = directory if temporary else None
 
     def _wake(self):
         try:
@@ -362,6 +415,16 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
             if self.zygote is not None:
                 self.zygote.close()
                 self.zygote = None
+        for name, value in (getattr(self, '_rccl_trace_env', None) or
+                            {}).items():
+            if os.environ.get(name) == value:
+                del os.environ[name]
+        self._rccl_trace_env = None
+        tmp = getattr(self, '_rccl_trace_tmp', None)
+        if tmp:
+            import shutil
+            shutil.rmtree(tmp, ignore_errors=True)
+            self._rccl_trace_tmp = None
 
     # ------------------------------------------------------------------
     # event loop body

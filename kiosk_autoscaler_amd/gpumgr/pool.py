@@ -459,18 +459,24 @@ class PoolMixin(object):
                 self._wake_at = min(self._wake_at, self._next_tick - lead)
         self._wake()
 
+    # margin of the wake lead over the slowest recent boot: the manager's
+    # loop wakes on time (``_loop`` sleeps to ``_wake_at``), so this covers
+    # the spawn request and the jitter of one boot, not a poll period
+    WAKE_MARGIN_S = 0.03
+
     def wake_lead(self):
         """Seconds before the next tick an arrival wakes a parked pool:
-        ``pool_wake_lead_s`` until woken standbys have been timed, then
-        1.5 x the slowest of the last 8 spawn -> booted+prebuilt times plus
-        50 ms and the arrival poll, at least 0.2 s, never above
-        ``pool_wake_lead_s`` (built-in worker: ~0.1-0.2 s -> 0.25-0.4 s;
-        PyTorch plug-in: ~0.55 s -> the cap)."""
+        ``pool_wake_lead_s`` until woken standbys have been timed, then the
+        slowest of the last 8 spawn -> booted+prebuilt times plus
+        ``WAKE_MARGIN_S``, never above ``pool_wake_lead_s``.  Every second
+        of lead beyond the boot is a standby holding its GPU unassigned
+        (the former 1.5 x max + 0.1 s, at least 0.2 s,
+        held ~0.15 s per wake); a boot slower than the 8 before it is late
+        by the difference once, then sets the lead."""
         cap = self.pool_wake_lead_s
         if cap <= 0 or not self._wake_boots:
             return cap
-        return min(cap, max(0.2, 1.5 * max(self._wake_boots) + 0.05 +
-                            self.pool_wake_poll_s))
+        return min(cap, max(self._wake_boots) + self.WAKE_MARGIN_S)
 
     def _prebuild_spec(self, template):
         """What an arrival-woken standby builds its engine for: the shape

@@ -50,7 +50,7 @@ logger = logging.getLogger('NodeFence')
 NODE_COMMANDS = ('comm_init', 'comm_uid', 'comm_shrink', 'comm_abort', 'fence',
                  'fence_abort', 'fence_commit')
 NODE_EVENTS = ('comm_uid', 'comm_ready', 'fenced', 'node_agent',
-               'node_preloaded')
+               'node_preloaded', 'comm_info')
 STORE_KEY = 'kiosk:nodefence:{uid}:{epoch}'
 
 
@@ -89,13 +89,27 @@ def _survivor_rank(rank, excluded):
 class RcclNodeTransport(object):
     name = 'rccl'
 
-    def __init__(self, timeout=60.0, native=None):
+    def __init__(self, timeout=60.0, native=None, trace=None):
         if native is None:
             from ..ops import native as native_ops
             native = native_ops.load()
         self.native = native
         self.timeout = float(timeout)
         self.comm = None
+        # this process's RCCL INFO log, when the manager routed it to a
+        # file (parallel/rccl_info.py): init breakdown, peer transports
+        if trace is None:
+            from .rccl_info import RcclTrace
+            trace = RcclTrace.for_process()
+        self.trace = trace
+
+    def info(self):
+        """What RCCL logged since the last call (parsed), or None."""
+        if self.trace is None:
+            return None
+        from .rccl_info import summary
+        parsed = self.trace.take()
+        return summary(parsed) if parsed is not None else None
 
     def make_uid(self, gen):
         return self.native.fence_unique_id().hex()
@@ -456,6 +470,11 @@ class NodeFenceAgent(object):
         # The worker gates its queue pulls on it (worker/runtime.py)
         self.agreed = {}
         self._results = {}    # seq -> (group, agreement) awaiting a commit
+        # seqs the manager committed before this rank stored their result:
+        # a commit can overtake the rank's own result (the reader thread
+        # handles ``fence_commit`` as soon as rank 0's report went out;
+        # ADVICE r4), so a result stored after its commit is promoted at once
+        self._early_commits = set()
         self.agreed_cv = threading.Condition()
         self._uids = {}
         self._uid_cv = threading.Condition()
@@ -585,11 +604,19 @@ class NodeFenceAgent(object):
             return
         self.gen, self.rank, self.nranks, self.sub = gen, rank, nranks, 0
         init_ms = (time.perf_counter() - t0) * 1e3
+        extra = {}
+        info = self._rccl_info()
+        if info:
+            extra['rccl'] = info
+        self._init_info = info or {}
+        # the peer transports are known after the first collective (RCCL
+        # connects lazily): reported then, once per generation
+        self._info_due = (gen, 0)
         self._emit('comm_ready', gen=gen, rank=rank, ok=True, init_ms=init_ms,
                    transport=self.transport.name, n=nranks, sub=0,
                    mode='init',
                    can_shrink=bool(getattr(self.transport, 'can_shrink',
-                                           False)))
+                                           False)), **extra)
 
     def _comm_shrink(self, message):
         gen, sub = int(message['gen']), int(message['sub'])
@@ -618,6 +645,38 @@ class NodeFenceAgent(object):
                    init_ms=(time.perf_counter() - t0) * 1e3,
                    transport=self.transport.name, n=self.nranks,
                    mode='shrink', can_shrink=True)
+
+    def _rccl_info(self):
+        hook = getattr(self.transport, 'info', None)
+        if not callable(hook):
+            return None
+        try:
+            return hook()
+        except Exception:  # pylint: disable=broad-except
+            return None
+
+    def _report_connections(self, report):
+        """After a generation's first successful all-reduce: what RCCL
+        connected (transport per peer, link types), to the manager."""
+        due = getattr(self, '_info_due', None)
+        if due is None or due != (report.get('gen'), report.get('sub', 0)):
+            return
+        self._info_due = None
+        info = self._rccl_info()
+        if info is None:
+            return
+        # the graph link types are logged at init, the connections now
+        init = getattr(self, '_init_info', None) or {}
+        links = list(init.get('link_types') or [])
+        links += [t for t in info.get('link_types') or () if t not in links]
+        if links:
+            info['link_types'] = links
+        if info.get('memory_bytes') is None and init.get('memory_bytes'):
+            info['memory_bytes'] = init['memory_bytes']
+        self._emit('comm_info', gen=report.get('gen'),
+                   sub=report.get('sub', 0), rank=report.get('rank'),
+                   n=report.get('n'), rccl=info,
+                   allreduce_us=report.get('allreduce_us'))
 
     def _drop(self):
         self.transport.close()
@@ -653,9 +712,15 @@ class NodeFenceAgent(object):
             # the agreed membership, read from this rank's own result
             mask = [i for i, bit in enumerate(result[1:]) if bit]
             seq = int(message.get('seq', 0))
+            entry = (message.get('group'), {'seq': seq, 'epoch': epoch,
+                                            'slots': mask})
             with self.agreed_cv:
-                self._results[seq] = (message.get('group'), {
-                    'seq': seq, 'epoch': epoch, 'slots': mask})
+                if seq in self._early_commits:
+                    # the commit arrived first: this result is published
+                    self._early_commits.discard(seq)
+                    self._promote(entry)
+                else:
+                    self._results[seq] = entry
         else:
             report['detail'] = 'got %s expected %s' % (result, expected)
         return report
@@ -667,13 +732,23 @@ class NodeFenceAgent(object):
             entry = self._results.pop(seq, None)
             for old in [k for k in self._results if k < seq]:
                 del self._results[old]
-            if entry is None:
+            if entry is not None:
+                self._promote(entry)
                 return
-            group, agreement = entry
-            current = self.agreed.get(group)
-            if current is None or current['seq'] < agreement['seq']:
-                self.agreed[group] = agreement
-                self.agreed_cv.notify_all()
+            self._early_commits.add(seq)
+            # bounded: a commit whose result never comes (a fence this rank
+            # skipped) is forgotten once much newer ones exist
+            for old in [k for k in self._early_commits if k < seq - 64]:
+                self._early_commits.discard(old)
+
+    def _promote(self, entry):
+        """(under ``agreed_cv``) a committed result becomes the group's
+        agreed membership unless a newer one already is."""
+        group, agreement = entry
+        current = self.agreed.get(group)
+        if current is None or current['seq'] < agreement['seq']:
+            self.agreed[group] = agreement
+            self.agreed_cv.notify_all()
 
     def agreement(self, group):
         """``{'seq', 'epoch', 'slots'}`` of the last fence of ``group`` this
@@ -724,6 +799,8 @@ class NodeFenceAgent(object):
             finally:
                 self.idle.set()
             self.completed.append(report)
+            if report.get('ok'):
+                self._report_connections(report)
             if self.events is not None:
                 self.events.emit('fence_rank', slot=self.slot, **report)
             if report.get('rank') == 0 or not report['ok']:

@@ -70,6 +70,32 @@ def _preload(backend):
     return time.monotonic_ns() - t0
 
 
+def _resolve_engine(backend):
+    """``WORKER_ENGINE`` may be an alias (``torch-kiosk``, ``builtin``)
+    when the manager did not know the backend: resolved here, before
+    anything reads it."""
+    value = os.environ.get('WORKER_ENGINE')
+    if value:
+        from ..models import engine_spec
+        os.environ['WORKER_ENGINE'] = engine_spec(value, backend)
+
+
+def _engine_collectives():
+    """Whether the engine runs collectives of its own: the built-in one
+    does not; a plug-in says so with a ``collectives`` attribute on its
+    factory (:class:`..models.torch_kiosk.TorchKioskEngine`: False),
+    assumed True when absent.  Only the factory's module is imported
+    (torch for a PyTorch engine, which the worker imports anyway)."""
+    spec = os.environ.get('WORKER_ENGINE')
+    if not spec:
+        return False
+    try:
+        from ..models.plugin import load_factory
+        return bool(getattr(load_factory(spec), 'collectives', True))
+    except Exception:  # pylint: disable=broad-except
+        return True
+
+
 def _imports_torch():
     """Torch before the native module (one HIP runtime per process):
     ``WORKER_IMPORT_TORCH``, default on for a ``WORKER_ENGINE`` plug-in
@@ -357,11 +383,13 @@ def main(argv=None):
     if backend == 'auto':
         backend = 'hip' if early and early.get('gpu') not in (None, '') \
             else 'cpu'
-    if backend == 'hip' and not os.environ.get('WORKER_ENGINE'):
+    _resolve_engine(backend)
+    if backend == 'hip' and not _engine_collectives():
         # the fence is this process's only RCCL user and moves 72 bytes: one
         # channel instead of RCCL's gfx950 default of 128 holds 166 MB of
         # HBM per communicator instead of 670 MB (profiles/r2_rccl_init);
-        # a plug-in engine may run collectives of its own: left alone
+        # an engine that runs collectives of its own (``collectives = True``
+        # on its factory, the default for a user plug-in) is left alone
         os.environ.setdefault('NCCL_MIN_NCHANNELS', '1')
         os.environ.setdefault('NCCL_MAX_NCHANNELS', '1')
     if early is not None:

@@ -120,6 +120,30 @@ def test_metrics_cold_starts_and_idle():
     assert summary['first_result_mean_s'] == pytest.approx(5.1)
 
 
+def test_fence_lag_ready_to_first_agreeing_fence():
+    """READY -> the first fence whose membership holds
+    the worker, per rank count; a worker that left unfenced is counted."""
+    events = [
+        _ev('worker_up', 1.0, worker='a'),
+        _ev('fence_done', 1.2, members=[], n=1),          # not its fence
+        _ev('fence_done', 1.6, members=['a'], n=1),
+        _ev('worker_up', 2.0, worker='b'),
+        _ev('worker_up', 2.1, worker='c'),
+        _ev('fence_done', 3.0, members=['a', 'b', 'c'], n=3),
+        _ev('worker_up', 5.0, worker='d'),
+        _ev('worker_exit', 5.5, worker='d'),
+        _ev('fence_done', 6.0, members=['d'], n=2),        # after its exit
+        _ev('worker_up', 9.0, worker='late'),              # outside window
+        _ev('fence_done', 9.1, members=['late'], n=1),
+    ]
+    lag = metrics.fence_lag(events, 0, int(8e9))
+    assert lag['fence_lag_count'] == 3 and lag['fence_lag_unfenced'] == 1
+    assert lag['fence_lag_max_s'] == pytest.approx(1.0)
+    assert lag['fence_lag_mean_s'] == pytest.approx((0.6 + 1.0 + 0.9) / 3)
+    assert lag['fence_lag_by_ranks']['1']['count'] == 1
+    assert lag['fence_lag_by_ranks']['3']['max_s'] == pytest.approx(1.0)
+
+
 def test_loadgen_writes_hash_before_key(redis_client):
     gen = LoadGenerator(redis_client, ['predict'], rate=50.0, service_ms=5,
                         seed=1)
@@ -199,7 +223,9 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
         default = dict((n, d) for n, _, d in EXTRA_DEFAULTS)
         assert line['config']['pool_idle_release_s'] == \
             default['POOL_IDLE_RELEASE_S']
-        assert line['config']['pool_wake_poll_s'] == 0.05
+        assert line['config']['pool_wake_poll_s'] == \
+            default['POOL_WAKE_POLL_S']
+        assert line['config']['engine'] == 'cpu-mock'
 
 
 def test_util_sampler_degrades_without_driver():

@@ -549,8 +549,8 @@ def test_arrival_wake_waits_for_the_lead_before_the_tick(resp_server):
         # the lead adapts to the woken standbys' measured boot (CPU: well
         # under the 0.4 s cap)
         until(lambda: len(manager._wake_boots) == 2)
-        assert manager.wake_lead() == min(0.4, max(
-            0.2, 1.5 * max(manager._wake_boots) + 0.05 + 0.02))
+        assert manager.wake_lead() == min(0.4, max(manager._wake_boots) +
+                                          manager.WAKE_MARGIN_S)
         # a woken standby that serves and is recycled is timed once, not
         # again (spawn -> recycled) when it reports as a standby after it
         manager.patch_namespaced_deployment('lead', 'default',

@@ -160,6 +160,33 @@ def test_agreement_gates_only_on_committed_fences():
     assert agent.close()
 
 
+def test_commit_that_overtakes_the_result_still_gates():
+    """the reader thread can handle ``fence_commit`` before the
+    agent thread stored that fence's result (rank 0's report goes out
+    first; a busy worker's agent lags).  The result is promoted when it
+    arrives; a later fence that is never committed still does not gate."""
+    native = _FakeNative(nranks_results=[[3, 0, 1] + [0] * 6])
+    chan = _Channel()
+    agent = NodeFenceAgent(0, nodefence.RcclNodeTransport(native=native),
+                           channel=chan)
+    agent.submit({'cmd': 'comm_init', 'gen': 1, 'rank': 0, 'nranks': 2})
+    assert chan.next('comm_ready')['ok']
+    agent.submit({'cmd': 'fence_commit', 'seq': 1})     # overtook the result
+    agent.submit({'cmd': 'fence', 'epoch': 3, 'seq': 1, 'gen': 1,
+                  'slots': [0, 1], 'width': 8, 'group': 'ns/r'})
+    assert chan.next('fenced')['ok']
+    wait_for(lambda: agent.agreement('ns/r') is not None)
+    assert agent.agreement('ns/r') == {'seq': 1, 'epoch': 3, 'slots': [0, 1]}
+    native.peers = [[4, 0, 0] + [0] * 6]
+    agent.submit({'cmd': 'fence', 'epoch': 4, 'seq': 2, 'gen': 1,
+                  'slots': [0], 'width': 8, 'group': 'ns/r'})
+    assert chan.next('fenced')['ok']
+    assert agent.agreement('ns/r')['seq'] == 1          # seq 2 not committed
+    agent.submit({'cmd': 'fence_commit', 'seq': 2})
+    assert agent.agreement('ns/r')['seq'] == 2
+    assert agent.close()
+
+
 def test_agent_non_root_waits_for_uid_and_aborts_cleanly():
     native = _FakeNative()
     chan = _Channel()
@@ -1281,12 +1308,14 @@ def test_sweep_stale_shm_segments(tmp_path):
 
 
 @pytest.mark.slow
-def test_arrival_woken_pool_builds_its_generation_after_ready(resp_server,
-                                                              tmp_path):
-    """A pool woken by a key's arrival builds no node communicator before
-    the scale-up it was woken for: a generation's init (seconds over RCCL)
-    would compete with the assignment's warm-start.  It is built once the
-    worker is READY, and the scale-up is fenced by it."""
+def test_arrival_woken_pool_builds_its_generation_before_the_scale_up(
+        resp_server, tmp_path):
+    """A pool woken by a key's arrival whose standby prebuilt its engine
+    builds the node communicator during the wake hold, before the tick that
+    scales: that standby's READY is graph launches alone, which a
+    generation's init never holds up (profiles/r4_collision), so the
+    scale-up is fenced as soon as it is READY instead of a whole init later
+    (VERDICT r4 weak 1).  One generation per wake, no regrow."""
     s, client, events, manager, scaler = _node_stack(
         resp_server, 'shm', tmp_path, MAX_PODS='2', WARM_POOL='2',
         POOL_IDLE_RELEASE_S='0.3', POOL_WAKE_POLL_S='0.02', INTERVAL='2')
@@ -1298,11 +1327,12 @@ def test_arrival_woken_pool_builds_its_generation_after_ready(resp_server,
         client.lpush('predict', 'predict:a')
         # one key: one standby (the pool is sized to the waiting keys)
         wait_for(lambda: len(manager.standbys) == 1 and all(
-            p.booted for p in manager.standbys.values()), timeout=60)
-        time.sleep(0.3)
+            p.booted and p.engine_cached
+            for p in manager.standbys.values()), timeout=60)
+        wait_for(lambda: manager.node.ready, timeout=30)
         assert len(manager.standbys) == 1
         later = events.records[parked_at:]
-        assert not [e for e in later if e['ev'] == 'node_comm_init']
+        assert [e for e in later if e['ev'] == 'node_comm_init']
         manager.patch_namespaced_deployment('worker', 'default',
                                             {'spec': {'replicas': 1}})
         wait_for(lambda: client.hget('predict:a', 'status') == 'done',
@@ -1312,7 +1342,10 @@ def test_arrival_woken_pool_builds_its_generation_after_ready(resp_server,
         later = events.records[parked_at:]
         ready = _index(later, lambda e: e['ev'] == 'worker_up')
         init = _index(later, lambda e: e['ev'] == 'node_comm_init')
-        assert ready is not None and init is not None and init > ready
+        fenced = _index(later, lambda e: e['ev'] == 'fence_done' and
+                        e.get('members'))
+        assert init < ready < fenced
+        assert len([e for e in later if e['ev'] == 'node_comm_init']) == 1
     finally:
         manager.stop(timeout=15)
 
@@ -1347,8 +1380,11 @@ def test_woken_pool_is_sized_to_the_waiting_keys(resp_server, tmp_path,
                                             {'spec': {'replicas': 2}})
         wait_for(lambda: _converged(manager, client) and
                  len(_ready_ids(manager)) == 2, timeout=60)
-        assert manager.node.ready and not manager.node.full
-        assert len(manager.node.members) == 3
+        # the woken pair's generation was built during the wake hold; the
+        # third process joins it by a regrow
+        wait_for(lambda: manager.node.ready and
+                 len(manager.node.members) == 3, timeout=30)
+        assert not manager.node.full
         # a fourth process joins the communicator by a regrow
         gens = manager.node.generations
         client.hset('predict:w3', mapping={'status': 'new', 'rows': 8,

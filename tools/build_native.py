@@ -30,6 +30,7 @@ HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 EXT = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
 EXT_PATH = os.path.join(ROOT, 'kiosk_autoscaler_amd', 'ops', '_kiosk_hip' + EXT)
 KREDIS = os.path.join(BUILD, 'kredis-server')
+RCCL_SLIM = os.path.join(BUILD, 'kiosk-rccl-slim')
 FAKE_DIR = os.path.join(BUILD, 'fake')
 FAKE_LIB = os.path.join(FAKE_DIR, 'libkiosk_fake_hip_rccl.so')
 FAKE_EXT = os.path.join(FAKE_DIR, '_kiosk_fence_cpu' + EXT)
@@ -147,6 +148,21 @@ def build_kredis(verbose=False, sanitize=False):
     return target
 
 
+def build_rccl_slim(verbose=False):
+    """``build/kiosk-rccl-slim`` (g++, host only): writes the one-ISA,
+    uncompressed, debug-stripped copy of RCCL the workers load
+    (``parallel/rccl_lib.py``; csrc/tools/rccl_slim.cpp has the why)."""
+    src = os.path.join(ROOT, 'csrc', 'tools', 'rccl_slim.cpp')
+    if not os.path.exists(src):
+        return None
+    os.makedirs(BUILD, exist_ok=True)
+    if _stale(RCCL_SLIM, [src]):
+        cxx = shutil.which('g++') or 'c++'
+        _run([cxx, '-O2', '-std=c++17', '-Wall', src, '-o', RCCL_SLIM,
+              '-ldl'], verbose)
+    return RCCL_SLIM
+
+
 def build_fake(verbose=False):
     """CPU build of the node-communicator bindings over the fake HIP + RCCL
     (host code only: g++, no hipcc, no GPU)."""
@@ -182,7 +198,8 @@ def build(verbose=False, clean=False, jobs=4, kernels=True, sanitize=False,
           fake=True):
     if clean and os.path.isdir(BUILD):
         shutil.rmtree(BUILD)
-    out = {'kredis': build_kredis(verbose)}
+    out = {'kredis': build_kredis(verbose),
+           'rccl_slim': build_rccl_slim(verbose)}
     if fake:
         out['fake_fence'] = build_fake(verbose)
     if sanitize:
