@@ -224,6 +224,10 @@ class Services(object):
             'EVENT_LOG': 'redis',
             'LOG_FILE': os.path.join(OUT_DIR, '%s_autoscaler.log' % tag),
             'JOB_IDLE_EXIT_S': '0.5',
+            # every worker's RCCL INFO log, kept with the run's files (the
+            # rccl_generations fields are parsed from them)
+            'RCCL_TRACE_DIR': env.get('RCCL_TRACE_DIR') or os.path.join(
+                OUT_DIR, 'rccl_%s' % tag),
             'PYTHONPATH': ROOT + os.pathsep + env.get('PYTHONPATH', ''),
         })
         if args.backend == 'cpu':
@@ -863,6 +867,9 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         # peer (P2P = xGMI; others flagged), all-reduce time; the largest
         # generation's rank -> slot / PCI device table
         'rccl_generations': summary['generations'],
+        # N5 / config 5: KEYS_PER_POD that fits the HBM the standbys measured
+        # free (last assignment), and the model's figure on a 288 GB MI355X
+        'hbm_sizing': hbm_sizing_summary(events, args),
         # what the workers actually ran (their READY warm-start reports)
         'engines_seen': sorted({str(e.get('backend')) for e in events
                                 if e.get('ev') == 'warmstart'}),
@@ -933,6 +940,24 @@ def start_util_sampler(n_gpus, bdfs=None):
     sampler = gpu_util.UtilSampler(0.1, bdfs or managed_bdfs(n_gpus))
     sampler.start()
     return sampler
+
+
+def hbm_sizing_summary(events, args):
+    from kiosk_autoscaler_amd.utils import hbm
+    last = None
+    for e in events:
+        if e.get('ev') == 'hbm_sizing':
+            last = e
+    model = hbm.report(args.dim, args.hidden, args.layers, args.rows,
+                       hbm_bytes=hbm.MI355X_HBM_BYTES)
+    return {'keys_per_pod_requested': (last or {}).get('requested'),
+            'keys_per_pod_used': (last or {}).get('keys_per_pod'),
+            'max_keys_per_pod_measured_free': (last or {}).get(
+                'max_keys_per_pod'),
+            'hbm_free_bytes': (last or {}).get('hbm_free'),
+            'max_keys_per_pod_288gb': model['max_keys_per_pod'],
+            'engine_bytes_one_key': model['engine_bytes_one_key'],
+            'per_key_bytes': model['per_key_bytes']}
 
 
 def rccl_lib_summary(events):

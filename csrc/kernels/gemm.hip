@@ -177,17 +177,17 @@ hipError_t launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C,
 }  // namespace
 
 // Raise the dynamic-LDS limits and resolve every launch handle once,
-// outside any graph capture (later calls return the first result: these
-// runtime calls take the registry lock, see launch.hpp).
+// outside any graph capture (once per device that succeeded: these runtime
+// calls take the registry lock, see launch.hpp).
 hipError_t gemm_prepare() {
-  static hipError_t result = [] {
+  static std::atomic<unsigned long long> done{0};
+  return prepare_per_device(done, [] {
     hipError_t err = configure_epi<EPI_NONE>();
     if (err == hipSuccess) err = configure_epi<EPI_BIAS_GELU>();
     if (err == hipSuccess) err = configure_epi<EPI_BIAS_RESIDUAL>();
     if (err == hipSuccess) err = gemm256_prepare();
     return err;
-  }();
-  return result;
+  });
 }
 
 int gemm_pick_variant(int M, int N, int K, bool have_workspace) {

@@ -17,6 +17,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstddef>
 #include <tuple>
 #include <type_traits>
@@ -24,10 +25,28 @@
 
 namespace kiosk {
 
-// hipFunction_t of a __global__ host stub; the first call per kernel asks
-// the runtime (under the registry lock), later ones hit a local cache.
-// nullptr if the kernel is unknown to the runtime.
+// hipFunction_t of a __global__ host stub on the current device; the first
+// call per (kernel, device) asks the runtime (under the registry lock),
+// later ones hit a local cache.  nullptr if the kernel is unknown to the
+// runtime.  (The handle is per device: a process that drives a second
+// device gets that device's)
 hipFunction_t resolve_kernel(const void* stub);
+
+// Runs `prepare` for the current device unless it already succeeded there:
+// a failure is not cached (the next call retries), and each device of the
+// process is prepared on its own.
+template <typename F>
+hipError_t prepare_per_device(std::atomic<unsigned long long>& done,
+                              F&& prepare) {
+  int device = 0;
+  hipError_t err = hipGetDevice(&device);
+  if (err != hipSuccess) return err;
+  const unsigned long long bit = 1ull << (device & 63);
+  if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
+  err = prepare();
+  if (err == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
+  return err;
+}
 
 namespace detail {
 

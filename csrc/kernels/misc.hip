@@ -158,7 +158,8 @@ hipError_t launch_spin(double ms, unsigned int* done, hipStream_t stream) {
 // querying attributes does it without a launch, so no hardware queue) and
 // resolves every kernel's launch handle.
 hipError_t misc_prepare() {
-  static hipError_t result = [] {
+  static std::atomic<unsigned long long> done{0};
+  return prepare_per_device(done, [] {
     hipFuncAttributes attr;
     hipError_t err = hipFuncGetAttributes(
         &attr, reinterpret_cast<const void*>(&init_bf16_kernel));
@@ -167,16 +168,20 @@ hipError_t misc_prepare() {
     if (err == hipSuccess) err = prepare_kernel(&partial_sums_kernel);
     if (err == hipSuccess) err = prepare_kernel(&spin_kernel);
     return err;
-  }();
-  return result;
+  });
 }
 
 namespace {
 
-// stub -> handle; a handful of kernels, looked up on every launch
+// (stub, device) -> handle; a handful of kernels, looked up on every launch
 struct KernelCache {
+  struct Entry {
+    const void* stub;
+    int device;
+    hipFunction_t f;
+  };
   std::mutex mu;
-  std::vector<std::pair<const void*, hipFunction_t>> entries;
+  std::vector<Entry> entries;
 };
 
 KernelCache& kernel_cache() {
@@ -187,18 +192,20 @@ KernelCache& kernel_cache() {
 }  // namespace
 
 hipFunction_t resolve_kernel(const void* stub) {
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) return nullptr;
   KernelCache& cache = kernel_cache();
   {
     std::lock_guard<std::mutex> lock(cache.mu);
     for (const auto& e : cache.entries) {
-      if (e.first == stub) return e.second;
+      if (e.stub == stub && e.device == device) return e.f;
     }
   }
   // outside our mutex: this call may wait on the runtime's registry lock
   hipFunction_t f = nullptr;
   if (hipGetFuncBySymbol(&f, stub) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lock(cache.mu);
-  cache.entries.emplace_back(stub, f);
+  cache.entries.push_back({stub, device, f});
   return f;
 }
 

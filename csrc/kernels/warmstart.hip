@@ -121,14 +121,14 @@ hipError_t launch_warmstart(const uint16_t* w, size_t n, uint32_t* record,
 }
 
 hipError_t warmstart_prepare() {
-  static hipError_t result = [] {
+  static std::atomic<unsigned long long> done{0};
+  return prepare_per_device(done, [] {
     hipError_t err = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&warmstart_kernel),
         hipFuncAttributeMaxDynamicSharedMemorySize, kGemmRingLdsBytes);
     if (err == hipSuccess) err = prepare_kernel(&warmstart_kernel);
     return err;
-  }();
-  return result;
+  });
 }
 
 }  // namespace kiosk

@@ -174,15 +174,24 @@ def standby_gpu(events, t_lo, t_hi):
     ``standby_ready`` and closes at the ``worker_assigned`` of the same pid
     (or the window end)."""
     open_at = {}
+    serving = set()     # pids assigned and not recycled since
     total = 0
     for e in sorted(events, key=lambda e: e.get('t', 0)):
         ev = e.get('ev')
         pid = e.get('pid')
         if ev == 'standby_ready' and (e.get('preinit') or e.get('recycled')):
+            if e.get('recycled'):
+                serving.discard(pid)
+            elif pid in serving:
+                # a booting standby the tick already assigned reports its
+                # boot after the assignment: it is a worker, not waiting
+                continue
             open_at.setdefault(pid, e['t'])
-        elif ev == 'worker_assigned' and pid in open_at:
-            start = open_at.pop(pid)
-            total += max(0, min(e['t'], t_hi) - max(start, t_lo))
+        elif ev == 'worker_assigned':
+            serving.add(pid)
+            if pid in open_at:
+                start = open_at.pop(pid)
+                total += max(0, min(e['t'], t_hi) - max(start, t_lo))
         elif ev == 'standby_exit' and pid in open_at:
             start = open_at.pop(pid)
             total += max(0, min(e['t'], t_hi) - max(start, t_lo))

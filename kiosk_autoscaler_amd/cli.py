@@ -139,6 +139,10 @@ def main(argv=None):
     settings = Settings()   # missing RESOURCE_NAME raises here (fatal)
     initialize_logger(debug_mode=settings.DEBUG, log_file=settings.LOG_FILE)
     _logger = logging.getLogger(__file__)
+    from .config import removed_knobs
+    for name, hint in removed_knobs():
+        _logger.warning('%s is set but no longer a setting of its own: %s.',
+                        name, hint)
     signal.signal(signal.SIGTERM, _on_sigterm)
     manager = None
     try:

@@ -61,6 +61,7 @@ logger = logging.getLogger('GpuManager')
 
 # pre-split names (tests, tools)
 _Process, _Pipe, _bare_worker = ManagedProcess, Pipe, bare_worker
+_EXIT = object()     # select() owner of a process's exit fd
 
 
 class Resource(object):
@@ -439,6 +440,14 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                 for worker in resource.workers.values():
                     if worker.state != EXITED and not worker.proc.eof:
                         fds[worker.proc.pipe.ev_r] = worker
+            # exit fds: a reaped process closes its own, so each wakes the
+            # loop once (the reap below runs on every pass)
+            procs = list(self.standbys.values()) + list(self.retiring) + [
+                w.proc for r in self.resources.values()
+                for w in r.workers.values() if w.state != EXITED]
+            for proc in procs:
+                if getattr(proc, 'pidfd', None) is not None:
+                    fds.setdefault(proc.pidfd, _EXIT)
         try:
             ready, _, _ = select.select(list(fds), [], [], timeout)
         except (OSError, ValueError):
@@ -446,6 +455,8 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
         with self.lock:
             for fd in ready:
                 owner = fds.get(fd)
+                if owner is _EXIT:
+                    continue              # reaped below
                 if owner is None:
                     try:
                         os.read(self._wake_r, 4096)
@@ -702,7 +713,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
         worker.exit_code = code
         worker.t_exit = time.monotonic_ns()
         if not recycled:
-            worker.proc.pipe.close()
+            worker.proc.close()
         del resource.workers[worker.id]
         self.history.append(worker.summary())
         self.events.emit('worker_exit', worker=worker.id, code=code,

@@ -47,8 +47,8 @@ class PoolMixin(object):
         self._wake_until = 0.0
         self.pool_wake_lead_s = float(pool_wake_lead_s or 0.0)
         self._next_tick = None    # monotonic instant of the next tick
-        # spawn -> booted+prebuilt of recent arrival-woken standbys: the
-        # lead adapts to it (1.5 x the slowest + 50 ms, capped by the knob)
+        # spawn request -> booted+prebuilt of recent arrival-woken standbys:
+        # the lead adapts to it (the slowest + WAKE_MARGIN_S, capped)
         self._wake_boots = collections.deque(maxlen=8)
         self._wake_at = None      # a deferred arrival wake
         self._next_arrival_check = 0.0
@@ -164,6 +164,10 @@ class PoolMixin(object):
         return z
 
     def _spawn(self, template, role, assign=None, slot=None):
+        # a boot is timed from the request, the zygote's fork included
+        # (~15 ms for a process that imported torch): what the wake lead
+        # must cover
+        t_request = time.monotonic_ns()
         cmd_r, cmd_w = os.pipe()
         ev_r, ev_w = os.pipe()
         args = ['--cmd-fd', str(cmd_r), '--ev-fd', str(ev_w),
@@ -224,6 +228,7 @@ class PoolMixin(object):
             os.close(cmd_r)
             os.close(ev_w)
         proc = ManagedProcess(popen, Pipe(cmd_w, ev_r), role)
+        proc.t_spawn = t_request
         proc.woken = woken
         proc.slot = slot.index if slot is not None else None
         proc.via = via
@@ -304,14 +309,19 @@ class PoolMixin(object):
 
     def _retire_excess(self, excess, now=None):
         """A pool sized to demand retires standbys it holds beyond its
-        target once they have waited a tick's hold (``pool_wake_hold_s``)
-        unassigned -- typically drained workers recycled mid-burst, which
-        would otherwise hold their GPU (context, engine) until the burst
-        ends.  Oldest-idle first; True if any was retired."""
+        target -- typically drained workers recycled mid-burst (a strict
+        policy's scale-down), which would otherwise hold their GPU
+        (context, engine) until the burst ends -- once they have waited one
+        boot time unassigned (the wake lead): a standby the demand comes
+        back for later is re-spawned, prebuilt, in that time, so holding
+        it any longer only holds its GPU (the former
+        tick-long hold kept 387 GPU-s of standbys at config 3 under
+        strict).  Oldest-idle first; True if any was retired."""
         if not self.pool_sized_to_demand() or excess <= 0:
             return False
         now = time.monotonic() if now is None else now
-        hold = max(self.pool_wake_hold_s, self.pool_idle_release_s)
+        hold = max(self.wake_lead() if self._wake_boots else
+                   self.pool_wake_lead_s, self.pool_idle_release_s)
         idle = sorted((proc.standby_since, index)
                       for index, proc in self.standbys.items()
                       if proc.booted and proc.standby_since is not None and
@@ -733,13 +743,13 @@ class PoolMixin(object):
         retired = False
         for index, proc in list(self.standbys.items()):
             if proc.popen.poll() is not None:
-                proc.pipe.close()
+                proc.close()
                 del self.standbys[index]
                 self.events.emit('standby_exit', pid=proc.pid, slot=index,
                                  code=proc.popen.returncode)
         for proc in list(self.retiring):
             if proc.popen.poll() is not None:
-                proc.pipe.close()
+                proc.close()
                 self.retiring.remove(proc)
                 self.events.emit('standby_exit', pid=proc.pid, slot=proc.slot,
                                  code=proc.popen.returncode, retired=True)

@@ -115,10 +115,30 @@ class ManagedProcess(object):
         self.woken = False      # spawned by an arrival wake (prebuilds)
         self.engine_cached = False  # standby holds a built engine
         self.standby_since = None   # monotonic s of its last 'standby'
+        # readable once the process has exited: the manager's loop wakes on
+        # it, so an exit is reaped (and its GPU time closed) at once rather
+        # than at the next 50 ms poll
+        self.pidfd = None
+        pidfd_open = getattr(os, 'pidfd_open', None)
+        if pidfd_open is not None and getattr(popen, 'pid', None):
+            try:
+                self.pidfd = pidfd_open(popen.pid)
+            except OSError:
+                self.pidfd = None
 
     @property
     def pid(self):
         return self.popen.pid
+
+    def close(self):
+        """Release the pipe and the exit fd (the process has exited)."""
+        self.pipe.close()
+        fd, self.pidfd = self.pidfd, None
+        if fd is not None:
+            try:
+                os.close(fd)
+            except OSError:
+                pass
 
 
 class Worker(object):

@@ -118,8 +118,7 @@ class CpuMlpEngine(object):
         from ..utils import hbm
         cfg = self.cfg
         rows = max(cfg.rows * cfg.batch, 256)
-        return hbm.model_bytes(cfg.dim, cfg.hidden, cfg.layers) + \
-            hbm.per_key_bytes(rows, cfg.dim, cfg.hidden)
+        return hbm.engine_bytes(cfg.dim, cfg.hidden, cfg.layers, rows)
 
     def forward(self, rows, passes, seed):
         import numpy as np
@@ -188,12 +187,14 @@ class HipMlpEngine(object):
         return info
 
     def hbm_bytes(self):
-        """Device bytes this engine holds (arena: weights + activations,
-        plus the split-K workspace)."""
+        """Device bytes this engine holds: its arena (weights, activations
+        and the split-K workspace, which the arena already contains -- it
+        was counted twice before round 5) plus the warm-start record."""
         if self.engine is None:
             return 0
+        from ..utils.hbm import WARM_RECORD_BYTES
         info = self.engine.info()
-        return int(info.get('arena_bytes', 0) + info.get('workspace_bytes', 0))
+        return int(info.get('arena_bytes', 0)) + WARM_RECORD_BYTES
 
     def measure(self, rows, passes=2):
         out = self.engine.forward(int(rows), passes, 0)

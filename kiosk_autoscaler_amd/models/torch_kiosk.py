@@ -126,8 +126,14 @@ class TorchKioskEngine(object):
         if stage:
             stage('stream_ready')
         rows, dim, hidden = self.max_rows, self.dim, self.hidden
-        ws = max(self.mod.gemm_workspace_bytes(rows, hidden, dim),
-                 self.mod.gemm_workspace_bytes(rows, dim, hidden))
+        # the split-K workspace any row count up to the capacity can want
+        # (the split count changes at 256-row steps; the built-in engine
+        # probes the same rows, so both arenas have one size, utils/hbm.py)
+        ws = 0
+        for m in range(256, rows + 256, 256):
+            m = min(m, rows)
+            ws = max(ws, self.mod.gemm_workspace_bytes(m, hidden, dim),
+                     self.mod.gemm_workspace_bytes(m, dim, hidden))
         self.workspace_bytes = ws
         f32, i32, i64 = torch.float32, torch.int32, torch.int64
         bf16 = torch.bfloat16

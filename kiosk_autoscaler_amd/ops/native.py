@@ -70,6 +70,52 @@ def _load_fake():
     return importlib.import_module('_kiosk_fence_cpu')
 
 
+def elf_soname(path):
+    """``DT_SONAME`` of an ELF64 shared library, or None."""
+    import struct
+    try:
+        with open(path, 'rb') as f:
+            head = f.read(64)
+            if head[:4] != b'\x7fELF' or head[4] != 2:
+                return None
+            shoff, = struct.unpack_from('<Q', head, 0x28)
+            shentsize, shnum = struct.unpack_from('<HH', head, 0x3a)
+            f.seek(shoff)
+            table = f.read(shentsize * shnum)
+            sections = [struct.unpack_from('<IIQQQQIIQQ', table, i * shentsize)
+                        for i in range(shnum)]
+            for sh in sections:
+                if sh[1] != 6:                    # SHT_DYNAMIC
+                    continue
+                f.seek(sh[4])
+                dyn = f.read(sh[5])
+                strtab = sections[sh[6]]
+                for off in range(0, len(dyn) - 15, 16):
+                    tag, val = struct.unpack_from('<qQ', dyn, off)
+                    if tag == 14:                 # DT_SONAME
+                        f.seek(strtab[4] + val)
+                        return f.read(256).split(b'\0')[0].decode()
+    except (OSError, IndexError, struct.error, UnicodeDecodeError):
+        return None
+    return None
+
+
+def comgr_abi_matches(torch_lib=None, rocm_lib='/opt/rocm/lib/libamd_comgr.so'):
+    """True when ROCm's comgr has the soname (ABI major) of the copy torch
+    bundles -- the one its HIP runtime was linked against.  Found without
+    importing torch (its package directory is located by name)."""
+    if torch_lib is None:
+        import importlib.util
+        spec = importlib.util.find_spec('torch')
+        if spec is None or not spec.submodule_search_locations:
+            return False
+        torch_lib = os.path.join(list(spec.submodule_search_locations)[0],
+                                 'lib', 'libamd_comgr.so')
+    ours, theirs = elf_soname(os.path.realpath(rocm_lib)), \
+        elf_soname(torch_lib)
+    return ours is not None and ours == theirs
+
+
 def prefer_rocm_comgr():
     """Map ROCm's ``libamd_comgr.so`` before torch loads its own.
 
@@ -81,11 +127,16 @@ def prefer_rocm_comgr():
     ROCm's comgr caches the whole blit-kernel compile on disk
     (``AMD_COMGR_CACHE``, on by default), torch's 7.0 copy only its code
     generation: a torch process's first stream drops from ~85 ms to
-    ~20 ms.  No-op once torch is imported, or with
-    ``KIOSK_TORCH_COMGR=bundled`` (keep torch's copy); returns the path
-    mapped, or None."""
+    ~20 ms.  No-op once torch is imported, with
+    ``KIOSK_TORCH_COMGR=bundled`` (keep torch's copy), or when ROCm's comgr
+    has another soname (ABI major) than torch's bundled one; returns the
+    path mapped, or None."""
     if 'torch' in sys.modules or \
             os.environ.get('KIOSK_TORCH_COMGR') == 'bundled':
+        return None
+    if not comgr_abi_matches():
+        # another comgr ABI than the one torch's HIP runtime was built
+        # against: keep torch's bundled copy (ADVICE r4)
         return None
     try:
         ctypes.CDLL('libamd_comgr.so', mode=ctypes.RTLD_GLOBAL)

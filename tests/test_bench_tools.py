@@ -144,6 +144,25 @@ def test_fence_lag_ready_to_first_agreeing_fence():
     assert lag['fence_lag_by_ranks']['3']['max_s'] == pytest.approx(1.0)
 
 
+def test_standby_time_of_a_standby_assigned_while_booting():
+    """A tick that assigns a standby still booting (a key that arrived
+    inside the wake lead) makes it a worker at once: its later boot report
+    must not open a standby interval (r5: one such report counted 5 s)."""
+    events = [
+        _ev('standby_ready', 0.0, pid=1, preinit={'x': 1}),
+        _ev('worker_assigned', 0.2, pid=1, worker='a'),
+        _ev('worker_recycled', 5.0, pid=1),
+        _ev('standby_ready', 5.0, pid=1, recycled=True),
+        _ev('standby_exit', 5.2, pid=1),
+        _ev('worker_assigned', 10.0, pid=2, worker='b'),     # before its boot
+        _ev('standby_ready', 10.05, pid=2, preinit={'x': 1}),
+        _ev('standby_ready', 15.0, pid=2, recycled=True),
+        _ev('standby_exit', 15.15, pid=2),
+    ]
+    assert metrics.standby_gpu(events, 0, int(20e9)) == pytest.approx(
+        0.2 + 0.2 + 0.15)
+
+
 def test_loadgen_writes_hash_before_key(redis_client):
     gen = LoadGenerator(redis_client, ['predict'], rate=50.0, service_ms=5,
                         seed=1)

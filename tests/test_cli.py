@@ -156,3 +156,44 @@ def test_max_pods_clamped_to_gpu_slots(resp_server):
         manager.stop(timeout=5)
         from kiosk_autoscaler_amd import gpumgr
         gpumgr.set_embedded(None)
+
+
+def test_worker_timeout_busy_and_start_bounds():
+    """the busy-progress bound and the assignment -> READY bound
+    are separate (``WORKER_TIMEOUT='busy[:start]'``); a busy bound alone
+    never kills a slow cold start; the round-3 ``START_TIMEOUT`` still sets
+    the start bound."""
+    def settings(**env):
+        base = {'RESOURCE_NAME': 'r'}
+        base.update(env)
+        return Settings(Config(environ=base, use_files=False))
+    s = settings(WORKER_TIMEOUT='30')
+    assert (s.WORKER_TIMEOUT, s.START_TIMEOUT) == (30.0, 0.0)
+    s = settings(WORKER_TIMEOUT='30:120')
+    assert (s.WORKER_TIMEOUT, s.START_TIMEOUT) == (30.0, 120.0)
+    s = settings(WORKER_TIMEOUT='30', START_TIMEOUT='90')
+    assert (s.WORKER_TIMEOUT, s.START_TIMEOUT) == (30.0, 90.0)
+    s = settings()
+    assert (s.WORKER_TIMEOUT, s.START_TIMEOUT) == (0.0, 0.0)
+
+
+def test_removed_knobs_are_reported():
+    from kiosk_autoscaler_amd.config import removed_knobs
+    found = dict(removed_knobs({'WARM_POOL_MODE': 'context',
+                                'START_TIMEOUT': '5', 'INTERVAL': '5',
+                                'MODEL_DIM': ''}))
+    assert sorted(found) == ['START_TIMEOUT', 'WARM_POOL_MODE']
+    assert 'busy:start' in found['START_TIMEOUT']
+
+
+def test_strict_policy_defaults_to_two_tick_hysteresis():
+    def settings(policy, interval='5'):
+        return Settings(Config(environ={'RESOURCE_NAME': 'r',
+                                        'SCALE_POLICY': policy,
+                                        'INTERVAL': interval},
+                               use_files=False))
+    assert settings('strict').SCALE_DOWN_DELAY == 5.0
+    assert settings('strict', '2').SCALE_DOWN_DELAY == 2.0
+    assert settings('strict:0').SCALE_DOWN_DELAY == 0.0
+    assert settings('strict:7.5').SCALE_DOWN_DELAY == 7.5
+    assert settings('reference').SCALE_DOWN_DELAY == 0.0

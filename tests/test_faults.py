@@ -79,7 +79,7 @@ def test_start_failure_and_start_timeout(stack):
 def test_slow_start_killed_by_start_timeout(stack):
     s, client, manager, scaler, events = stack(
         extra_env={'KIOSK_FAULTS': 'slow_start=60000'}, WARM_POOL='1',
-        WORKER_TIMEOUT='2.0')
+        WORKER_TIMEOUT='2.0:2.0')       # busy bound : start bound
     dead = _served_once_after_failure(s, client, manager, scaler, events)
     assert dead['killed'].startswith('not READY')
 

@@ -178,15 +178,22 @@ def test_connect_embedded():
 def test_hbm_sizing():
     from kiosk_autoscaler_amd.utils import hbm
     w = hbm.model_bytes(4096, 16384, 4)
-    assert w == 4 * (2 * 4096 * 16384 + 16384 + 4096) * 2
+    # bf16 matrices, fp32 biases (as the engine stores them)
+    assert w == 4 * (2 * 4096 * 16384 * 2 + 16384 * 4 + 4096 * 4)
     per = hbm.per_key_bytes(2048, 4096, 16384)
     limit = hbm.max_keys_per_pod(288 * 10 ** 9, w, per)
     assert limit > 1000          # 288 GB holds thousands of 2048-row keys
+    assert hbm.report(4096, 16384, 4, 2048,
+                      hbm_bytes=288 * 10 ** 9)['max_keys_per_pod'] > 1000
     assert hbm.size_keys_per_pod(4, 4096, 16384, 4, 2048,
                                  hbm_bytes=288 * 10 ** 9) == 4
-    # a tiny HBM forces a clamp (and never below 1)
+    # a tiny HBM forces a clamp (and never below 1): exactly the engine of
+    # three keys fits (weights, activations and split-K workspace)
+    three = hbm.engine_bytes(4096, 16384, 4, 3 * 2048)
     assert hbm.size_keys_per_pod(64, 4096, 16384, 4, 2048,
-                                 hbm_bytes=w + (8 << 30) + 3 * per) == 3
+                                 hbm_bytes=three + (8 << 30)) == 3
+    assert hbm.size_keys_per_pod(64, 4096, 16384, 4, 2048,
+                                 hbm_bytes=three + (8 << 30) - 1) == 2
     assert hbm.size_keys_per_pod(64, 4096, 16384, 4, 2048, hbm_bytes=1) == 1
     assert os.getpid() == hbm.report(8, 16, 1, 2)['pid']
 
@@ -831,15 +838,18 @@ def test_deep_idle_standby_target_follows_waiting_keys():
 
 def test_sized_pool_retires_standbys_idle_beyond_demand():
     """A deep-idle pool sized to demand retires the standbys it holds beyond
-    its target once they waited a tick's hold unassigned (drained workers
-    recycled mid-burst), oldest first -- never a resident pool's, never one
-    still booting or idle for less than the hold."""
+    its target once they waited one boot time (the wake lead) unassigned --
+    drained workers recycled mid-burst, which a tick-long hold kept for
+    seconds -- oldest first; never a resident pool's,
+    never one still booting or idle for less than that."""
     import types
     from kiosk_autoscaler_amd.gpumgr.controller import GpuManager
     slots = [gpus.GpuSlot(i, str(i)) for i in range(4)]
     tpl = gpumgr.WorkerTemplate(queues=['q'], backend='cpu')
     manager = GpuManager(slots, pool_size=4, pool_template=tpl,
-                         pool_idle_release_s=0.5, pool_wake_hold_s=8.5)
+                         pool_idle_release_s=0.01, pool_wake_hold_s=8.5,
+                         pool_wake_lead_s=0.75)
+    manager._wake_boots.extend([0.10, 0.12])      # lead 0.15 s
     sent = []
 
     def proc(since, booted=True):
@@ -847,16 +857,18 @@ def test_sized_pool_retires_standbys_idle_beyond_demand():
             booted=booted, standby_since=since,
             popen=types.SimpleNamespace(poll=lambda: None),
             pipe=types.SimpleNamespace(send=sent.append))
-    manager.standbys = {0: proc(100.0), 1: proc(95.0), 2: proc(109.0),
+    manager.standbys = {0: proc(109.5), 1: proc(109.0), 2: proc(109.95),
                         3: proc(None, booted=False)}
     assert not manager._retire_excess(2, now=110.0)    # boot pool: resident
     manager.pool_parks = 1
+    assert manager.wake_lead() == pytest.approx(0.15)
     assert manager._retire_excess(2, now=110.0)
-    # 1 (idle 15 s) then 0 (10 s); 2 (1 s) and the booting 3 stay
+    # 1 (idle 1 s) then 0 (0.5 s); 2 (50 ms) and the booting 3 stay
     assert sorted(manager.standbys) == [2, 3]
     assert sent == [{'cmd': 'exit'}, {'cmd': 'exit'}]
     assert len(manager.retiring) == 2
     assert not manager._retire_excess(2, now=110.0)    # none idle long enough
+    assert manager._retire_excess(2, now=110.2)        # a boot time later
 
 
 def test_workers_get_a_writable_comgr_cache(tmp_path):

@@ -193,3 +193,74 @@ def test_arrival_rebuilds_a_released_engine(stack):
     view = manager.list_namespaced_deployment('default').items[0]
     assert view.spec.replicas == 0
     assert manager.standbys[0].engine_cached
+
+
+def test_engine_bytes_mirror_the_arena():
+    """the model counts the engine's arena byte for byte
+    -- bf16 matrices, fp32 biases, x / y / h, partial sums, seed word, the
+    split-K workspace of every row count up to the capacity, 256-B aligned
+    -- plus the warm-start record.  The benchmark model at 2048 rows: its
+    down-projection splits K in four below 2048 rows (117 MB of fp32
+    partial planes at 1792 rows)."""
+    assert hbm.splitk_splits(1792, 4096, 16384) == 4
+    assert hbm.splitk_splits(2048, 16384, 4096) == 1
+    assert hbm.workspace_bytes(2048, 4096, 16384) == 117441024
+    total = hbm.engine_bytes(4096, 16384, 4, 2048)
+    assert total == 1292178176 + hbm.WARM_RECORD_BYTES
+    # the split-K arithmetic matches the kernels' own (native module, no GPU
+    # needed to ask it)
+    from kiosk_autoscaler_amd.ops import native
+    if not native.extension_candidates():
+        pytest.skip('_kiosk_hip not built')
+    mod = native.load(torch_first=False)
+    for m in (256, 300, 1024, 1536, 1792, 2048, 4096):
+        for n, k in ((16384, 4096), (4096, 16384), (1024, 4096)):
+            assert mod.gemm_workspace_bytes(m, n, k) == \
+                hbm.splitk_workspace_bytes(m, n, k), (m, n, k)
+
+
+def test_max_keys_per_pod_on_288_gb():
+    row = hbm.report(4096, 16384, 4, 2048, hbm_bytes=288 * 10 ** 9)
+    # (288 GB - 8 GiB reserve - 1.07 GB weights - workspace) / 100.7 MB
+    assert 2700 < row['max_keys_per_pod'] < 2800
+    kpp = row['max_keys_per_pod']
+    assert hbm.engine_bytes(4096, 16384, 4, kpp * 2048) <= \
+        288 * 10 ** 9 - (8 << 30) < \
+        hbm.engine_bytes(4096, 16384, 4, (kpp + 1) * 2048)
+
+
+@pytest.mark.gpu
+def test_gpu_engine_footprint_matches_the_model():
+    """the predicted footprint of the benchmark model's
+    engine (2048-row capacity) against what hipMemGetInfo says a build
+    took, within 2 %, for the built-in engine and the PyTorch one."""
+    import torch
+    from kiosk_autoscaler_amd.models.torch_kiosk import TorchKioskEngine
+    from kiosk_autoscaler_amd.ops import native
+    from kiosk_autoscaler_amd.worker.runtime import WorkerConfig
+    mod = native.load()
+    mod.preinit_device(0)
+    predicted = hbm.engine_bytes(4096, 16384, 4, 2048)
+    torch.cuda.synchronize()
+    free0, _ = mod.mem_info()
+    engine = mod.Engine(0, 4096, 16384, 4, 2048, 1)
+    engine.warmstart()
+    mod.synchronize()
+    free1, _ = mod.mem_info()
+    used = free0 - free1
+    engine.close()
+    assert abs(used - predicted) <= 0.02 * predicted, (used, predicted)
+    cfg = WorkerConfig({'MODEL_DIM': '4096', 'MODEL_HIDDEN': '16384',
+                        'MODEL_LAYERS': '4', 'ROWS_PER_KEY': '2048'},
+                       {'worker_id': 'hbm'})
+    torch.cuda.synchronize()
+    free0, _ = mod.mem_info()
+    eng = TorchKioskEngine(cfg)
+    eng.warmstart()
+    torch.cuda.synchronize()
+    free1, _ = mod.mem_info()
+    used_torch = free0 - free1
+    assert eng.hbm_bytes() + hbm.WARM_RECORD_BYTES >= predicted - 4096
+    eng.close()
+    assert abs(used_torch - predicted) <= 0.02 * predicted, (used_torch,
+                                                             predicted)

@@ -16,7 +16,7 @@ DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data')
 def test_parse_captured_mi355x_generation():
     """A 1-rank generation on MI355X with the slim RCCL
     (profiles/r5_fence_lag): RCCL's init breakdown and bus id."""
-    with open(os.path.join(DATA, 'rccl_info_mi355x_1rank.log')) as f:
+    with open(os.path.join(DATA, 'rccl_info_mi355x_1rank.txt')) as f:
         info = rccl_info.parse(f.read())
     assert info['version'].startswith('2.27.7')
     assert (info['rank'], info['nranks'], info['bus_id']) == (0, 1, '75000')
@@ -29,15 +29,10 @@ def test_parse_captured_mi355x_generation():
     assert info['channels'] == [] and info['non_gpu_peer'] == []
 
 
-EIGHT_RANKS = """\
-h:1:2 [0] NCCL INFO Pattern 4, crossNic 0, nChannels 1, bw 40.000000/40.000000, type XGMI/PIX, sameChannels 1
-h:1:2 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC/read
-h:1:2 [0] NCCL INFO Channel 00/0 : 7[7] -> 0[0] via P2P/IPC/read
-h:1:2 [0] NCCL INFO Channel 01/1 : 0[0] -> 1[1] via P2P/IPC
-h:1:2 [0] NCCL INFO Channel 00 : 0[0] -> 4[4] via SHM/direct/direct
-h:1:2 [0] NCCL INFO Channel 00/0 : 0[75000] -> 2[85000] [send] via NET/Socket/0
-h:1:2 [0] NCCL INFO Init timings - ncclCommInitRankConfig_impl: rank 0 nranks 8 total 1.25 (kernels 0.28, alloc 0.03, bootstrap 0.40, allgathers 0.30, topo 0.10, graphs 0.04, connections 0.05, rest 0.05)
-"""
+# RCCL's channel / graph / timing lines for one rank of an 8-rank
+# generation, with one SHM and one NET peer to flag (format of RCCL 2.27)
+with open(os.path.join(DATA, 'rccl_info_peer_sample.txt')) as _f:
+    EIGHT_RANKS = _f.read()
 
 
 def test_parse_peer_transports_and_flags():

@@ -93,3 +93,27 @@ def test_bundled_comgr_opt_out(monkeypatch):
     monkeypatch.setenv('KIOSK_TORCH_COMGR', 'bundled')
     monkeypatch.delitem(sys.modules, 'torch', raising=False)
     assert native.prefer_rocm_comgr() is None
+
+
+def test_rocm_comgr_preferred_only_with_torchs_abi(tmp_path):
+    """ROCm's comgr replaces torch's bundled copy only when both
+    carry the same soname (comgr ABI major) -- another ROCm / torch pair
+    keeps the bundled one."""
+    import subprocess
+    from kiosk_autoscaler_amd.ops import native
+    src = tmp_path / 'c.c'
+    src.write_text('int amd_comgr_x(void) { return 3; }\n')
+
+    def lib(name, soname):
+        out = tmp_path / name
+        subprocess.run(['gcc', '-shared', '-fPIC', str(src), '-o', str(out),
+                        '-Wl,-soname,' + soname], check=True)
+        return str(out)
+    rocm3 = lib('rocm3.so', 'libamd_comgr.so.3')
+    torch3 = lib('torch3.so', 'libamd_comgr.so.3')
+    torch2 = lib('torch2.so', 'libamd_comgr.so.2')
+    assert native.elf_soname(rocm3) == 'libamd_comgr.so.3'
+    assert native.comgr_abi_matches(torch_lib=torch3, rocm_lib=rocm3)
+    assert not native.comgr_abi_matches(torch_lib=torch2, rocm_lib=rocm3)
+    assert not native.comgr_abi_matches(torch_lib=str(tmp_path / 'none'),
+                                        rocm_lib=rocm3)
