@@ -43,6 +43,11 @@ class Autoscaler(object):
         policy: ``'reference'`` (bit-compatible) or ``'strict'``.
         scale_down_delay: seconds a lower target must persist before a
             scale-down is applied (``strict`` hysteresis; 0 = immediate).
+        zero_delay: seconds a target of zero must persist before the last
+            workers are scaled away (``strict``'s default hysteresis: a
+            transient empty queue mid-burst would otherwise make the next
+            key pay a cold start; scale-downs that keep workers are
+            immediate).
         events: optional :class:`~kiosk_autoscaler_amd.utils.EventLog`.
         tally: ``'reference'`` (``LLEN`` on a replica, then a ``SCAN`` of
             the master: two non-atomic reads, SURVEY §5.2, so an item a
@@ -54,7 +59,7 @@ class Autoscaler(object):
     def __init__(self, redis_client, queues='predict', queue_delim=',',
                  actuator=None, policy='reference', scale_down_delay=0.0,
                  events=None, clock=timeit.default_timer,
-                 tally='reference'):
+                 tally='reference', zero_delay=0.0):
         self.redis_keys = {q: 0 for q in queues.split(queue_delim)}
         self.in_progress = {q: 0 for q in self.redis_keys}
         # distinct workers holding processing keys (a batched worker holds
@@ -68,6 +73,7 @@ class Autoscaler(object):
             raise ValueError('unknown policy %r' % policy)
         self.policy = policy
         self.scale_down_delay = float(scale_down_delay)
+        self.zero_delay = float(zero_delay)
         self.events = events if events is not None else NULL_EVENTS
         self._clock = clock
         self._lower_since = None
@@ -253,11 +259,18 @@ class Autoscaler(object):
         desired = policies.decide(
             self.redis_keys, min_pods, max_pods, keys_per_pod, current_pods,
             policy=self.policy, busy=len(self.busy_workers))
-        if desired < current_pods and self.scale_down_delay > 0:
+        delay = self.scale_down_delay
+        if desired == 0:
+            delay = max(delay, self.zero_delay)
+        if desired < current_pods and delay > 0:
             now = self._clock()
             if self._lower_since is None:
                 self._lower_since = now
-            if now - self._lower_since < self.scale_down_delay:
+            if now - self._lower_since < delay:
+                # (a drop to zero still held: keep the workers but let a
+                # lower non-zero target through at once)
+                if desired == 0 and self.scale_down_delay <= 0:
+                    return max(1, min(current_pods, desired or 1))
                 return current_pods
         else:
             self._lower_since = None

@@ -86,6 +86,8 @@ def build(settings=None, redis_client=None, actuator=None, events=None):
                         queue_delim=settings.QUEUE_DELIMITER,
                         actuator=actuator, policy=settings.policy,
                         scale_down_delay=settings.SCALE_DOWN_DELAY,
+                        zero_delay=getattr(settings, 'SCALE_TO_ZERO_DELAY',
+                                           0.0),
                         events=events, tally=settings.TALLY_MODE)
     return redis_client, scaler, manager
 

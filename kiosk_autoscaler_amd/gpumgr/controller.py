@@ -352,13 +352,23 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
             logger.warning('RCCL trace directory: %s', err)
             return
         env = rccl_info.trace_env(directory)
+        self.events.emit('rccl_trace', dir=directory if env else None,
+                         nccl_debug=os.environ.get('NCCL_DEBUG'),
+                         nccl_debug_file=os.environ.get('NCCL_DEBUG_FILE'),
+                         rccl_trace=os.environ.get('RCCL_TRACE'))
         if not env:
+            logger.info('RCCL INFO logs not traced (NCCL_DEBUG=%s, '
+                        'NCCL_DEBUG_FILE=%s, RCCL_TRACE=%s).',
+                        os.environ.get('NCCL_DEBUG'),
+                        os.environ.get('NCCL_DEBUG_FILE'),
+                        os.environ.get('RCCL_TRACE'))
             if temporary:
                 os.rmdir(directory)
             return
         os.environ.update(env)
         self._rccl_trace_env = env        # removed again at stop
         self._rccl_trace_tmp = directory if temporary else None
+        logger.info('RCCL INFO logs of every worker: %s', directory)
 
     def _wake(self):
         try:
@@ -369,10 +379,12 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
     def _loop(self):
         while not self._stop.is_set():
             timeout = 0.05
-            wake_at = self._wake_at
-            if wake_at is not None:
-                # a deferred arrival wake is due: do not sleep past it
-                timeout = min(timeout, max(0.001, wake_at - time.monotonic()))
+            for due in (self._wake_at, self._spawn_at):
+                if due is not None:
+                    # a deferred arrival wake / standby spawn: do not sleep
+                    # past it
+                    timeout = min(timeout, max(0.001,
+                                               due - time.monotonic()))
             self.poll(timeout)
 
     def stop(self, timeout=10.0):

@@ -51,6 +51,7 @@ class PoolMixin(object):
         # the lead adapts to it (the slowest + WAKE_MARGIN_S, capped)
         self._wake_boots = collections.deque(maxlen=8)
         self._wake_at = None      # a deferred arrival wake
+        self._spawn_at = None     # a deferred standby spawn (awake pool)
         self._next_arrival_check = 0.0
         # queue -> length at the last check; reset to empty when demand
         # ends (a scale to zero implies empty queues, stranded keys aside),
@@ -253,10 +254,13 @@ class PoolMixin(object):
             return
         have = len(self.standbys)
         free = self._free_slots()[:self.pool_size]
-        target = self._standby_target(time.monotonic(), have, len(free))
+        now = time.monotonic()
+        target = self._standby_target(now, have, len(free))
         if have > target and self._retire_excess(have - target):
             changed = True
             have = len(self.standbys)
+        if target > have and not self._spawn_due(now):
+            target = have      # spawned one boot time before the tick
         for slot in free:
             if have >= target:
                 break
@@ -306,6 +310,25 @@ class PoolMixin(object):
             self._next_waiting_check = 0.0
             target = need()
         return target
+
+    def _spawn_due(self, now):
+        """Whether a standby for waiting keys is spawned now.  An awake
+        pool sized to demand spawns it one wake lead before the tick that
+        can assign it, like the arrival wake of a parked pool: spawned at
+        once, it would hold its GPU (context, prebuilt engine) unassigned
+        for the rest of the tick phase -- 2.5 s on average, 163 GPU-s at
+        config 3 under strict (profiles/r5_config3).  ``_spawn_at`` is when
+        it becomes due (the manager's loop wakes for it)."""
+        self._spawn_at = None
+        if not self.pool_sized_to_demand() or self._next_tick is None or \
+                now < self._wake_until:
+            return True
+        lead = self.wake_lead()
+        due = self._next_tick - lead
+        if now >= due or self._next_tick <= now:
+            return True
+        self._spawn_at = due
+        return False
 
     def _retire_excess(self, excess, now=None):
         """A pool sized to demand retires standbys it holds beyond its

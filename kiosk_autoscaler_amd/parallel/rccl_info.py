@@ -112,12 +112,16 @@ def summary(parsed):
 
 def trace_env(directory, environ=None):
     """The NCCL_DEBUG settings that send each worker's RCCL INFO log to a
-    file of its own under ``directory`` (``{}`` when the operator set
-    ``NCCL_DEBUG`` / ``NCCL_DEBUG_FILE`` or ``RCCL_TRACE=0``)."""
+    file of its own under ``directory``.  ``{}`` with ``RCCL_TRACE=0``, or
+    when the operator already has RCCL's INFO output (``NCCL_DEBUG=INFO``)
+    or a log file (``NCCL_DEBUG_FILE``); a quieter ``NCCL_DEBUG`` (e.g.
+    ``WARN``) is raised to INFO into the files (its warnings land there)."""
     environ = os.environ if environ is None else environ
     if str(environ.get('RCCL_TRACE', '1')).lower() in ('0', 'false', 'off',
                                                        'no') or \
-            environ.get('NCCL_DEBUG') or environ.get('NCCL_DEBUG_FILE'):
+            environ.get('NCCL_DEBUG_FILE') or \
+            str(environ.get('NCCL_DEBUG', '')).upper() in ('INFO', 'TRACE'):
+        # off, or the operator already routes (or reads) RCCL's INFO output
         return {}
     return {'NCCL_DEBUG': 'INFO', 'NCCL_DEBUG_SUBSYS': 'INIT,GRAPH',
             'NCCL_DEBUG_FILE': os.path.join(directory, 'rccl.%h.%p.log')}

@@ -188,6 +188,36 @@ def test_strict_policy_with_hysteresis(redis_client):
     assert scaler.scale('ns', 'deployment', 'w', 0, 8, 1) == 1  # applied
 
 
+def test_strict_default_holds_only_the_last_worker(redis_client):
+    """Plain ``strict``: a scale-down that keeps
+    workers applies at once; a target of zero keeps one worker until it
+    was read on two ticks ``zero_delay`` apart -- an empty queue for one
+    tick mid-burst does not make the next key pay a cold start."""
+    clock = [0.0]
+    replicas = [4]
+    scaler = make(redis_client, queues='predict', policy='strict',
+                  zero_delay=5.0, clock=lambda: clock[0])
+    scaler.actuator.list_namespaced_deployment = lambda ns: ResourceList(
+        items=[ResourceView(kind='deployment', metadata=Metadata(name='w'),
+                            spec=Spec(replicas=replicas[0]),
+                            status=Status(available_replicas=replicas[0]))])
+    redis_client.rpush('predict', 'a', 'b')
+    assert scaler.scale('ns', 'deployment', 'w', 0, 8, 1) == 2   # at once
+    replicas[0] = 2
+    redis_client.delete('predict')
+    clock[0] = 5.0
+    assert scaler.scale('ns', 'deployment', 'w', 0, 8, 1) == 1   # zero held
+    replicas[0] = 1
+    clock[0] = 7.0
+    redis_client.rpush('predict', 'c')                           # a new key
+    assert scaler.scale('ns', 'deployment', 'w', 0, 8, 1) == 1
+    redis_client.delete('predict')
+    clock[0] = 12.0
+    assert scaler.scale('ns', 'deployment', 'w', 0, 8, 1) == 1   # held anew
+    clock[0] = 17.0
+    assert scaler.scale('ns', 'deployment', 'w', 0, 8, 1) == 0   # two ticks
+
+
 @pytest.mark.parametrize('tally', ['reference', 'atomic'])
 def test_strict_busy_floor_counts_workers_not_keys(redis_client, tally):
     """A batched (job) worker holds one processing key per slot: the strict

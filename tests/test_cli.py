@@ -192,8 +192,11 @@ def test_strict_policy_defaults_to_two_tick_hysteresis():
                                         'SCALE_POLICY': policy,
                                         'INTERVAL': interval},
                                use_files=False))
-    assert settings('strict').SCALE_DOWN_DELAY == 5.0
-    assert settings('strict', '2').SCALE_DOWN_DELAY == 2.0
-    assert settings('strict:0').SCALE_DOWN_DELAY == 0.0
-    assert settings('strict:7.5').SCALE_DOWN_DELAY == 7.5
-    assert settings('reference').SCALE_DOWN_DELAY == 0.0
+    def delays(policy, interval='5'):
+        s = settings(policy, interval)
+        return s.SCALE_DOWN_DELAY, s.SCALE_TO_ZERO_DELAY
+    assert delays('strict') == (0.0, 5.0)
+    assert delays('strict', '2') == (0.0, 2.0)
+    assert delays('strict:0') == (0.0, 0.0)
+    assert delays('strict:7.5') == (7.5, 0.0)
+    assert delays('reference') == (0.0, 0.0)

@@ -306,16 +306,20 @@ def test_hip_worker_spawns_without_site_packages(monkeypatch):
 
 @pytest.mark.gpu
 def test_gpu_cold_spawn_opens_the_device_in_parallel(resp_server):
-    """MI355X, no standby (``WARM_POOL=0``): the worker starts as
-    ``python -S`` (no torch, no numpy), opens the device on a helper thread
-    while it imports and connects, serves a key and drains."""
+    """MI355X, no standby (``WARM_POOL=0``): the torch-free worker
+    (``WORKER_ENGINE=builtin``) starts as ``python -S`` (no torch, no
+    numpy), opens the device on a helper thread while it imports and
+    connects, serves a key and drains."""
     import sys
     import time
     from kiosk_autoscaler_amd.config import Config, Settings
     from kiosk_autoscaler_amd.redisq import StrictRedis
     from kiosk_autoscaler_amd.utils.events import EventLog
+    if 'WORKER_ENGINE' in os.environ:
+        pytest.skip('WORKER_ENGINE set in the environment')
     env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
            'QUEUES': 'predict', 'RESOURCE_NAME': 'cold', 'MAX_PODS': '1',
+           'WORKER_ENGINE': 'builtin',
            'WORKER_BACKEND': 'hip', 'WARM_POOL': '0', 'FENCE': 'none',
            'REDIS_INTERVAL': '0', 'GPU_IDS': '0', 'MODEL': '1024x4096x2',
            'ROWS_PER_KEY': '256'}
@@ -891,3 +895,30 @@ def test_workers_get_a_writable_comgr_cache(tmp_path):
     assert comgr_cache_env({'HOME': str(ro), 'AMD_COMGR_CACHE_DIR': '/x'}) \
         == {}
     assert comgr_cache_env({'HOME': str(ro), 'AMD_COMGR_CACHE': '0'}) == {}
+
+
+def test_awake_sized_pool_spawns_one_lead_before_the_tick():
+    """An awake deep-idle pool spawns the standby for a waiting key one
+    wake lead before the tick that can assign it, not at once: spawned at
+    once it held its GPU for the rest of the tick phase (163 GPU-s at
+    config 3 under strict, profiles/r5_config3).  A resident pool, an
+    unknown tick or a tick within the lead spawn at once."""
+    from kiosk_autoscaler_amd.gpumgr.controller import GpuManager
+    slots = [gpus.GpuSlot(i, str(i)) for i in range(4)]
+    tpl = gpumgr.WorkerTemplate(queues=['q'], backend='cpu')
+    manager = GpuManager(slots, pool_size=4, pool_template=tpl,
+                         pool_idle_release_s=0.01, pool_wake_lead_s=0.75)
+    now = time.monotonic()
+    manager._next_tick = now + 2.0
+    assert manager._spawn_due(now)                 # boot pool: resident
+    manager.pool_parks = 1
+    manager._wake_boots.extend([0.10, 0.12])       # lead 0.15 s
+    assert not manager._spawn_due(now)
+    assert manager._spawn_at == pytest.approx(now + 2.0 - 0.15)
+    assert manager._spawn_due(now + 1.9)           # inside the lead
+    assert manager._spawn_at is None
+    manager._next_tick = None
+    assert manager._spawn_due(now)                 # no tick known
+    manager._next_tick = now + 2.0
+    manager._wake_until = now + 1.0                # an arrival's wake hold
+    assert manager._spawn_due(now)

@@ -65,7 +65,11 @@ def test_trace_env_and_log_path():
     assert env['NCCL_DEBUG'] == 'INFO' and 'INIT' in env['NCCL_DEBUG_SUBSYS']
     assert rccl_info.log_path(env, pid=42, host='n1') == '/d/rccl.n1.42.log'
     assert rccl_info.trace_env('/d', environ={'RCCL_TRACE': '0'}) == {}
-    assert rccl_info.trace_env('/d', environ={'NCCL_DEBUG': 'WARN'}) == {}
+    assert rccl_info.trace_env('/d', environ={'NCCL_DEBUG': 'INFO'}) == {}
+    assert rccl_info.trace_env('/d', environ={'NCCL_DEBUG_FILE': '/x'}) == {}
+    # a quieter level is raised to INFO into the per-process files
+    assert rccl_info.trace_env('/d', environ={'NCCL_DEBUG': 'WARN'})[
+        'NCCL_DEBUG'] == 'INFO'
     assert rccl_info.log_path({'NCCL_DEBUG': 'WARN',
                                'NCCL_DEBUG_FILE': '/x'}) is None
 
