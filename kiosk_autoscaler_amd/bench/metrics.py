@@ -171,15 +171,22 @@ def standby_gpu(events, t_lo, t_hi):
     its context and code objects resident while it waits for an assignment:
     the reference at 0 replicas holds nothing, so this cost is reported next
     to the GPU-idle % instead of being hidden in it.  An interval opens at
-    ``standby_ready`` and closes at the ``worker_assigned`` of the same pid
-    (or the window end)."""
+    ``standby_ready`` (a recycled worker: at its ``worker_recycled``, where
+    its worker time ends) and closes at the ``worker_assigned`` or
+    ``standby_exit`` of the same pid (or the window end)."""
     open_at = {}
     serving = set()     # pids assigned and not recycled since
     total = 0
     for e in sorted(events, key=lambda e: e.get('t', 0)):
         ev = e.get('ev')
         pid = e.get('pid')
-        if ev == 'standby_ready' and (e.get('preinit') or e.get('recycled')):
+        if ev in ('worker_recycled', 'worker_retired') and pid is not None:
+            # the drained worker's GPU stays held from its recycle on (its
+            # 'standby' report follows after it freed its buffers)
+            serving.discard(pid)
+            open_at.setdefault(pid, e['t'])
+        elif ev == 'standby_ready' and (e.get('preinit') or
+                                        e.get('recycled')):
             if e.get('recycled'):
                 serving.discard(pid)
             elif pid in serving:

@@ -343,8 +343,15 @@ class PoolMixin(object):
         if not self.pool_sized_to_demand() or excess <= 0:
             return False
         now = time.monotonic() if now is None else now
-        hold = max(self.wake_lead() if self._wake_boots else
-                   self.pool_wake_lead_s, self.pool_idle_release_s)
+        lead = self.wake_lead() if self._wake_boots else \
+            self.pool_wake_lead_s
+        hold = max(lead, self.pool_idle_release_s)
+        if self._next_tick is not None and self._next_tick - now > lead and \
+                now >= self._wake_until:
+            # the next tick that could assign it is further away than a
+            # boot: a standby it needs is spawned one lead before it
+            # (``_spawn_due``), so nothing is gained by holding this one
+            hold = self.pool_idle_release_s
         idle = sorted((proc.standby_since, index)
                       for index, proc in self.standbys.items()
                       if proc.booted and proc.standby_since is not None and
@@ -706,6 +713,9 @@ class PoolMixin(object):
         else:
             proc.pipe.send({'cmd': 'exit'})
             self.retiring.append(proc)
+            # its GPU is held until the process is gone (standby_exit)
+            self.events.emit('worker_retired', worker=worker.id,
+                             gpu=slot.index, pid=proc.pid)
 
     ORPHAN_SCAN_S = 5.0
 

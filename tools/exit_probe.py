@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""How long a worker's exit holds its GPU: ``os._exit`` -> reaped, by what
+the process holds (the tail of every deep-idle cycle: a parked standby's
+exit is standby GPU time, profiles/r5_standby).
+
+Like the zygote, the parent loads the native module (and RCCL, and torch
+for the ``torch`` cases) without a HIP call and forks one child per case;
+the child builds what the case names, reports, waits for ``go`` and calls
+``os._exit``; the parent times ``go`` -> ``waitpid``.
+
+Cases: ``ctx`` (HIP context + stream), ``engine`` (+ the production engine,
+1.3 GB), ``engine_rccl`` (+ a 1-rank RCCL communicator), ``engine_free``
+(engine closed -- hipFree -- before the exit, timed separately),
+``torch_engine_rccl`` (the PyTorch engine + RCCL).  One JSON line per case.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CASES = ('ctx', 'engine', 'engine_rccl', 'engine_free', 'torch_engine_rccl')
+
+
+def child(case, mod, wfd, rfd):
+    info = {}
+    mod.preinit_device(0)
+    keep = []
+    if case.startswith('torch'):
+        from kiosk_autoscaler_amd.models.torch_kiosk import TorchKioskEngine
+        from kiosk_autoscaler_amd.worker.runtime import WorkerConfig
+        cfg = WorkerConfig({'MODEL_DIM': '4096', 'MODEL_HIDDEN': '16384',
+                            'MODEL_LAYERS': '4', 'ROWS_PER_KEY': '2048'},
+                           {'worker_id': 'exit'})
+        engine = TorchKioskEngine(cfg)
+        engine.warmstart()
+        keep.append(engine)
+    elif case.startswith('engine'):
+        engine = mod.Engine(0, 4096, 16384, 4, 2048, 1)
+        engine.warmstart()
+        keep.append(engine)
+    if case.endswith('rccl'):
+        fence = mod.Fence(mod.fence_unique_id(), 1, 0, 60.0)
+        fence.allreduce([1] * 9)
+        keep.append(fence)
+    if case == 'engine_free':
+        t0 = time.monotonic_ns()
+        keep[0].close()
+        info['close_ms'] = (time.monotonic_ns() - t0) / 1e6
+    free, total = mod.mem_info()
+    info['used_gb'] = (total - free) / 1e9
+    os.write(wfd, (json.dumps(info) + '\n').encode())
+    os.read(rfd, 1)            # go
+    os._exit(0)
+
+
+def main():
+    cases = sys.argv[1].split(',') if len(sys.argv) > 1 else list(CASES)
+    os.environ.setdefault('NCCL_MIN_NCHANNELS', '1')
+    os.environ.setdefault('NCCL_MAX_NCHANNELS', '1')
+    torch_first = any(c.startswith('torch') for c in cases)
+    from kiosk_autoscaler_amd.ops import native
+    mod = native.load(torch_first=torch_first)
+    mod.fence_dlopen()
+    for case in cases:
+        for rep in range(3):
+            up_r, up_w = os.pipe()
+            go_r, go_w = os.pipe()
+            pid = os.fork()
+            if pid == 0:
+                os.close(up_r)
+                os.close(go_w)
+                try:
+                    child(case, mod, up_w, go_r)
+                except Exception as err:  # pylint: disable=broad-except
+                    os.write(up_w, (json.dumps({'error': str(err)}) +
+                                    '\n').encode())
+                    os._exit(1)
+            os.close(up_w)
+            os.close(go_r)
+            line = b''
+            while not line.endswith(b'\n'):
+                chunk = os.read(up_r, 4096)
+                if not chunk:
+                    break
+                line += chunk
+            info = json.loads(line.decode() or '{}')
+            time.sleep(0.2)
+            t0 = time.monotonic_ns()
+            os.write(go_w, b'g')
+            _, status = os.waitpid(pid, 0)
+            info.update({'case': case, 'rep': rep,
+                         'exit_ms': (time.monotonic_ns() - t0) / 1e6,
+                         'status': status})
+            print(json.dumps(info), flush=True)
+            os.close(up_r)
+            os.close(go_w)
+            time.sleep(0.3)
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())
