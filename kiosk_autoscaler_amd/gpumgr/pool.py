@@ -53,6 +53,7 @@ class PoolMixin(object):
         self._wake_at = None      # a deferred arrival wake
         self._spawn_at = None     # a deferred standby spawn (awake pool)
         self._next_arrival_check = 0.0
+        self._arrival_watch = False   # no demand: queues are polled
         # queue -> length at the last check; reset to empty when demand
         # ends (a scale to zero implies empty queues, stranded keys aside),
         # so a key landing before the first check still counts as arrived
@@ -113,8 +114,20 @@ class PoolMixin(object):
         argv = self._interpreter(tpl) + [
             '-m', 'kiosk_autoscaler_amd.worker.zygote', '--backend',
             tpl.backend]
-        self.zygote = zygote.ZygoteClient(argv, self._environment(tpl))
-        self.events.emit('zygote_spawn', pid=self.zygote.pid)
+        self.zygote = zygote.ZygoteClient(argv, self._environment(tpl),
+                                          embryos=self.zygote_embryos())
+        self.events.emit('zygote_spawn', pid=self.zygote.pid,
+                         embryos=self.zygote_embryos())
+
+    def zygote_embryos(self):
+        """Pre-forked workers the zygote keeps (one per GPU slot, at most
+        8; ``ZYGOTE_EMBRYOS`` overrides, 0 = fork on request): a spawn then
+        hands its request to a process that already exists instead of
+        waiting for two forks of a torch-sized image (profiles/r5_boot)."""
+        override = os.environ.get('ZYGOTE_EMBRYOS', '')
+        if override.strip():
+            return max(0, int(override))
+        return min(8, max(1, len(self.slots)))
 
     def _check_zygote(self):
         """False (and the zygote forgotten, restarted after a pause) once
@@ -234,7 +247,10 @@ class PoolMixin(object):
         proc.slot = slot.index if slot is not None else None
         proc.via = via
         self.events.emit('process_spawn', role=role, pid=popen.pid,
-                         slot=proc.slot, via=via)
+                         slot=proc.slot, via=via,
+                         embryo=bool(getattr(popen, 'embryo', False)),
+                         request_ms=round((time.monotonic_ns() - t_request)
+                                          / 1e6, 3))
         return proc
 
     def _refill_pool(self):
@@ -413,6 +429,7 @@ class PoolMixin(object):
         demand = any(r.declared > 0 or any(w.state != EXITED
                                            for w in r.workers.values())
                      for r in self.resources.values())
+        self._arrival_watch = not demand
         if demand:
             self._last_demand = now
             self._queued = {}
@@ -527,6 +544,37 @@ class PoolMixin(object):
                         'keys_per_pod': resource.template.keys_per_pod}
         return {'kind': 'deployment', 'keys_per_pod': template.keys_per_pod}
 
+    def _arrival_check_due(self):
+        """When the next queue-length read is due while arrivals are
+        watched (else None): the manager's loop must not sleep past it --
+        its idle timeout (50 ms) was the real poll period, so a key was
+        seen up to 50 ms late instead of ``pool_wake_poll_s``
+        (profiles/r5_boot)."""
+        if not self._arrival_watch or self.pool_wake_poll_s <= 0 or \
+                self.redis is None:
+            return None
+        return self._next_arrival_check
+
+    # queue-read period inside the wake window (the last ``wake_lead()``
+    # before a parked pool's tick): an arrival there wakes the pool at once,
+    # so each ms it goes unseen is a ms of the standby's boot lost
+    ARRIVAL_FINE_S = 0.004
+
+    def _next_arrival_read(self, now):
+        """``pool_wake_poll_s`` after ``now``, but never past the start of
+        the next tick's wake window, and ``ARRIVAL_FINE_S`` inside it: a key
+        seen before the window is woken at the window's start anyway, one
+        seen inside it is woken on sight."""
+        period = self.pool_wake_poll_s
+        if self._next_tick is None or not self.pool_parked:
+            return now + period
+        window = self._next_tick - self.wake_lead()
+        if now >= window:
+            if now >= self._next_tick:
+                return now + period
+            return now + min(period, self.ARRIVAL_FINE_S)
+        return min(now + period, window)
+
     def _arrived(self, now):
         """True when a managed queue grew since the last check (read every
         ``pool_wake_poll_s`` while no worker is declared or live).  Growth,
@@ -535,7 +583,7 @@ class PoolMixin(object):
         if self.pool_wake_poll_s <= 0 or self.redis is None or \
                 now < self._next_arrival_check:
             return False
-        self._next_arrival_check = now + self.pool_wake_poll_s
+        self._next_arrival_check = self._next_arrival_read(now)
         lengths = self._queue_lengths()
         if not lengths:
             return False

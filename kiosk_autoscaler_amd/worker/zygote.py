@@ -106,14 +106,16 @@ class ZygoteLost(OSError):
 class ZygoteClient(object):
     """Manager side: start the zygote, fork workers from it."""
 
-    def __init__(self, argv, env, timeout=10.0):
+    def __init__(self, argv, env, timeout=10.0, embryos=0):
         import subprocess
         self.sock, child = socket.socketpair(socket.AF_UNIX,
                                              socket.SOCK_SEQPACKET)
         env = dict(env)
         env['KIOSK_ZYGOTE_FD'] = str(child.fileno())
+        self.embryos = set()        # pids of the zygote's pre-forked workers
         self.popen = subprocess.Popen(
-            list(argv) + ['--zygote-fd', str(child.fileno())], env=env,
+            list(argv) + ['--zygote-fd', str(child.fileno()),
+                          '--embryos', str(int(embryos))], env=env,
             pass_fds=(child.fileno(),), close_fds=True,
             start_new_session=True)
         child.close()
@@ -195,15 +197,45 @@ class ZygoteClient(object):
                 raise ZygoteLost('zygote closed its socket during fork %d'
                                  % rid)
             reply = json.loads(data)
+            if 'embryos' in reply:
+                self.embryos = set(int(p) for p in reply['embryos'])
+            else:
+                self.embryos = set(getattr(self, 'embryos', ()))
             if reply.get('id') == rid:
                 break
             # a late reply to a request given up on: not ours
         if 'pid' not in reply:
             raise OSError('zygote fork failed: %s' % reply.get('error'))
         self.forks += 1
-        return ForkedChild(int(reply['pid']))
+        child = ForkedChild(int(reply['pid']))
+        child.embryo = reply.get('via') == 'embryo'
+        self.embryos.discard(child.pid)
+        return child
+
+    def embryo_pids(self):
+        """The zygote's pre-forked workers, as last reported (reading any
+        report waiting on the socket; a late fork reply read here is
+        dropped, as :meth:`fork` would)."""
+        while True:
+            try:
+                self.sock.setblocking(False)
+                data = self.sock.recv(MAX_MSG)
+            except (BlockingIOError, OSError):
+                break
+            finally:
+                try:
+                    self.sock.setblocking(True)
+                except OSError:
+                    pass
+            if not data:
+                break
+            message = json.loads(data)
+            if 'embryos' in message:
+                self.embryos = set(int(p) for p in message['embryos'])
+        return set(self.embryos)
 
     def close(self):
+        self.embryo_pids()
         try:
             self.sock.close()
         except OSError:
@@ -214,6 +246,18 @@ class ZygoteClient(object):
                 self.popen.wait(timeout=5)
             except Exception:  # pylint: disable=broad-except
                 self.popen.kill()
+        # the embryos (this process's children) end on the zygote's EOF
+        deadline = time.monotonic() + 2.0
+        for pid in sorted(self.embryos):
+            while True:
+                try:
+                    done, _ = os.waitpid(pid, os.WNOHANG)
+                except ChildProcessError:
+                    break
+                if done or time.monotonic() > deadline:
+                    break
+                time.sleep(0.005)
+        self.embryos = set()
 
 
 # ---------------------------------------------------------------------------
@@ -245,7 +289,10 @@ def _preload(backend):
 def _child(request, fds, sock):
     """In the grandchild: become the worker described by ``request``."""
     sock.close()
-    os.setsid()
+    try:
+        os.setsid()
+    except OSError:
+        pass                    # an embryo: already a session leader
     cmd_r, ev_w = fds
     keep = {0, 1, 2, cmd_r, ev_w}
     for fd in range(3, 1024):
@@ -278,8 +325,129 @@ def _child(request, fds, sock):
     os._exit(code or 0)
 
 
-def _serve(sock):
+def _double_fork(body):
+    """Run ``body()`` in a grandchild re-parented to the manager (the
+    intermediate child exits at once; the manager is the subreaper).
+    Returns the grandchild's pid, or None."""
+    r, w = os.pipe()
+    mid = os.fork()
+    if mid == 0:
+        code = 0
+        try:
+            os.close(r)
+            intermediate = os.getpid()
+            pid = os.fork()
+            if pid == 0:
+                os.close(w)
+                # wait for the intermediate to exit: the worker is then the
+                # manager's (subreaper) child and its death signal binds there
+                deadline = time.monotonic() + 5.0
+                while os.getppid() == intermediate and \
+                        time.monotonic() < deadline:
+                    time.sleep(0.0002)
+                body()
+                os._exit(0)
+            os.write(w, str(pid).encode())
+        except BaseException:  # pylint: disable=broad-except
+            code = 1
+        os._exit(code)
+    os.close(w)
+    data = b''
     while True:
+        chunk = os.read(r, 64)
+        if not chunk:
+            break
+        data += chunk
+    os.close(r)
+    os.waitpid(mid, 0)
+    return int(data) if data else None
+
+
+def _embryo(esock):
+    """A pre-forked worker waiting for its request (profiles/r5_boot: the
+    double ``fork`` of a torch-sized zygote, ~20 ms, was on every woken
+    standby's critical path).  It holds no GPU and no pipe of the manager's
+    until the request comes; the zygote going away ends it."""
+    try:
+        os.setsid()
+    except OSError:
+        pass
+    keep = {0, 1, 2, esock.fileno()}
+    for fd in range(3, 1024):
+        if fd not in keep:
+            try:
+                os.close(fd)
+            except OSError:
+                pass
+    signal.signal(signal.SIGTERM, signal.SIG_DFL)
+    try:
+        payload, fds, _flags, _addr = socket.recv_fds(esock, MAX_MSG, 4)
+    except OSError:
+        os._exit(0)
+    if not payload or len(fds) != 2:
+        os._exit(0)
+    _child(json.loads(payload), fds, esock)
+
+
+class _Embryos(object):
+    """The zygote's stock of pre-forked workers (``--embryos``)."""
+
+    def __init__(self, target):
+        self.target = max(0, int(target))
+        self.ready = []             # [(pid, socket)]
+
+    def pids(self):
+        return [pid for pid, _ in self.ready]
+
+    def make(self):
+        ours, theirs = socket.socketpair(socket.AF_UNIX,
+                                         socket.SOCK_SEQPACKET)
+        try:
+            pid = _double_fork(lambda: (ours.close(), _embryo(theirs)))
+        finally:
+            theirs.close()
+        if pid is None:
+            ours.close()
+            return False
+        self.ready.append((pid, ours))
+        return True
+
+    def top_up(self, sock):
+        """Refill the stock, yielding to a waiting request."""
+        import select
+        while len(self.ready) < self.target:
+            if select.select([sock], [], [], 0)[0]:
+                return
+            try:
+                if not self.make():
+                    return
+            except OSError:
+                return
+
+    def hand(self, payload, fds):
+        """Give the request to a waiting embryo: its pid, or None (none
+        left, or every one died)."""
+        while self.ready:
+            pid, esock = self.ready.pop(0)
+            try:
+                socket.send_fds(esock, [payload], list(fds))
+                return pid
+            except OSError:
+                continue
+            finally:
+                esock.close()
+        return None
+
+
+def _serve(sock, embryos=0):
+    stock = _Embryos(embryos)
+    reported = []
+    while True:
+        stock.top_up(sock)
+        if stock.pids() != reported:
+            # the manager reaps the embryos it knows of when the zygote goes
+            reported = stock.pids()
+            sock.send(json.dumps({'embryos': reported}).encode())
         try:
             payload, fds, _flags, _addr = socket.recv_fds(sock, MAX_MSG, 4)
         except OSError:
@@ -297,40 +465,19 @@ def _serve(sock):
             sock.send(json.dumps({'id': request.get('id'),
                                   'error': str(err)}).encode())
             continue
-        r, w = os.pipe()
-        mid = os.fork()
-        if mid == 0:
-            os.close(r)
-            intermediate = os.getpid()
-            pid = os.fork()
-            if pid == 0:
-                os.close(w)
-                # wait for the intermediate to exit: the worker is then the
-                # manager's (subreaper) child and its death signal binds there
-                deadline = time.monotonic() + 5.0
-                while os.getppid() == intermediate and \
-                        time.monotonic() < deadline:
-                    time.sleep(0.0002)
-                _child(request, fds, sock)
-            os.write(w, str(pid).encode())
-            os._exit(0)
-        os.close(w)
+        pid = stock.hand(payload, fds)
+        via = 'embryo'
+        if pid is None:
+            via = 'fork'
+            pid = _double_fork(lambda: _child(request, fds, sock))
         for fd in fds:
             os.close(fd)
-        data = b''
-        while True:
-            chunk = os.read(r, 64)
-            if not chunk:
-                break
-            data += chunk
-        os.close(r)
-        os.waitpid(mid, 0)
-        if data:
-            sock.send(json.dumps({'id': request.get('id'),
-                                  'pid': int(data)}).encode())
+        if pid is not None:
+            reply = {'id': request.get('id'), 'pid': pid, 'via': via}
         else:
-            sock.send(json.dumps({'id': request.get('id'),
-                                  'error': 'fork failed'}).encode())
+            reply = {'id': request.get('id'), 'error': 'fork failed'}
+        reply['embryos'] = reported = stock.pids()
+        sock.send(json.dumps(reply).encode())
 
 
 def main(argv=None):
@@ -338,6 +485,7 @@ def main(argv=None):
     parser = argparse.ArgumentParser(description=__doc__)
     parser.add_argument('--zygote-fd', type=int, required=True)
     parser.add_argument('--backend', default='cpu')
+    parser.add_argument('--embryos', type=int, default=0)
     args = parser.parse_args(argv)
     sock = socket.socket(fileno=args.zygote_fd)
     t0 = time.monotonic()
@@ -355,7 +503,7 @@ def main(argv=None):
     signal.signal(signal.SIGCHLD, signal.SIG_DFL)
     sock.send(json.dumps({'ready': True,
                           'preload_s': time.monotonic() - t0}).encode())
-    return _serve(sock)
+    return _serve(sock, args.embryos)
 
 
 if __name__ == '__main__':

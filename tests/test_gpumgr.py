@@ -578,6 +578,32 @@ def test_arrival_wake_waits_for_the_lead_before_the_tick(resp_server):
         manager.stop()
 
 
+def test_queue_reads_tighten_inside_the_wake_window():
+    """profiles/r5_boot: the loop's 50 ms idle timeout was the real arrival
+    poll, so a key 125 ms before the tick was seen 76 ms before it.  While
+    arrivals are watched the loop wakes for each read; reads come every
+    ``pool_wake_poll_s``, one lands on the wake window's start, and inside
+    the window they come every ``ARRIVAL_FINE_S``."""
+    manager = gpumgr.GpuManager([], pool_wake_poll_s=0.02,
+                                pool_wake_lead_s=0.4)
+    manager.redis = object()
+    assert manager._arrival_check_due() is None        # demand: no watch
+    manager._arrival_watch = True
+    manager._next_arrival_check = 12.5
+    assert manager._arrival_check_due() == 12.5
+    # no tick known / pool awake: the plain period
+    assert manager._next_arrival_read(10.0) == pytest.approx(10.02)
+    manager.pool_parked = True
+    manager._next_tick = 11.0                 # window opens at 10.6
+    assert manager._next_arrival_read(10.0) == pytest.approx(10.02)
+    assert manager._next_arrival_read(10.59) == pytest.approx(10.6)
+    assert manager._next_arrival_read(10.7) == pytest.approx(
+        10.7 + manager.ARRIVAL_FINE_S)
+    assert manager._next_arrival_read(11.01) == pytest.approx(11.03)
+    manager.redis = None
+    assert manager._arrival_check_due() is None
+
+
 def test_pci_mapping_verified_and_remapped(monkeypatch):
     """a process reports the PCI address HIP sees for its pinned
     ordinal; a match verifies the slot, a mismatch remaps the slot to the

@@ -327,6 +327,10 @@ def test_zygote_cold_spawn_reaped_like_a_child(stack):
                          for i in range(2)), timeout=30)
     spawns = [e for e in events.records if e['ev'] == 'process_spawn']
     assert spawns and spawns[-1]['via'] == 'zygote'
+    # handed to a pre-forked embryo, which the zygote replaced
+    assert spawns[-1]['embryo'] is True
+    embryos = wait_for(lambda: manager.zygote.embryo_pids(), timeout=10)
+    assert spawns[-1]['pid'] not in embryos
     worker = manager.status()['resources'][0]['workers'][0]
     assert worker['pid'] == spawns[-1]['pid']
     assert os.getppid() != worker['pid']
@@ -352,6 +356,14 @@ def test_zygote_cold_spawn_reaped_like_a_child(stack):
              timeout=30)
     wait_for(lambda: client.hget('predict:slow', 'status') == 'done',
              timeout=60)
+    # the zygote's stock ends with it, reaped by the client
+    zyg = manager.zygote
+    embryos = zyg.embryo_pids()
+    assert embryos
+    zyg.close()
+    for pid in embryos:
+        with pytest.raises(ChildProcessError):
+            os.waitpid(pid, os.WNOHANG)
 
 
 def test_dead_zygote_is_restarted(stack):
