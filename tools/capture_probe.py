@@ -30,14 +30,55 @@ def child(case, mod):
     t0 = time.perf_counter()
     mod.preinit_device(0)
     out['preinit_ms'] = ms(t0)
-    if case == 'engine':
+    if case in ('engine', 'engine_calls'):
         from kiosk_autoscaler_amd.models.torch_kiosk import TorchKioskEngine
         from kiosk_autoscaler_amd.worker.runtime import WorkerConfig
+        calls = []
+
+        class Timed(object):
+            """The native module, each call timed (first capture only)."""
+
+            def __init__(self, real):
+                self._real = real
+
+            def __getattr__(self, name):
+                fn = getattr(self._real, name)
+                if not callable(fn):
+                    return fn
+
+                def timed(*args, **kw):
+                    t = time.perf_counter()
+                    try:
+                        return fn(*args, **kw)
+                    finally:
+                        calls.append((name, ms(t)))
+                return timed
+
+        class Probe(TorchKioskEngine):
+            def _enqueue_forward(self, rows):
+                if case != 'engine_calls' or calls:
+                    return TorchKioskEngine._enqueue_forward(self, rows)
+                real, self.mod = self.mod, Timed(self.mod)
+                t = time.perf_counter()
+                try:
+                    return TorchKioskEngine._enqueue_forward(self, rows)
+                finally:
+                    self.mod = real
+                    calls.append(('enqueue_total', ms(t)))
+
+            def _record(self, enqueue):
+                t = time.perf_counter()
+                try:
+                    return TorchKioskEngine._record(self, enqueue)
+                finally:
+                    calls.append(('record_total', ms(t)))
         stages = {}
         t0 = time.perf_counter()
-        TorchKioskEngine(WorkerConfig({}, {'worker_id': 'probe'}),
-                         stage=lambda name: stages.setdefault(name, ms(t0)))
+        Probe(WorkerConfig({}, {'worker_id': 'probe'}),
+              stage=lambda name: stages.setdefault(name, ms(t0)))
         out['stages'] = stages
+        if calls:
+            out['calls'] = calls
         return out
     handle = mod.take_stream(0)
     stream = torch.cuda.ExternalStream(handle) if handle else \
@@ -79,7 +120,7 @@ def child(case, mod):
 
 def main():
     cases = sys.argv[1].split(',') if len(sys.argv) > 1 else \
-        ['kernel', 'h2d', 'd2h', 'engine', 'engine']
+        ['kernel', 'h2d', 'd2h', 'engine', 'engine_calls']
     import torch  # noqa: F401  (before the native module: one HIP runtime)
     from kiosk_autoscaler_amd.ops import native
     mod = native.load(torch_first=True)
