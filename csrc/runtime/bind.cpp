@@ -4,6 +4,8 @@
 // on torch-allocated tensors (tensor.data_ptr(), the current stream);
 // Engine / Fence are the runtime objects the worker uses.  Every
 // long-running call releases the GIL.
+#include <chrono>
+
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -125,6 +127,73 @@ py::dict fwd_to_dict(const kiosk::ForwardResult& r) {
   d["graph"] = r.graph;
   return d;
 }
+
+// A hipGraph recorded from the caller's own launches on one stream (the
+// PyTorch engine's forward and warm start).  torch.cuda.CUDAGraph would also
+// capture torch's RNG state and open a private memory pool: 10-27 ms on a
+// woken standby's first capture, on its critical path (profiles/r5_boot);
+// this engine uses neither.  Capture is thread-local, as the built-in
+// engine's, so the node agent's thread may call HIP meanwhile.
+class StreamGraph {
+ public:
+  explicit StreamGraph(unsigned long long stream)
+      : stream_(stream_of(stream)) {}
+  ~StreamGraph() { reset(); }
+  StreamGraph(const StreamGraph&) = delete;
+  StreamGraph& operator=(const StreamGraph&) = delete;
+
+  void begin() {
+    reset();
+    check_hip(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal),
+              "hipStreamBeginCapture");
+    capturing_ = true;
+  }
+  // ends the capture and instantiates; after a failed enqueue the caller
+  // calls abort() instead
+  void end() {
+    if (!capturing_) {
+      throw std::runtime_error("StreamGraph.end: not capturing");
+    }
+    capturing_ = false;
+    hipGraph_t graph = nullptr;
+    hipError_t err = hipStreamEndCapture(stream_, &graph);
+    if (err != hipSuccess) {
+      if (graph) hipGraphDestroy(graph);
+      check_hip(err, "hipStreamEndCapture");
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    err = hipGraphInstantiate(&exec_, graph, nullptr, nullptr, 0);
+    instantiate_us_ = std::chrono::duration<double, std::micro>(
+                          std::chrono::steady_clock::now() - t0).count();
+    hipGraphDestroy(graph);
+    if (err != hipSuccess) exec_ = nullptr;
+    check_hip(err, "hipGraphInstantiate");
+  }
+  void abort() {
+    if (!capturing_) return;
+    capturing_ = false;
+    hipGraph_t graph = nullptr;
+    (void)hipStreamEndCapture(stream_, &graph);
+    if (graph) hipGraphDestroy(graph);
+  }
+  void launch() {
+    if (!exec_) throw std::runtime_error("StreamGraph.launch: no graph");
+    check_hip(hipGraphLaunch(exec_, stream_), "hipGraphLaunch");
+  }
+  void reset() {
+    abort();
+    if (exec_) hipGraphExecDestroy(exec_);
+    exec_ = nullptr;
+  }
+  bool ready() const { return exec_ != nullptr; }
+  double instantiate_us() const { return instantiate_us_; }
+
+ private:
+  hipStream_t stream_;
+  hipGraphExec_t exec_ = nullptr;
+  bool capturing_ = false;
+  double instantiate_us_ = 0.0;
+};
 
 }  // namespace
 
@@ -388,6 +457,32 @@ PYBIND11_MODULE(_kiosk_hip, m) {
       .def_property_readonly("hidden", &kiosk::Engine::hidden)
       .def_property_readonly("layers", &kiosk::Engine::layers)
       .def_property_readonly("max_rows", &kiosk::Engine::max_rows);
+
+  py::class_<StreamGraph>(m, "StreamGraph")
+      .def(py::init<unsigned long long>(), py::arg("stream"))
+      .def("begin", &StreamGraph::begin,
+           py::call_guard<py::gil_scoped_release>())
+      .def("end", &StreamGraph::end, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &StreamGraph::abort,
+           py::call_guard<py::gil_scoped_release>())
+      .def("launch", &StreamGraph::launch,
+           py::call_guard<py::gil_scoped_release>())
+      .def("reset", &StreamGraph::reset,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("ready", &StreamGraph::ready)
+      .def_property_readonly("instantiate_us", &StreamGraph::instantiate_us);
+  // hipMemcpyAsync (either direction, pinned host memory): inside a
+  // StreamGraph capture it becomes a copy node
+  m.def(
+      "memcpy_async",
+      [](unsigned long long dst, unsigned long long src, size_t nbytes,
+         unsigned long long stream) {
+        check_hip(hipMemcpyAsync(ptr<void>(dst), ptr<const void>(src), nbytes,
+                                 hipMemcpyDefault, stream_of(stream)),
+                  "hipMemcpyAsync");
+      },
+      py::arg("dst"), py::arg("src"), py::arg("nbytes"), py::arg("stream") = 0,
+      py::call_guard<py::gil_scoped_release>());
 
   kiosk::bind_comm(m);
 }

@@ -13,10 +13,11 @@ allocator, torch's stream) and every kernel one of ours:
   epilogue, then the down-projection GEMM with the fused bias+residual
   epilogue (split-K into a preallocated workspace where the grid alone would
   leave CUs idle), then the deterministic partial-sum kernel -- the whole
-  forward, input generation included, captured once into a
-  ``torch.cuda.CUDAGraph``.  The job's seed reaches the captured input
-  kernel through a pinned host word copied inside the graph, so a forward
-  is exactly one graph launch;
+  forward, input generation included, captured once into a native hipGraph
+  (``StreamGraph``, not ``torch.cuda.CUDAGraph``: no RNG state or memory
+  pool to set up on a woken standby's critical path, profiles/r5_boot).
+  The job's seed reaches the captured input kernel through a pinned host
+  word copied inside the graph, so a forward is exactly one graph launch;
 * N1 warm-start: the warm-start kernel over the engine's own first weight
   matrix (every CU, the GEMM's LDS ring zeroed, an MFMA loop), captured as
   a second graph: once the engine is built, READY is one graph launch --
@@ -92,8 +93,8 @@ class TorchKioskEngine(object):
         """Standby boot (``worker/main.py``): torch's lazy CUDA init plus
         our launch handles -- no hipBLASLt handle (this engine never calls
         a torch matmul) and no torch fill: the engine clears its buffers
-        with ``hipMemsetAsync`` (profiles/r4_comgr; torch's CUDAGraph
-        capture still issues four small int64 fills of its own)."""
+        with ``hipMemsetAsync`` and captures its graphs natively
+        (profiles/r4_comgr, profiles/r5_boot)."""
         import torch
         torch.cuda.init()
         native.load().prepare_kernels()
@@ -183,7 +184,7 @@ class TorchKioskEngine(object):
         self.stream.synchronize()
         if stage:
             stage('weights_on_device')
-        self.graphs = {}               # rows -> (CUDAGraph, output tensor)
+        self.graphs = {}               # rows -> (StreamGraph, output tensor)
         self.warm_graph = None
         self._capture(self.max_rows)
         if stage:
@@ -203,10 +204,10 @@ class TorchKioskEngine(object):
     def _enqueue_forward(self, rows):
         """The forward on the current stream (captured, never run eagerly
         outside a graph)."""
-        torch = self.torch
         mod = self.mod
-        stream = torch.cuda.current_stream().cuda_stream
-        self.seed_dev.copy_(self.seed_host, non_blocking=True)
+        stream = self.stream.cuda_stream
+        mod.memcpy_async(self.seed_dev.data_ptr(), self.seed_host.data_ptr(),
+                         8, stream)
         x = self.x[:rows]
         mod.init_uniform_bf16_devseed(x.data_ptr(), x.numel(),
                                       self.seed_dev.data_ptr(), -1.0, 1.0,
@@ -227,23 +228,28 @@ class TorchKioskEngine(object):
         out = cur[:rows]
         mod.partial_sums(out.data_ptr(), out.numel(),
                          self.partials.data_ptr(), stream)
-        self.partials_host.copy_(self.partials, non_blocking=True)
+        mod.memcpy_async(self.partials_host.data_ptr(),
+                         self.partials.data_ptr(),
+                         self.partials.numel() * 4, stream)
         return out
 
     def _record(self, enqueue):
-        """Capture ``enqueue()`` on the engine's stream.  Directly through
-        ``capture_begin``/``capture_end``: ``torch.cuda.graph`` would also
-        empty the caching allocator (nothing here allocates), and the
-        capture is thread-local (as the built-in engine's), so the node
-        agent's thread may call HIP meanwhile."""
-        graph = self.torch.cuda.CUDAGraph()
+        """Capture ``enqueue()`` (launches on the engine's stream) as a
+        native hipGraph (``_kiosk_hip.StreamGraph``): torch.cuda.CUDAGraph
+        would also capture torch's RNG state and open a private memory pool
+        -- 10-27 ms on a woken standby's first capture, on its path to READY
+        (profiles/r5_boot) -- and this engine needs neither.  Thread-local
+        capture (as the built-in engine's): the node agent's thread may
+        call HIP meanwhile."""
+        graph = self.mod.StreamGraph(self.stream.cuda_stream)
         self.stream.synchronize()
-        with self.torch.cuda.stream(self.stream):
-            graph.capture_begin(capture_error_mode='thread_local')
-            try:
-                result = enqueue()
-            finally:
-                graph.capture_end()
+        graph.begin()
+        try:
+            result = enqueue()
+        except BaseException:
+            graph.abort()
+            raise
+        graph.end()
         return graph, result
 
     def _capture(self, rows):
@@ -254,7 +260,7 @@ class TorchKioskEngine(object):
         w1 = self.weights[0][0]
 
         def enqueue():
-            stream = self.torch.cuda.current_stream().cuda_stream
+            stream = self.stream.cuda_stream
             self.mod.memset_async(self.warm_record.data_ptr(), 0,
                                   self.warm_record.numel() * 4, stream)
             self.mod.warmstart_raw(
@@ -267,8 +273,7 @@ class TorchKioskEngine(object):
     def warmstart(self):
         """N1: one graph launch (every CU, LDS ring, MFMA loop)."""
         t0 = time.perf_counter()
-        with self.torch.cuda.stream(self.stream):
-            self.warm_graph.replay()
+        self.warm_graph.launch()
         self.stream.synchronize()
         rec = self.warm_record.view(-1, 8)
         return {'backend': 'torch-kiosk', 'blocks': int(rec.shape[0]),
@@ -287,8 +292,7 @@ class TorchKioskEngine(object):
         # the previous replay may still read the pinned seed word
         self.stream.synchronize()
         self.seed_host[0] = int(seed)
-        with self.torch.cuda.stream(self.stream):
-            entry[0].replay()
+        entry[0].launch()
         return entry[1]
 
     def infer(self, jobs):
@@ -335,6 +339,10 @@ class TorchKioskEngine(object):
             return
         # nothing of ours may still run when the arena's hipFree comes
         self.stream.synchronize()
+        for graph, _ in self.graphs.values():
+            graph.reset()
+        if self.warm_graph is not None:
+            self.warm_graph.reset()
         self.graphs = {}
         self.warm_graph = None
         self.weights = None

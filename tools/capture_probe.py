@@ -30,6 +30,16 @@ def child(case, mod):
     t0 = time.perf_counter()
     mod.preinit_device(0)
     out['preinit_ms'] = ms(t0)
+    if case == 'native':
+        t0 = time.perf_counter()
+        engine = mod.Engine(0, 4096, 16384, 4, 2048, 1)
+        out['build_ms'] = ms(t0)
+        out['stages'] = dict(engine.stage_times())
+        t0 = time.perf_counter()
+        engine.forward(2048, 1, 0)
+        out['first_forward_ms'] = ms(t0)
+        engine.close()
+        return out
     if case in ('engine', 'engine_calls'):
         from kiosk_autoscaler_amd.models.torch_kiosk import TorchKioskEngine
         from kiosk_autoscaler_amd.worker.runtime import WorkerConfig
@@ -67,11 +77,24 @@ def child(case, mod):
                     calls.append(('enqueue_total', ms(t)))
 
             def _record(self, enqueue):
+                # TorchKioskEngine._record (native StreamGraph), timed
                 t = time.perf_counter()
-                try:
-                    return TorchKioskEngine._record(self, enqueue)
-                finally:
-                    calls.append(('record_total', ms(t)))
+                graph = self.mod.StreamGraph(self.stream.cuda_stream)
+                self.stream.synchronize()
+                graph.begin()
+                calls.append(('capture_begin', ms(t)))
+                t = time.perf_counter()
+                result = enqueue()
+                calls.append(('enqueue', ms(t)))
+                t = time.perf_counter()
+                graph.end()
+                calls.append(('capture_end', ms(t)))
+                calls.append(('instantiate', graph.instantiate_us / 1e3))
+                t = time.perf_counter()
+                graph.launch()
+                self.stream.synchronize()
+                calls.append(('first_launch', ms(t)))
+                return graph, result
         stages = {}
         t0 = time.perf_counter()
         Probe(WorkerConfig({}, {'worker_id': 'probe'}),
