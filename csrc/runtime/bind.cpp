@@ -226,11 +226,8 @@ PYBIND11_MODULE(_kiosk_hip, m) {
          unsigned long long bias, unsigned long long res, int M, int N, int K,
          int epilogue, unsigned long long stream, int variant,
          unsigned long long workspace, unsigned long long workspace_bytes) {
-        static bool prepared = false;
-        if (!prepared) {
-          check_hip(kiosk::gemm_prepare(), "gemm_prepare");
-          prepared = true;
-        }
+        // per device, once (an atomic test after the first success)
+        check_hip(kiosk::gemm_prepare(), "gemm_prepare");
         check_hip(kiosk::launch_gemm_variant(
                       ptr<const uint16_t>(a), ptr<const uint16_t>(b),
                       ptr<uint16_t>(c), ptr<const float>(bias),
