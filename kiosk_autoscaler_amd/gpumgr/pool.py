@@ -48,8 +48,8 @@ class PoolMixin(object):
         self.pool_wake_lead_s = float(pool_wake_lead_s or 0.0)
         self._next_tick = None    # monotonic instant of the next tick
         # spawn request -> booted+prebuilt of recent arrival-woken standbys:
-        # the lead adapts to it (the slowest + WAKE_MARGIN_S, capped)
-        self._wake_boots = collections.deque(maxlen=8)
+        # the lead adapts to it (wake_lead)
+        self._wake_boots = collections.deque(maxlen=16)
         self._wake_at = None      # a deferred arrival wake
         self._spawn_at = None     # a deferred standby spawn (awake pool)
         self._next_arrival_check = 0.0
@@ -516,24 +516,32 @@ class PoolMixin(object):
                 self._wake_at = min(self._wake_at, self._next_tick - lead)
         self._wake()
 
-    # margin of the wake lead over the slowest recent boot: the manager's
+    # margin of the wake lead over the boot it is sized for: the manager's
     # loop wakes on time (``_loop`` sleeps to ``_wake_at``), so this covers
-    # the spawn request and the jitter of one boot, not a poll period
-    WAKE_MARGIN_S = 0.03
+    # the spawn request (0.5 ms from an embryo) and a boot's jitter, not a
+    # poll period
+    WAKE_MARGIN_S = 0.05
 
     def wake_lead(self):
         """Seconds before the next tick an arrival wakes a parked pool:
         ``pool_wake_lead_s`` until woken standbys have been timed, then the
-        slowest of the last 8 spawn -> booted+prebuilt times plus
-        ``WAKE_MARGIN_S``, never above ``pool_wake_lead_s``.  Every second
-        of lead beyond the boot is a standby holding its GPU unassigned
-        (the former 1.5 x max + 0.1 s, at least 0.2 s,
-        held ~0.15 s per wake); a boot slower than the 8 before it is late
-        by the difference once, then sets the lead."""
+        second slowest of the last 16 spawn -> booted+prebuilt times (the
+        slowest while fewer than 4 are known) plus ``WAKE_MARGIN_S``, never
+        above ``pool_wake_lead_s``.  Every second of lead beyond the boot is
+        a standby holding its GPU unassigned; a boot slower than the lead is
+        late by the difference.  The boot's spread is the HIP context
+        (50-70 ms, now and then 150 ms, once in a while 0.5 s:
+        profiles/r4_boot, profiles/r5_boot), so the slowest sample is an
+        outlier the next wakes rarely repeat: over 576 woken boots of rounds
+        4-5, the second slowest of 16 + 50 ms is late less often and by less
+        than the slowest of 8 + 30 ms (3.9 against 4.4 ms a wake) and holds
+        10 ms less (83 against 94 ms a wake; tools/wake_lead_replay.py)."""
         cap = self.pool_wake_lead_s
         if cap <= 0 or not self._wake_boots:
             return cap
-        return min(cap, max(self._wake_boots) + self.WAKE_MARGIN_S)
+        boots = sorted(self._wake_boots)
+        sized = boots[-2] if len(boots) >= 4 else boots[-1]
+        return min(cap, sized + self.WAKE_MARGIN_S)
 
     def _prebuild_spec(self, template):
         """What an arrival-woken standby builds its engine for: the shape

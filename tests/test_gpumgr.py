@@ -578,6 +578,26 @@ def test_arrival_wake_waits_for_the_lead_before_the_tick(resp_server):
         manager.stop()
 
 
+def test_wake_lead_sizes_for_the_second_slowest_recent_boot():
+    """One slow HIP context (0.5 s) must not hold the next 15 wakes' GPUs
+    for it: the lead follows the second slowest of the last 16 woken boots
+    (the slowest while fewer than 4 are known), plus the margin, capped."""
+    manager = gpumgr.GpuManager([], pool_wake_lead_s=0.75)
+    margin = manager.WAKE_MARGIN_S
+    assert manager.wake_lead() == 0.75               # nothing timed yet
+    for boot in (0.10, 0.55):
+        manager._wake_boots.append(boot)
+    assert manager.wake_lead() == pytest.approx(0.55 + margin)
+    for boot in (0.11, 0.09, 0.12):
+        manager._wake_boots.append(boot)
+    assert manager.wake_lead() == pytest.approx(0.12 + margin)
+    for _ in range(16):                  # the outlier ages out of the window
+        manager._wake_boots.append(0.1)
+    assert manager.wake_lead() == pytest.approx(0.1 + margin)
+    manager._wake_boots.extend([0.9, 0.9])
+    assert manager.wake_lead() == 0.75               # the cap
+
+
 def test_queue_reads_tighten_inside_the_wake_window():
     """profiles/r5_boot: the loop's 50 ms idle timeout was the real arrival
     poll, so a key 125 ms before the tick was seen 76 ms before it.  While
@@ -879,7 +899,7 @@ def test_sized_pool_retires_standbys_idle_beyond_demand():
     manager = GpuManager(slots, pool_size=4, pool_template=tpl,
                          pool_idle_release_s=0.01, pool_wake_hold_s=8.5,
                          pool_wake_lead_s=0.75)
-    manager._wake_boots.extend([0.10, 0.12])      # lead 0.15 s
+    manager._wake_boots.extend([0.10, 0.12])      # lead 0.12 s + margin
     sent = []
 
     def proc(since, booted=True):
@@ -891,7 +911,7 @@ def test_sized_pool_retires_standbys_idle_beyond_demand():
                         3: proc(None, booted=False)}
     assert not manager._retire_excess(2, now=110.0)    # boot pool: resident
     manager.pool_parks = 1
-    assert manager.wake_lead() == pytest.approx(0.15)
+    assert manager.wake_lead() == pytest.approx(0.12 + manager.WAKE_MARGIN_S)
     assert manager._retire_excess(2, now=110.0)
     # 1 (idle 1 s) then 0 (0.5 s); 2 (50 ms) and the booting 3 stay
     assert sorted(manager.standbys) == [2, 3]
@@ -938,9 +958,10 @@ def test_awake_sized_pool_spawns_one_lead_before_the_tick():
     manager._next_tick = now + 2.0
     assert manager._spawn_due(now)                 # boot pool: resident
     manager.pool_parks = 1
-    manager._wake_boots.extend([0.10, 0.12])       # lead 0.15 s
+    manager._wake_boots.extend([0.10, 0.12])       # lead 0.12 s + margin
     assert not manager._spawn_due(now)
-    assert manager._spawn_at == pytest.approx(now + 2.0 - 0.15)
+    assert manager._spawn_at - now == pytest.approx(
+        2.0 - 0.12 - manager.WAKE_MARGIN_S)
     assert manager._spawn_due(now + 1.9)           # inside the lead
     assert manager._spawn_at is None
     manager._next_tick = None

@@ -40,7 +40,7 @@ def child(case, mod):
         out['first_forward_ms'] = ms(t0)
         engine.close()
         return out
-    if case in ('engine', 'engine_calls'):
+    if case in ('engine', 'engine_calls', 'engine_warm_first'):
         from kiosk_autoscaler_amd.models.torch_kiosk import TorchKioskEngine
         from kiosk_autoscaler_amd.worker.runtime import WorkerConfig
         calls = []
@@ -66,7 +66,7 @@ def child(case, mod):
 
         class Probe(TorchKioskEngine):
             def _enqueue_forward(self, rows):
-                if case != 'engine_calls' or calls:
+                if case == 'engine' or calls:
                     return TorchKioskEngine._enqueue_forward(self, rows)
                 real, self.mod = self.mod, Timed(self.mod)
                 t = time.perf_counter()
@@ -95,13 +95,32 @@ def child(case, mod):
                 self.stream.synchronize()
                 calls.append(('first_launch', ms(t)))
                 return graph, result
+
+        class WarmFirst(Probe):
+            """The warm-start graph captured before the forward's."""
+
+            def _capture(self, rows):
+                if self.warm_graph is None:
+                    self._capture_warm()
+                return Probe._capture(self, rows)
+
+            def _capture_warm(self):
+                if self.warm_graph is None:
+                    Probe._capture_warm(self)
         stages = {}
         t0 = time.perf_counter()
-        Probe(WorkerConfig({}, {'worker_id': 'probe'}),
-              stage=lambda name: stages.setdefault(name, ms(t0)))
+        cls = WarmFirst if case == 'engine_warm_first' else Probe
+        engine = cls(WorkerConfig({}, {'worker_id': 'probe'}),
+                     stage=lambda name: stages.setdefault(name, ms(t0)))
         out['stages'] = stages
+        # a second forward graph (another row count): per-graph cost or
+        # first-instantiate cost?
+        t0 = time.perf_counter()
+        engine._capture(1024)
+        out['second_forward_graph_ms'] = ms(t0)
         if calls:
             out['calls'] = calls
+        engine.close()
         return out
     handle = mod.take_stream(0)
     stream = torch.cuda.ExternalStream(handle) if handle else \
