@@ -25,7 +25,7 @@ from .autoscaler import Autoscaler
 from .config import Settings
 from .redisq import RedisClient
 from .utils.events import EventLog
-from .utils.logs import initialize_logger
+from .utils.logs import flush_deferred, initialize_logger
 
 
 class _Terminate(Exception):
@@ -111,6 +111,8 @@ def run_loop(scaler, settings, max_ticks=None, sleep=time.sleep,
             # observability hook for the benchmark's phase control
             scaler.redis_client.set(tick_key, '%d %d %d' % (
                 started, time.monotonic_ns(), ticks))
+        # the tick's log records are written now, after its decision
+        flush_deferred()
         ticks += 1
         if max_ticks is not None and ticks >= max_ticks:
             break

@@ -90,7 +90,10 @@ def test_logger_format_and_rotation(tmp_path):
     try:
         initialize_logger(debug_mode=False, log_file=str(tmp_path / 'a.log'),
                           stream=open(os.devnull, 'w'))
-        handlers = root.handlers[len(saved):]
+        added = root.handlers[len(saved):]
+        # one deferred handler in front of the reference's two
+        assert len(added) == 1 and hasattr(added[0], 'handlers')
+        handlers = added[0].handlers
         rotating = [h for h in handlers
                     if isinstance(h, logging.handlers.RotatingFileHandler)]
         assert rotating and rotating[0].maxBytes == 10000000
@@ -100,6 +103,19 @@ def test_logger_format_and_rotation(tmp_path):
         assert console.level == logging.INFO
         assert handlers[0].formatter._fmt == LOG_FORMAT
         assert root.level == logging.DEBUG
+        # held until the tick ends, then written in the reference's format;
+        # WARNING and above at once
+        args = {'q': 1}
+        logging.getLogger('Autoscaler').debug('keys %s', args)
+        args['q'] = 2                  # the text is fixed at the call
+        assert 'keys' not in (tmp_path / 'a.log').read_text()
+        from kiosk_autoscaler_amd.utils.logs import flush_deferred
+        flush_deferred()
+        text = (tmp_path / 'a.log').read_text()
+        assert "]:[DEBUG]:[Autoscaler]: keys {'q': 1}" in text
+        logging.getLogger('Autoscaler').warning('now')
+        assert ']:[WARNING]:[Autoscaler]: now' in (tmp_path /
+                                                   'a.log').read_text()
     finally:
         for handler in root.handlers[len(saved):]:
             root.removeHandler(handler)

@@ -40,6 +40,26 @@ def child(case, mod):
         out['first_forward_ms'] = ms(t0)
         engine.close()
         return out
+    if case.startswith('dummy_'):
+        # one throwaway graph of <kind> on its own stream first: does the
+        # engine's first instantiate then drop to the second's cost?
+        kind = case[len('dummy_'):]
+        side = torch.cuda.Stream()
+        scratch = torch.empty(4096, dtype=torch.uint8, device='cuda')
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        graph = mod.StreamGraph(side.cuda_stream)
+        graph.begin()
+        if kind == 'memset':
+            mod.memset_async(scratch.data_ptr(), 0, 64, side.cuda_stream)
+        elif kind == 'kernel':
+            mod.init_uniform_f32(scratch.data_ptr(), 16, 1, -1.0, 1.0,
+                                 side.cuda_stream)
+        graph.end()
+        out['dummy_ms'] = ms(t0)
+        out['dummy_instantiate_ms'] = graph.instantiate_us / 1e3
+        graph.reset()
+        case = 'engine_calls'
     if case in ('engine', 'engine_calls', 'engine_warm_first'):
         from kiosk_autoscaler_amd.models.torch_kiosk import TorchKioskEngine
         from kiosk_autoscaler_amd.worker.runtime import WorkerConfig
