@@ -334,6 +334,15 @@ PYBIND11_MODULE(_kiosk_hip, m) {
         return d;
       },
       py::arg("device") = 0);
+  m.def(
+      "graph_prewarm",
+      [](int device) {
+        const auto t0 = std::chrono::steady_clock::now();
+        check_hip(kiosk::graph_prewarm(device), "graph_prewarm");
+        return std::chrono::duration<double, std::milli>(
+                   std::chrono::steady_clock::now() - t0).count();
+      },
+      py::arg("device") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("release_kept_stream", &kiosk::release_kept_stream,
         py::call_guard<py::gil_scoped_release>());
   // the stream preinit_device warmed (its hardware queue already set up)

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <mutex>
 #include <set>
+#include <thread>
 
 #include "../kernels/kernels.hpp"
 #include "trace.hpp"
@@ -97,6 +98,39 @@ void release_kept_stream() {
   destroy_on_device(s, device);
 }
 
+hipError_t graph_prewarm(int device) {
+  // The HIP runtime's first hipGraphInstantiate of a graph with a node pays
+  // a one-time set-up (5-16 ms on MI355X, whatever the graph holds; the
+  // next instantiations take 0.02-0.04 ms, profiles/r5_boot): paid here,
+  // on a graph of one 4-byte memset built without a stream, so no capture
+  // and no queue is involved and it can run beside the stream's creation.
+  hipError_t err = hipSetDevice(device);
+  if (err != hipSuccess) return err;
+  void* buf = nullptr;
+  err = hipMalloc(&buf, 256);
+  if (err != hipSuccess) return err;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  err = hipGraphCreate(&graph, 0);
+  if (err == hipSuccess) {
+    hipMemsetParams params{};
+    params.dst = buf;
+    params.value = 0;
+    params.elementSize = 4;
+    params.width = 1;
+    params.height = 1;
+    params.pitch = 4;
+    hipGraphNode_t node = nullptr;
+    err = hipGraphAddMemsetNode(&node, graph, nullptr, 0, &params);
+  }
+  if (err == hipSuccess) err = hipGraphInstantiate(&exec, graph, nullptr,
+                                                   nullptr, 0);
+  if (exec) hipGraphExecDestroy(exec);
+  if (graph) hipGraphDestroy(graph);
+  hipError_t free_err = hipFree(buf);
+  return err != hipSuccess ? err : free_err;
+}
+
 std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   TraceRange range("kiosk.preinit");
   std::vector<std::pair<std::string, long long>> stages;
@@ -104,18 +138,42 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   check_hip(hipSetDevice(device), "hipSetDevice");
   check_hip(hipFree(nullptr), "hip context init");
   stages.emplace_back("preinit_context", monotonic_ns());
-  // every launch handle resolved now: no later launch consults the
-  // runtime's fat-binary registry (kernels/launch.hpp)
-  check_hip(gemm_prepare(), "gemm_prepare");
-  check_hip(misc_prepare(), "misc_prepare");
-  check_hip(warmstart_prepare(), "warmstart_prepare");
-  stages.emplace_back("preinit_prepared", monotonic_ns());
+  // every launch handle resolved (no later launch consults the runtime's
+  // fat-binary registry, kernels/launch.hpp) and the runtime's graph
+  // set-up paid, on a helper thread while this one creates the stream:
+  // the first hardware queue (~12 ms) and the two (~7 + ~5 ms) overlap
+  hipError_t helper_err = hipSuccess;
+  const char* helper_what = "";
+  long long prepared_ns = 0;
+  std::thread helper([&] {
+    auto step = [&](hipError_t err, const char* what) {
+      if (err != hipSuccess && helper_err == hipSuccess) {
+        helper_err = err;
+        helper_what = what;
+      }
+    };
+    step(hipSetDevice(device), "hipSetDevice(helper)");
+    if (helper_err == hipSuccess) step(gemm_prepare(), "gemm_prepare");
+    if (helper_err == hipSuccess) step(misc_prepare(), "misc_prepare");
+    if (helper_err == hipSuccess) step(warmstart_prepare(), "warmstart_prepare");
+    prepared_ns = monotonic_ns();
+    if (helper_err == hipSuccess) step(graph_prewarm(device), "graph_prewarm");
+  });
   hipStream_t stream = take_kept_stream(device);
+  hipError_t stream_err = hipSuccess;
   if (!stream) {
-    check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking),
-              "hipStreamCreate");
+    stream_err = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
   }
-  stages.emplace_back("preinit_stream", monotonic_ns());
+  const long long stream_ns = monotonic_ns();
+  helper.join();
+  if (stream_err != hipSuccess || helper_err != hipSuccess) {
+    if (stream_err == hipSuccess && stream) (void)hipStreamDestroy(stream);
+    check_hip(stream_err, "hipStreamCreate");
+    check_hip(helper_err, helper_what);
+  }
+  stages.emplace_back("preinit_prepared", prepared_ns);
+  stages.emplace_back("preinit_stream", stream_ns);
+  stages.emplace_back("preinit_helper_joined", monotonic_ns());
   // 128x128 operands + bias + output + sums + warm-start record
   const size_t elems = 128 * 128;
   char* scratch = nullptr;

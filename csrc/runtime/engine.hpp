@@ -30,6 +30,9 @@ void release_kept_stream();
 unsigned long long take_stream(int device);
 void return_stream(unsigned long long handle, int device);
 std::vector<std::pair<std::string, long long>> preinit_device(int device);
+// Pays the HIP runtime's one-time graph set-up (the first instantiation of
+// a non-empty graph) on a one-memset graph; preinit_device runs it.
+hipError_t graph_prewarm(int device);
 // `context` standby: HIP context + every kernel's code object, no launch (so
 // no hardware queue and no HBM beyond the code objects).
 std::vector<std::pair<std::string, long long>> preload_modules(int device);

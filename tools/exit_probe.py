@@ -11,7 +11,9 @@ the child builds what the case names, reports, waits for ``go`` and calls
 Cases: ``ctx`` (HIP context + stream), ``engine`` (+ the production engine,
 1.3 GB), ``engine_rccl`` (+ a 1-rank RCCL communicator), ``engine_free``
 (engine closed -- hipFree -- before the exit, timed separately),
-``torch_engine_rccl`` (the PyTorch engine + RCCL).  One JSON line per case.
+``torch_engine_rccl`` (the PyTorch engine + RCCL), ``engine_rccl_abort`` /
+``engine_rccl_destroy`` (the communicator aborted / destroyed after ``go``,
+before the exit; ``teardown_ms``).  One JSON line per case.
 """
 import json
 import os
@@ -21,7 +23,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-CASES = ('ctx', 'engine', 'engine_rccl', 'engine_free', 'torch_engine_rccl')
+CASES = ('ctx', 'engine', 'engine_rccl', 'engine_free', 'torch_engine_rccl',
+         'engine_rccl_abort', 'engine_rccl_destroy')
 
 
 def child(case, mod, wfd, rfd):
@@ -41,10 +44,14 @@ def child(case, mod, wfd, rfd):
         engine = mod.Engine(0, 4096, 16384, 4, 2048, 1)
         engine.warmstart()
         keep.append(engine)
-    if case.endswith('rccl'):
+    if 'rccl' in case:
         fence = mod.Fence(mod.fence_unique_id(), 1, 0, 60.0)
         fence.allreduce([1] * 9)
         keep.append(fence)
+    if case.endswith(('_abort', '_destroy')):
+        # timed in the child just before its exit: what the comm's own
+        # teardown costs against the kernel's at exit
+        info['teardown'] = case.rsplit('_', 1)[1]
     if case == 'engine_free':
         t0 = time.monotonic_ns()
         keep[0].close()
@@ -53,6 +60,10 @@ def child(case, mod, wfd, rfd):
     info['used_gb'] = (total - free) / 1e9
     os.write(wfd, (json.dumps(info) + '\n').encode())
     os.read(rfd, 1)            # go
+    if 'teardown' in info:
+        t0 = time.monotonic_ns()
+        getattr(keep[-1], info['teardown'])()
+        os.write(wfd, ('%.3f\n' % ((time.monotonic_ns() - t0) / 1e6)).encode())
     os._exit(0)
 
 
@@ -91,6 +102,9 @@ def main():
             t0 = time.monotonic_ns()
             os.write(go_w, b'g')
             _, status = os.waitpid(pid, 0)
+            if 'teardown' in info:
+                tail = os.read(up_r, 64).decode().strip()
+                info['teardown_ms'] = float(tail) if tail else None
             info.update({'case': case, 'rep': rep,
                          'exit_ms': (time.monotonic_ns() - t0) / 1e6,
                          'status': status})
