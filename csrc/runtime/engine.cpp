@@ -8,7 +8,6 @@
 #include <cstring>
 #include <mutex>
 #include <set>
-#include <thread>
 
 #include "../kernels/kernels.hpp"
 #include "trace.hpp"
@@ -101,9 +100,9 @@ void release_kept_stream() {
 hipError_t graph_prewarm(int device) {
   // The HIP runtime's first hipGraphInstantiate of a graph with a node pays
   // a one-time set-up (5-16 ms on MI355X, whatever the graph holds; the
-  // next instantiations take 0.02-0.04 ms, profiles/r5_boot): paid here,
-  // on a graph of one 4-byte memset built without a stream, so no capture
-  // and no queue is involved and it can run beside the stream's creation.
+  // next instantiations take 0.02-0.06 ms, profiles/r5_boot): paid here,
+  // by the standby's boot, on a graph of one 4-byte memset built without a
+  // stream (no capture, no queue).
   hipError_t err = hipSetDevice(device);
   if (err != hipSuccess) return err;
   void* buf = nullptr;
@@ -138,42 +137,28 @@ std::vector<std::pair<std::string, long long>> preinit_device(int device) {
   check_hip(hipSetDevice(device), "hipSetDevice");
   check_hip(hipFree(nullptr), "hip context init");
   stages.emplace_back("preinit_context", monotonic_ns());
-  // every launch handle resolved (no later launch consults the runtime's
-  // fat-binary registry, kernels/launch.hpp) and the runtime's graph
-  // set-up paid, on a helper thread while this one creates the stream:
-  // the first hardware queue (~12 ms) and the two (~7 + ~5 ms) overlap
-  hipError_t helper_err = hipSuccess;
-  const char* helper_what = "";
-  long long prepared_ns = 0;
-  std::thread helper([&] {
-    auto step = [&](hipError_t err, const char* what) {
-      if (err != hipSuccess && helper_err == hipSuccess) {
-        helper_err = err;
-        helper_what = what;
-      }
-    };
-    step(hipSetDevice(device), "hipSetDevice(helper)");
-    if (helper_err == hipSuccess) step(gemm_prepare(), "gemm_prepare");
-    if (helper_err == hipSuccess) step(misc_prepare(), "misc_prepare");
-    if (helper_err == hipSuccess) step(warmstart_prepare(), "warmstart_prepare");
-    prepared_ns = monotonic_ns();
-    if (helper_err == hipSuccess) step(graph_prewarm(device), "graph_prewarm");
-  });
+  // every launch handle resolved now: no later launch consults the
+  // runtime's fat-binary registry (kernels/launch.hpp).  (Run beside the
+  // stream's creation on a helper thread, the two only slowed each other:
+  // 19 + 17 ms against 7 + 12 ms, profiles/r5_boot.)
+  check_hip(gemm_prepare(), "gemm_prepare");
+  check_hip(misc_prepare(), "misc_prepare");
+  check_hip(warmstart_prepare(), "warmstart_prepare");
+  stages.emplace_back("preinit_prepared", monotonic_ns());
   hipStream_t stream = take_kept_stream(device);
-  hipError_t stream_err = hipSuccess;
   if (!stream) {
-    stream_err = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+    check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking),
+              "hipStreamCreate");
   }
-  const long long stream_ns = monotonic_ns();
-  helper.join();
-  if (stream_err != hipSuccess || helper_err != hipSuccess) {
-    if (stream_err == hipSuccess && stream) (void)hipStreamDestroy(stream);
-    check_hip(stream_err, "hipStreamCreate");
-    check_hip(helper_err, helper_what);
+  stages.emplace_back("preinit_stream", monotonic_ns());
+  // the engine's first graph then instantiates in 0.05 ms instead of 6-16
+  try {
+    check_hip(graph_prewarm(device), "graph_prewarm");
+  } catch (...) {
+    (void)hipStreamDestroy(stream);
+    throw;
   }
-  stages.emplace_back("preinit_prepared", prepared_ns);
-  stages.emplace_back("preinit_stream", stream_ns);
-  stages.emplace_back("preinit_helper_joined", monotonic_ns());
+  stages.emplace_back("preinit_graph_prewarm", monotonic_ns());
   // 128x128 operands + bias + output + sums + warm-start record
   const size_t elems = 128 * 128;
   char* scratch = nullptr;
