@@ -45,8 +45,14 @@ def child(case, mod, wfd, rfd):
         engine.warmstart()
         keep.append(engine)
     if 'rccl' in case:
+        free, total = mod.mem_info()
+        before = total - free
+        t0 = time.monotonic_ns()
         fence = mod.Fence(mod.fence_unique_id(), 1, 0, 60.0)
         fence.allreduce([1] * 9)
+        info['rccl_init_ms'] = (time.monotonic_ns() - t0) / 1e6
+        free, total = mod.mem_info()
+        info['rccl_hbm_mb'] = (total - free - before) / 1e6
         keep.append(fence)
     if case.endswith(('_abort', '_destroy')):
         # timed in the child just before its exit: what the comm's own
