@@ -242,6 +242,69 @@ def test_fence_warmup_and_preinit(mod):
     assert list(stages.values()) == sorted(stages.values())
 
 
+def test_preinit_pays_the_graph_setup(mod):
+    """``preinit_device`` ends with the runtime's one-time graph set-up
+    (``graph_prewarm``, profiles/r5_boot) after the stream, and the call is
+    repeatable on its own."""
+    stages = mod.preinit_device(0)
+    names = list(stages)
+    assert names.index('preinit_graph_prewarm') == \
+        names.index('preinit_stream') + 1
+    assert mod.graph_prewarm(0) >= 0.0
+
+
+def test_stream_graph_replays_kernels_and_copies(mod):
+    """``StreamGraph`` (the PyTorch engine's native capture): a pinned-host
+    word copied in, a kernel seeded from it, the result copied out -- one
+    launch per replay, a new host word per replay; ``abort`` ends a failed
+    capture so the stream is usable again."""
+    stream = torch.cuda.Stream()
+    s = stream.cuda_stream
+    seed_host = torch.zeros(1, dtype=torch.int64).pin_memory()
+    seed_dev = torch.zeros(1, dtype=torch.int64, device='cuda')
+    buf = torch.empty(4096, dtype=torch.bfloat16, device='cuda')
+    out_host = torch.zeros(4096, dtype=torch.bfloat16).pin_memory()
+    torch.cuda.synchronize()
+    graph = mod.StreamGraph(s)
+    assert not graph.ready
+    with pytest.raises(RuntimeError):
+        graph.launch()
+    graph.begin()
+    mod.memcpy_async(seed_dev.data_ptr(), seed_host.data_ptr(), 8, s)
+    mod.init_uniform_bf16_devseed(buf.data_ptr(), buf.numel(),
+                                  seed_dev.data_ptr(), -1.0, 1.0, s)
+    mod.memcpy_async(out_host.data_ptr(), buf.data_ptr(), buf.numel() * 2, s)
+    graph.end()
+    assert graph.ready and graph.instantiate_us >= 0
+    results = []
+    for seed in (5, 6, 5):
+        stream.synchronize()
+        seed_host[0] = seed
+        graph.launch()
+        stream.synchronize()
+        results.append(out_host.clone())
+    # the eager kernel with the same seeds
+    for seed, got in zip((5, 6, 5), results):
+        ref = torch.empty_like(buf)
+        seed_dev.fill_(seed)
+        torch.cuda.synchronize()
+        mod.init_uniform_bf16_devseed(ref.data_ptr(), ref.numel(),
+                                      seed_dev.data_ptr(), -1.0, 1.0, 0)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref.cpu())
+    assert not torch.equal(results[0], results[1])
+    assert torch.equal(results[0], results[2])
+    # a capture abandoned half-way leaves the stream capturable again
+    graph.begin()
+    mod.memset_async(buf.data_ptr(), 0, 64, s)
+    graph.abort()
+    mod.memset_async(buf.data_ptr(), 0, buf.numel() * 2, s)
+    stream.synchronize()
+    assert int(buf.float().abs().sum()) == 0
+    graph.reset()
+    assert not graph.ready
+
+
 def test_preload_modules_stamps(mod):
     """The context standby's code-object preload (no launch) reports its
     stages in order."""

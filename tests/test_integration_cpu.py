@@ -366,6 +366,26 @@ def test_zygote_cold_spawn_reaped_like_a_child(stack):
             os.waitpid(pid, os.WNOHANG)
 
 
+def test_dead_embryos_are_skipped_and_replaced(stack):
+    """An embryo killed while it waits costs nothing but its speed: the
+    zygote finds it gone when it hands it a request, forks the worker the
+    slow way, and restocks."""
+    s, client, manager, scaler, events = stack(WARM_POOL='0')
+    wait_for(lambda: manager.zygote.poll_ready(), timeout=60)
+    killed = wait_for(lambda: manager.zygote.embryo_pids(), timeout=10)
+    for pid in killed:
+        os.kill(pid, signal.SIGKILL)
+    enqueue(client, 1)
+    assert tick(scaler, s) == 1
+    wait_for(lambda: client.hget('predict:job0', 'status') == 'done',
+             timeout=30)
+    spawn = [e for e in events.records if e['ev'] == 'process_spawn'][-1]
+    assert spawn['via'] == 'zygote' and spawn['embryo'] is False
+    fresh = wait_for(lambda: manager.zygote.embryo_pids() - killed,
+                     timeout=10)
+    assert fresh and not fresh & killed
+
+
 def test_dead_zygote_is_restarted(stack):
     """A zygote that dies costs the fast path only until it is restarted;
     spawns meanwhile go through exec."""
