@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The PyTorch-ROCm engine's lifecycle for rocprofv3: a standby's boot
 (``preinit_device``, ``warm_device``), the engine build (one DLPack arena,
-weights by the init kernel, forward + warm-start CUDA graphs), READY (one
+weights by the init kernel, forward + warm-start native hipGraphs), READY (one
 warm-start graph launch) and K keys of forward passes.
 
 Under ``rocprofv3 --kernel-trace --stats`` the kernel table shows that the
