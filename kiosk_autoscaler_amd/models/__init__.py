@@ -4,7 +4,7 @@ Engines a worker can run (``WORKER_ENGINE``):
 
 * ``torch-kiosk`` (default on GPU slots) -- the PyTorch-ROCm engine
   (:class:`.torch_kiosk.TorchKioskEngine`): torch tensors, torch's stream and
-  CUDA graphs around the hand-written gfx950 kernels;
+  native hipGraphs around the hand-written gfx950 kernels;
 * ``builtin`` -- the torch-free engine of the native module
   (:class:`.mlp.HipMlpEngine`), spawned with ``python -S``;
 * ``torch-mlp`` -- the plain-PyTorch example (:mod:`.torch_engine`);
