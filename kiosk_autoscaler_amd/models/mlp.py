@@ -184,6 +184,8 @@ class HipMlpEngine(object):
             self.measure(self.cfg.rows, passes=1)
         info['pass_ms'] = self.pass_ms[self.cfg.rows]
         info['reused'] = self.reused
+        # the engine name the bench reports (engines_seen)
+        info['backend'] = 'builtin'
         return info
 
     def hbm_bytes(self):
