@@ -24,7 +24,7 @@ import timeit
 
 from . import policy as policies
 from .gpumgr.resources import ActuatorError
-from .utils.events import NULL as NULL_EVENTS
+from .utils.events import NULL as NULL_EVENTS, now_ns
 from .utils.keys import worker_of
 
 
@@ -292,10 +292,8 @@ class Autoscaler(object):
                           '%s pods and a desired state of %s pods.',
                           str(resource_type).capitalize(), name, namespace,
                           current_pods, desired_pods)
-        self.events.emit('tick', keys=dict(self.redis_keys),
-                         in_progress=dict(self.in_progress),
-                         current=current_pods, desired=desired_pods,
-                         tick_s=self._clock() - tick_start)
+        tick_s = self._clock() - tick_start
+        decided_ns = now_ns()
         self.last_decision = desired_pods
         try:
             self.scale_resource(desired_pods, current_pods, resource_type,
@@ -304,4 +302,11 @@ class Autoscaler(object):
             self.logger.warning('Failed to scale %s `%s.%s` due to %s: %s',
                                 resource_type, namespace, name,
                                 type(err).__name__, err)
+        # stamped at the decision, sent after the actuator call: with a
+        # Redis event sink the send is a round trip the PATCH need not wait
+        # for (profiles/r5_boot)
+        self.events.emit('tick', t_ns=decided_ns, keys=dict(self.redis_keys),
+                         in_progress=dict(self.in_progress),
+                         current=current_pods, desired=desired_pods,
+                         tick_s=tick_s)
         return desired_pods

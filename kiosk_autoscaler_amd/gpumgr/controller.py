@@ -253,8 +253,12 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
             resource.declared = declared
             resource.generation += 1
             self._persist(resource)
-            self.events.emit('patch', kind=kind, name=name, declared=declared)
+            patched_ns = time.monotonic_ns()
             self._reconcile(resource)
+            # stamped before the reconcile, sent after it: the assignment
+            # does not wait for the event sink's round trip
+            self.events.emit('patch', t_ns=patched_ns, kind=kind, name=name,
+                             declared=declared)
             view = resource.view()
         self._wake()
         return view
@@ -513,8 +517,10 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
         }
         proc = self._take_standby(resource.template, slot)
         from_pool = proc is not None
+        sizing = None
         if from_pool and proc.hbm_free:
-            self._size_from_free(resource, assign, proc.hbm_free, slot)
+            sizing = self._size_from_free(resource, assign, proc.hbm_free,
+                                          slot)
         if from_pool:
             if not proc.pipe.send(assign):
                 proc.popen.kill()
@@ -526,6 +532,8 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
         proc.role = 'worker'
         worker = Worker(wid, resource, slot, proc, from_pool)
         resource.workers[wid] = worker
+        if sizing is not None:
+            self.events.emit('hbm_sizing', **sizing)
         self.events.emit('worker_assigned', worker=wid, gpu=slot.index,
                          pid=proc.pid, from_pool=from_pool,
                          resource=resource.name)
@@ -536,7 +544,8 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
 
     def _size_from_free(self, resource, assign, free, slot):
         """N5: clamp this assignment's KEYS_PER_POD (the job worker's batch)
-        to what fits in the HBM the standby measured free."""
+        to what fits in the HBM the standby measured free.  Returns the
+        ``hbm_sizing`` event's fields."""
         from ..utils import hbm
         tpl = resource.template
         env = tpl.env
@@ -558,9 +567,10 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                            tpl.keys_per_pod, free / 1e9, slot.index, limit,
                            kpp)
         assign['template'] = dict(assign['template'], keys_per_pod=kpp)
-        self.events.emit('hbm_sizing', gpu=slot.index, hbm_free=free,
-                         max_keys_per_pod=limit, keys_per_pod=kpp,
-                         requested=tpl.keys_per_pod)
+        # the event's fields: sent once the assignment is on its way
+        return {'t_ns': time.monotonic_ns(), 'gpu': slot.index,
+                'hbm_free': free, 'max_keys_per_pod': limit,
+                'keys_per_pod': kpp, 'requested': tpl.keys_per_pod}
 
     def _drain(self, worker, reason, recycle=None):
         if worker.state in (DRAINING, EXITED):

@@ -232,15 +232,20 @@ class WorkerRuntime(object):
         self.redis = self.redis_factory()
         self.engine = self.engine_factory(cfg, self._stage)
         self._stage('weights_ready')
+        info = None
         if cfg.warm_start:
             info = self.engine.warmstart()
-            self._stage('warmstart_done')
-            self._emit_event('warmstart', **{k: v for k, v in info.items()
-                                             if k != 'cu_mask'})
+            t_warm = self._stage('warmstart_done')
         if self.faults:
             self.faults.at_start()
         t_ready = self._stage('ready')
         self.channel.emit('ready', t=t_ready, stages=self.stages)
+        if info is not None:
+            # stamped at the warm start, sent after READY (an event sink
+            # round trip READY need not wait for)
+            self._emit_event('warmstart', t_ns=t_warm,
+                             **{k: v for k, v in info.items()
+                                if k != 'cu_mask'})
         self._emit_event('worker_ready', gpu=cfg.slot, t_ns=t_ready,
                          stages=self.stages)
         if self.node_agent is not None:
