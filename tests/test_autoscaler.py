@@ -155,6 +155,38 @@ def test_scale(redis_client):
                      name='test')
 
 
+def test_tick_event_is_stamped_at_the_decision_and_sent_after_the_patch(
+        redis_client):
+    """The ``tick`` event carries the decision instant but is sent once the
+    actuator call returned (a Redis event sink's round trip stays off the
+    PATCH), also when the PATCH fails."""
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    events = EventLog(source='test')
+    events.keep = True
+    scaler = make(redis_client, events=events)
+    redis_client.lpush('queue', 'a', 'b')
+    sent = []
+    actuator = scaler.actuator
+    real = actuator.patch_namespaced_job
+
+    def patch(*args):
+        sent.append([e['ev'] for e in events.records])
+        return real(*args)
+    actuator.patch_namespaced_job = patch
+    scaler.scale(namespace='ns', resource_type='job', name='pod1',
+                 max_pods=4)
+    assert sent == [[]]                     # nothing sent before the PATCH
+    kinds = [e['ev'] for e in events.records]
+    assert kinds == ['scale', 'tick']
+    scale_ev, tick_ev = events.records
+    assert tick_ev['t'] <= scale_ev['t'] and tick_ev['desired'] == 2
+    actuator.patch_namespaced_job = actuator_error
+    redis_client.lpush('queue', 'c')
+    scaler.scale(namespace='ns', resource_type='job', name='pod1',
+                 max_pods=4)
+    assert events.records[-1]['ev'] == 'tick'
+
+
 def test_scale_decisions(redis_client):
     """The reference test is smoke-only; assert the actual decisions."""
     scaler = make(redis_client, queues='predict,track')
