@@ -196,6 +196,98 @@ def test_slim_keeps_one_isa_uncompressed_and_stripped(tmp_path, tool,
     assert ctypes.CDLL(out).ncclGetVersion(ctypes.byref(ctypes.c_int())) == 0
 
 
+@pytest.fixture(scope='module')
+def asan_tool():
+    import build_native
+    try:
+        path = build_native.build_rccl_slim(sanitize=True)
+    except Exception as err:  # pylint: disable=broad-except
+        pytest.skip('no sanitizer build: %s' % err)
+    if path is None or not os.path.exists(path):
+        pytest.skip('kiosk-rccl-slim-asan not built')
+    return path
+
+
+# size fields the tool bounds by the section instead of trusting: a bogus
+# value leaves the result intact
+_TOLERATED = ('ccob_total_huge', 'ccob_inflated_huge')
+
+
+def _corruptions(lib):
+    """Truncated and corrupted copies of a good library: the tool must
+    refuse each (exit 2) without reading out of bounds, or -- for a size
+    field it bounds itself (``_TOLERATED``) -- still slim it."""
+    with open(lib, 'rb') as f:
+        good = f.read()
+    sec_off, sec_size = _section(lib, '.hip_fatbin')
+    out = {'empty': b'', 'elf_header_only': good[:64],
+           'cut_before_section': good[:sec_off + 16],
+           'cut_in_section': good[:sec_off + sec_size // 2]}
+    shoff, = struct.unpack_from('<Q', good, 0x28)
+
+    def patched(offset, fmt, value):
+        blob = bytearray(good)
+        struct.pack_into(fmt, blob, offset, value)
+        return bytes(blob)
+    out['shoff_past_eof'] = patched(0x28, '<Q', len(good) + 4096)
+    out['shnum_huge'] = patched(0x3c, '<H', 0xfff0)
+    out['shstrndx_bad'] = patched(0x3e, '<H', 0xfff0)
+    body = sec_off
+    if good[body:body + 4] == b'CCOB':
+        out['ccob_total_huge'] = patched(body + 8, '<Q', 1 << 60)
+        out['ccob_inflated_huge'] = patched(body + 16, '<Q', 1 << 60)
+        out['ccob_payload_garbage'] = patched(body + 32, '<Q',
+                                              0x4141414141414141)
+        out['ccob_version_9'] = patched(body + 4, '<H', 9)
+    else:
+        out['bundle_count_huge'] = patched(body + 24, '<Q', 1 << 40)
+        # the gfx950 entry's offset / size, and an id length past the table
+        pos = body + 32
+        count, = struct.unpack_from('<Q', good, body + 24)
+        for _ in range(count):
+            _, size, idlen = struct.unpack_from('<QQQ', good, pos)
+            if size:
+                break
+            pos += 24 + idlen
+        out['entry_offset_past_end'] = patched(pos, '<Q', 1 << 40)
+        out['entry_size_huge'] = patched(pos + 8, '<Q', 1 << 40)
+        out['entry_offset_wraps'] = patched(pos, '<Q', (1 << 64) - 16)
+        out['entry_idlen_huge'] = patched(body + 48, '<Q', 1 << 40)
+    return out
+
+
+@pytest.mark.parametrize('compressed', [True, False])
+def test_sanitized_slim_survives_malformed_libraries(tmp_path, asan_tool,
+                                                     compressed):
+    """SURVEY §5.2 for the new parser: under ASan+UBSan the tool slims a
+    good library and refuses truncated / corrupted ELF and bundle headers
+    cleanly (exit 2, no sanitizer report)."""
+    tmp = str(tmp_path)
+    bundle = _bundle([('host-x86_64-unknown-linux-gnu-', b''),
+                      ('hipv4-amdgcn-amd-amdhsa--gfx950',
+                       _code_object(tmp, 'k950', 5))])
+    lib = _library(tmp, _ccob(bundle) if compressed else bundle,
+                   slack=len(bundle))
+    env = dict(os.environ, ASAN_OPTIONS='detect_leaks=1:exitcode=99',
+               UBSAN_OPTIONS='halt_on_error=1:exitcode=98')
+    ok = subprocess.run([asan_tool, '--src', lib, '--out',
+                         os.path.join(tmp, 'ok.so')], env=env,
+                        capture_output=True, text=True, timeout=120)
+    assert ok.returncode == 0, ok.stderr[-2000:]
+    for name, blob in _corruptions(lib).items():
+        bad = os.path.join(tmp, 'bad_%s.so' % name)
+        with open(bad, 'wb') as f:
+            f.write(blob)
+        proc = subprocess.run([asan_tool, '--src', bad, '--out',
+                               os.path.join(tmp, 'out_%s.so' % name)],
+                              env=env, capture_output=True, text=True,
+                              timeout=120)
+        assert 'Sanitizer' not in proc.stderr, (name, proc.stderr[-3000:])
+        want = 0 if name in _TOLERATED else 2
+        assert proc.returncode == want, (name, proc.returncode,
+                                         proc.stderr[-2000:])
+
+
 def test_slim_refuses_a_bundle_without_the_isa(tmp_path, tool):
     tmp = str(tmp_path)
     bundle = _bundle([('host-x86_64-unknown-linux-gnu-', b''),

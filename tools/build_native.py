@@ -148,19 +148,27 @@ def build_kredis(verbose=False, sanitize=False):
     return target
 
 
-def build_rccl_slim(verbose=False):
+RCCL_SLIM_ASAN = os.path.join(BUILD, 'kiosk-rccl-slim-asan')
+
+
+def build_rccl_slim(verbose=False, sanitize=False):
     """``build/kiosk-rccl-slim`` (g++, host only): writes the one-ISA,
     uncompressed, debug-stripped copy of RCCL the workers load
-    (``parallel/rccl_lib.py``; csrc/tools/rccl_slim.cpp has the why)."""
+    (``parallel/rccl_lib.py``; csrc/tools/rccl_slim.cpp has the why).
+    With ``sanitize`` the ASan+UBSan build ``build/kiosk-rccl-slim-asan``
+    (it parses ELF and offload-bundle headers: tests/test_rccl_slim.py
+    feeds it truncated and corrupted ones)."""
     src = os.path.join(ROOT, 'csrc', 'tools', 'rccl_slim.cpp')
     if not os.path.exists(src):
         return None
     os.makedirs(BUILD, exist_ok=True)
-    if _stale(RCCL_SLIM, [src]):
+    target = RCCL_SLIM_ASAN if sanitize else RCCL_SLIM
+    flags = SANITIZE_FLAGS if sanitize else ['-O2']
+    if _stale(target, [src]):
         cxx = shutil.which('g++') or 'c++'
-        _run([cxx, '-O2', '-std=c++17', '-Wall', src, '-o', RCCL_SLIM,
-              '-ldl'], verbose)
-    return RCCL_SLIM
+        _run([cxx] + flags + ['-std=c++17', '-Wall', src, '-o', target,
+                              '-ldl'], verbose)
+    return target
 
 
 def build_fake(verbose=False):
@@ -204,6 +212,7 @@ def build(verbose=False, clean=False, jobs=4, kernels=True, sanitize=False,
         out['fake_fence'] = build_fake(verbose)
     if sanitize:
         out['kredis_asan'] = build_kredis(verbose, sanitize=True)
+        out['rccl_slim_asan'] = build_rccl_slim(verbose, sanitize=True)
     if kernels:
         objects = compile_units(verbose, jobs)
         out['extension'] = link_extension(objects, verbose)
@@ -217,7 +226,8 @@ def main():
     parser.add_argument('-j', '--jobs', type=int, default=4)
     parser.add_argument('--no-kernels', action='store_true')
     parser.add_argument('--sanitize', action='store_true',
-                        help='also build the ASan+UBSan kredis-server')
+                        help='also build the ASan+UBSan kredis-server and '
+                             'kiosk-rccl-slim')
     parser.add_argument('--fake-hip', action='store_true',
                         help='only the CPU fence module over the fake '
                              'HIP + RCCL (build/fake)')
