@@ -7,9 +7,7 @@ some; everything after it is stable).  Torch-free (ROCm 7.2's runtime)
 unless ``--torch``.  One JSON line per process.
 """
 import argparse
-import ctypes
 import json
-import os
 import subprocess
 import sys
 import time
