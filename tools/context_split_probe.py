@@ -50,18 +50,31 @@ def main():
     ap.add_argument('--n', type=int, default=12)
     ap.add_argument('--torch', action='store_true')
     ap.add_argument('--gap', type=float, default=0.5)
+    ap.add_argument('--variants', default='',
+                    help="comma-separated NAME=VALUE environment variants "
+                         "(each its own --n processes; 'default' = as is), "
+                         "interleaved process by process")
     args = ap.parse_args()
-    rows = []
-    for _ in range(args.n):
+    import itertools
+    import os
+    variants = [v for v in args.variants.split(',') if v] or ['default']
+    # interleaved, process by process: a slow spell of the box hits every
+    # variant alike
+    for _, variant in itertools.product(range(args.n), variants):
+        env = dict(os.environ)
+        if '=' in variant:
+            name, _, value = variant.partition('=')
+            env[name] = value
         t0 = time.perf_counter()
         out = subprocess.run([sys.executable, '-c', CHILD,
                               '1' if args.torch else '0'],
-                             capture_output=True, text=True, timeout=120)
+                             capture_output=True, text=True, timeout=120,
+                             env=env)
         line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() \
             else json.dumps({'error': out.stderr[-500:]})
         row = json.loads(line)
         row['process_ms'] = round((time.perf_counter() - t0) * 1e3, 1)
-        rows.append(row)
+        row['variant'] = variant
         print(json.dumps(row), flush=True)
         time.sleep(args.gap)
     return 0
