@@ -380,6 +380,9 @@ def _embryo(esock):
             except OSError:
                 pass
     signal.signal(signal.SIGTERM, signal.SIG_DFL)
+    if _hsa_preinit_wanted():
+        import threading
+        threading.Thread(target=_hsa_preinit, daemon=True).start()
     try:
         payload, fds, _flags, _addr = socket.recv_fds(esock, MAX_MSG, 4)
     except OSError:
@@ -387,6 +390,36 @@ def _embryo(esock):
     if not payload or len(fds) != 2:
         os._exit(0)
     _child(json.loads(payload), fds, esock)
+
+
+# s an embryo waits before its ROCr init: the replacement forked right
+# after a hand-off stays clear of the woken worker's own boot
+HSA_PREINIT_DELAY_S = 1.0
+
+
+def _hsa_preinit_wanted():
+    """``KIOSK_EMBRYO_HSA=1``: the embryo runs ROCr's ``hsa_init`` while it
+    waits.  That is the variable part of a woken standby's HIP context --
+    45-60 ms, but 110-300 ms in a third of fresh processes on a busy host
+    (profiles/r5_boot/context_split.jsonl) -- and it binds no device: HIP
+    applies ``HIP_VISIBLE_DEVICES`` (the slot pin, set from the request)
+    at ``hipInit``.  Not with ``ROCR_VISIBLE_DEVICES`` pinning, which ROCr
+    reads at ``hsa_init`` itself."""
+    return os.environ.get('KIOSK_EMBRYO_HSA', '') == '1' and \
+        'ROCR_VISIBLE_DEVICES' not in os.environ
+
+
+def _hsa_preinit():
+    time.sleep(HSA_PREINIT_DELAY_S)
+    try:
+        import ctypes
+        # the runtime the process already mapped (torch's copy in a torch
+        # zygote, ROCm's otherwise): matched by soname, reference-counted,
+        # so HIP's own init later returns at once
+        lib = ctypes.CDLL('libhsa-runtime64.so.1', mode=ctypes.RTLD_GLOBAL)
+        lib.hsa_init()
+    except (OSError, AttributeError):
+        pass
 
 
 class _Embryos(object):
