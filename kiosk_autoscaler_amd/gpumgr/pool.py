@@ -114,10 +114,12 @@ class PoolMixin(object):
         argv = self._interpreter(tpl) + [
             '-m', 'kiosk_autoscaler_amd.worker.zygote', '--backend',
             tpl.backend]
+        rocr = self.zygote_rocr_embryos(tpl)
         self.zygote = zygote.ZygoteClient(argv, self._environment(tpl),
-                                          embryos=self.zygote_embryos())
+                                          embryos=self.zygote_embryos(),
+                                          rocr_embryos=rocr)
         self.events.emit('zygote_spawn', pid=self.zygote.pid,
-                         embryos=self.zygote_embryos())
+                         embryos=self.zygote_embryos(), rocr_embryos=rocr)
 
     def zygote_embryos(self):
         """Pre-forked workers the zygote keeps (one per GPU slot, at most
@@ -128,6 +130,22 @@ class PoolMixin(object):
         if override.strip():
             return max(0, int(override))
         return min(8, max(1, len(self.slots)))
+
+    def zygote_rocr_embryos(self, template):
+        """How many embryos initialise ROCr while they wait (HIP workers
+        only; ``ZYGOTE_ROCR_EMBRYOS`` overrides, 0 = none).  Each halves a
+        woken standby's boot (~105 -> ~50 ms, profiles/r5_boot) and takes
+        ROCr's init variance (110-300 ms spikes) off the scale-up path, but
+        opens the device: two, so a full node's workers plus these stay
+        well inside a per-device process budget."""
+        if template is None or template.backend not in ('hip', 'auto') or \
+                not any(getattr(slot, 'kind', 'gpu') != 'cpu'
+                        for slot in self.slots):
+            return 0
+        override = os.environ.get('ZYGOTE_ROCR_EMBRYOS', '')
+        if override.strip():
+            return min(self.zygote_embryos(), max(0, int(override)))
+        return min(2, self.zygote_embryos())
 
     def _check_zygote(self):
         """False (and the zygote forgotten, restarted after a pause) once

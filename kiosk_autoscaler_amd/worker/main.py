@@ -416,6 +416,11 @@ def main(argv=None):
         try:
             mod = native.load()
             preinit = dict(mod.preinit_device(0))
+            if os.environ.get('KIOSK_EMBRYO_HSA_NS'):
+                # ROCr was initialised while this process waited as an
+                # embryo (worker/zygote.py _HsaPreinit)
+                preinit['embryo_hsa_ns'] = int(
+                    os.environ.pop('KIOSK_EMBRYO_HSA_NS'))
             # a PyTorch plug-in: torch's CUDA init + hipBLASLt handle too
             preinit.update(_warm_torch())
             if not node and os.environ.get('FENCE', 'auto') in ('auto',

@@ -106,7 +106,7 @@ class ZygoteLost(OSError):
 class ZygoteClient(object):
     """Manager side: start the zygote, fork workers from it."""
 
-    def __init__(self, argv, env, timeout=10.0, embryos=0):
+    def __init__(self, argv, env, timeout=10.0, embryos=0, rocr_embryos=0):
         import subprocess
         self.sock, child = socket.socketpair(socket.AF_UNIX,
                                              socket.SOCK_SEQPACKET)
@@ -115,7 +115,8 @@ class ZygoteClient(object):
         self.embryos = set()        # pids of the zygote's pre-forked workers
         self.popen = subprocess.Popen(
             list(argv) + ['--zygote-fd', str(child.fileno()),
-                          '--embryos', str(int(embryos))], env=env,
+                          '--embryos', str(int(embryos)),
+                          '--rocr-embryos', str(int(rocr_embryos))], env=env,
             pass_fds=(child.fileno(),), close_fds=True,
             start_new_session=True)
         child.close()
@@ -293,8 +294,10 @@ def _child(request, fds, sock):
         os.setsid()
     except OSError:
         pass                    # an embryo: already a session leader
+    hsa_ns = _PREINIT.settle(request)
     cmd_r, ev_w = fds
-    keep = {0, 1, 2, cmd_r, ev_w}
+    # (a kept ROCr runtime's own descriptors: KFD, render node, events)
+    keep = {0, 1, 2, cmd_r, ev_w} | _PREINIT.fds
     for fd in range(3, 1024):
         if fd not in keep:
             try:
@@ -305,6 +308,8 @@ def _child(request, fds, sock):
         signal.signal(sig, signal.SIG_DFL)
     os.environ.clear()
     os.environ.update(request['env'])
+    if hsa_ns is not None:
+        os.environ['KIOSK_EMBRYO_HSA_NS'] = str(hsa_ns)
     argv = list(request['argv'])
     # the fds were renumbered by SCM_RIGHTS: point the worker at them
     for flag, fd in (('--cmd-fd', cmd_r), ('--ev-fd', ev_w)):
@@ -363,11 +368,12 @@ def _double_fork(body):
     return int(data) if data else None
 
 
-def _embryo(esock):
+def _embryo(esock, rocr=False):
     """A pre-forked worker waiting for its request (profiles/r5_boot: the
     double ``fork`` of a torch-sized zygote, ~20 ms, was on every woken
-    standby's critical path).  It holds no GPU and no pipe of the manager's
-    until the request comes; the zygote going away ends it."""
+    standby's critical path).  It holds no GPU memory and no pipe of the
+    manager's until the request comes; the zygote going away ends it.
+    ``rocr``: it initialises ROCr while it waits (:class:`_HsaPreinit`)."""
     try:
         os.setsid()
     except OSError:
@@ -380,9 +386,8 @@ def _embryo(esock):
             except OSError:
                 pass
     signal.signal(signal.SIGTERM, signal.SIG_DFL)
-    if _hsa_preinit_wanted():
-        import threading
-        threading.Thread(target=_hsa_preinit, daemon=True).start()
+    if rocr:
+        _PREINIT.start()
     try:
         payload, fds, _flags, _addr = socket.recv_fds(esock, MAX_MSG, 4)
     except OSError:
@@ -392,57 +397,144 @@ def _embryo(esock):
     _child(json.loads(payload), fds, esock)
 
 
-# s an embryo waits before its ROCr init: the replacement forked right
-# after a hand-off stays clear of the woken worker's own boot
-HSA_PREINIT_DELAY_S = 1.0
+class _HsaPreinit(object):
+    """An embryo runs ROCr's ``hsa_init`` while it waits (``--rocr-embryos``
+    of them).  That is the variable part of a woken standby's HIP context --
+    45-60 ms, 110-300 ms in a third of fresh processes on a busy host
+    (profiles/r5_boot/context_split.jsonl) -- and HIP's own set-up after it
+    is 4-11 ms: a woken boot goes from ~105 ms to ~50 ms (profiles/r5_boot).
+    It maps no HBM (idle-node HBM stays 1 MiB) but opens the KFD, so it is
+    one more process on the device: few of them (the pool's default is 2).
+
+    ROCr reads ``ROCR_VISIBLE_DEVICES`` at ``hsa_init``, HIP applies
+    ``HIP_VISIBLE_DEVICES`` at ``hipInit``: the embryo initialises under the
+    zygote's environment and, at the hand-off, keeps that runtime only if
+    the worker's pin gives the same ``ROCR_VISIBLE_DEVICES``; otherwise it
+    shuts ROCr down again and HIP initialises it afresh."""
+
+    # seconds an embryo waits before its init: the replacement forked right
+    # after a hand-off stays clear of the woken worker's own boot
+    DELAY_S = 1.0
+
+    def __init__(self):
+        self.thread = None
+        self.cancel = None
+        self.lib = None
+        self.rocr = None
+        self.done_ns = None
+        self.fds = set()
+
+    def start(self):
+        import threading
+        self.rocr = os.environ.get('ROCR_VISIBLE_DEVICES')
+        self.cancel = threading.Event()
+        self.thread = threading.Thread(target=self._run, daemon=True)
+        self.thread.start()
+
+    def _run(self):
+        if self.cancel.wait(self.DELAY_S):
+            return                  # the request came first
+        try:
+            import ctypes
+            # the runtime the process already mapped (torch's copy in a
+            # torch zygote, ROCm's otherwise), matched by soname and
+            # reference-counted: HIP's own hsa_init later returns at once
+            lib = ctypes.CDLL('libhsa-runtime64.so.1', mode=ctypes.RTLD_GLOBAL)
+            before = _open_fds()
+            if lib.hsa_init() == 0:
+                self.fds = _open_fds() - before
+                self.lib = lib
+                self.done_ns = time.monotonic_ns()
+        except (OSError, AttributeError):
+            pass
+
+    def settle(self, request):
+        """At the hand-off, before the worker's environment is applied:
+        the ``monotonic_ns`` stamp of a kept init, or None."""
+        if self.thread is None:
+            return None
+        self.cancel.set()
+        self.thread.join()
+        if self.lib is None:
+            self._say('no ROCr init before the request')
+            return None
+        rocr = _worker_rocr(request)
+        if rocr == self.rocr:
+            return self.done_ns
+        self.lib.hsa_shut_down()
+        self.lib = None
+        # (self.fds stay open: the thunk below ROCr keeps its KFD descriptor
+        # across a shut-down and reuses it at the next init)
+        self._say('ROCr shut down: the worker pins ROCR_VISIBLE_DEVICES=%s, '
+                  'initialised with %s' % (rocr, self.rocr))
+        return None
+
+    @staticmethod
+    def _say(text):
+        sys.stderr.write('embryo %d: %s\n' % (os.getpid(), text))
 
 
-def _hsa_preinit_wanted():
-    """``KIOSK_EMBRYO_HSA=1``: the embryo runs ROCr's ``hsa_init`` while it
-    waits.  That is the variable part of a woken standby's HIP context --
-    45-60 ms, but 110-300 ms in a third of fresh processes on a busy host
-    (profiles/r5_boot/context_split.jsonl) -- and it binds no device: HIP
-    applies ``HIP_VISIBLE_DEVICES`` (the slot pin, set from the request)
-    at ``hipInit``.  Not with ``ROCR_VISIBLE_DEVICES`` pinning, which ROCr
-    reads at ``hsa_init`` itself."""
-    return os.environ.get('KIOSK_EMBRYO_HSA', '') == '1' and \
-        'ROCR_VISIBLE_DEVICES' not in os.environ
+_PREINIT = _HsaPreinit()
 
 
-def _hsa_preinit():
-    time.sleep(HSA_PREINIT_DELAY_S)
+def _open_fds():
     try:
-        import ctypes
-        # the runtime the process already mapped (torch's copy in a torch
-        # zygote, ROCm's otherwise): matched by soname, reference-counted,
-        # so HIP's own init later returns at once
-        lib = ctypes.CDLL('libhsa-runtime64.so.1', mode=ctypes.RTLD_GLOBAL)
-        lib.hsa_init()
-    except (OSError, AttributeError):
-        pass
+        listed = [int(fd) for fd in os.listdir('/proc/self/fd')]
+    except OSError:
+        return set()
+    found = set()
+    for fd in listed:
+        try:
+            os.fstat(fd)    # (not the listing's own descriptor, closed now)
+            found.add(fd)
+        except OSError:
+            pass
+    return found
+
+
+def _worker_rocr(request):
+    """The ``ROCR_VISIBLE_DEVICES`` the worker of ``request`` will run with
+    (worker/pinning.py applies the ``--assign`` or ``--pin`` GPU)."""
+    from .pinning import apply_assignment_env, parse_assignment
+    env = {k: str(v) for k, v in request.get('env', {}).items()}
+    argv = list(request.get('argv', ()))
+    early = None
+    for flag in ('--pin', '--assign'):
+        if flag in argv and argv.index(flag) + 1 < len(argv):
+            try:
+                early = parse_assignment(argv[argv.index(flag) + 1])
+            except ValueError:
+                early = None
+    if early:
+        apply_assignment_env({'gpu': early.get('gpu')}, env)
+    return env.get('ROCR_VISIBLE_DEVICES')
 
 
 class _Embryos(object):
-    """The zygote's stock of pre-forked workers (``--embryos``)."""
+    """The zygote's stock of pre-forked workers (``--embryos``), of which
+    up to ``rocr`` initialise ROCr while they wait and are handed out
+    first."""
 
-    def __init__(self, target):
+    def __init__(self, target, rocr=0):
         self.target = max(0, int(target))
-        self.ready = []             # [(pid, socket)]
+        self.rocr = max(0, int(rocr))
+        self.ready = []             # [(pid, socket, rocr)]
 
     def pids(self):
-        return [pid for pid, _ in self.ready]
+        return [pid for pid, _, _ in self.ready]
 
     def make(self):
+        rocr = sum(1 for _, _, r in self.ready if r) < self.rocr
         ours, theirs = socket.socketpair(socket.AF_UNIX,
                                          socket.SOCK_SEQPACKET)
         try:
-            pid = _double_fork(lambda: (ours.close(), _embryo(theirs)))
+            pid = _double_fork(lambda: (ours.close(), _embryo(theirs, rocr)))
         finally:
             theirs.close()
         if pid is None:
             ours.close()
             return False
-        self.ready.append((pid, ours))
+        self.ready.append((pid, ours, rocr))
         return True
 
     def top_up(self, sock):
@@ -461,7 +553,9 @@ class _Embryos(object):
         """Give the request to a waiting embryo: its pid, or None (none
         left, or every one died)."""
         while self.ready:
-            pid, esock = self.ready.pop(0)
+            first = next((i for i, (_, _, r) in enumerate(self.ready) if r),
+                         0)
+            pid, esock, _ = self.ready.pop(first)
             try:
                 socket.send_fds(esock, [payload], list(fds))
                 return pid
@@ -472,8 +566,8 @@ class _Embryos(object):
         return None
 
 
-def _serve(sock, embryos=0):
-    stock = _Embryos(embryos)
+def _serve(sock, embryos=0, rocr_embryos=0):
+    stock = _Embryos(embryos, rocr_embryos)
     reported = []
     while True:
         stock.top_up(sock)
@@ -519,6 +613,7 @@ def main(argv=None):
     parser.add_argument('--zygote-fd', type=int, required=True)
     parser.add_argument('--backend', default='cpu')
     parser.add_argument('--embryos', type=int, default=0)
+    parser.add_argument('--rocr-embryos', type=int, default=0)
     args = parser.parse_args(argv)
     sock = socket.socket(fileno=args.zygote_fd)
     t0 = time.monotonic()
@@ -536,7 +631,7 @@ def main(argv=None):
     signal.signal(signal.SIGCHLD, signal.SIG_DFL)
     sock.send(json.dumps({'ready': True,
                           'preload_s': time.monotonic() - t0}).encode())
-    return _serve(sock, args.embryos)
+    return _serve(sock, args.embryos, args.rocr_embryos)
 
 
 if __name__ == '__main__':

@@ -584,3 +584,56 @@ def test_engine_cache_across_assignments(mod):
         for eng in list(wmain._ENGINES.values()):
             eng.close()
         wmain._ENGINES.clear()
+
+
+_EMBRYO_CHILD = r'''
+import json, os, sys
+from kiosk_autoscaler_amd.ops import native
+from kiosk_autoscaler_amd.worker import zygote
+mod = native.load()
+pre = zygote._HsaPreinit()
+pre.DELAY_S = 0.0
+pre.start()
+pre.thread.join()
+inited = pre.lib is not None
+if sys.argv[1] == 'shut':
+    pre.rocr = 'another pin'        # the worker's pin differs: shut down
+stamp = pre.settle({'argv': ['--pin', '{"gpu": 0}'],
+                    'env': dict(os.environ)})
+for fd in range(3, 1024):               # as zygote._child does
+    if fd not in pre.fds:
+        try:
+            os.close(fd)
+        except OSError:
+            pass
+stages = dict(mod.preinit_device(0))
+print(json.dumps({'inited': inited, 'stamp': stamp,
+                  'context_ms': (stages['preinit_context'] -
+                                 stages['preinit_enter']) / 1e6,
+                  'launched': 'preinit_first_launch' in stages}))
+sys.stdout.flush()
+os._exit(0)
+'''
+
+
+@pytest.mark.parametrize('mode', ['keep', 'shut'])
+def test_embryo_rocr_preinit_then_device(mode):
+    """An embryo's early ROCr init (worker/zygote.py ``_HsaPreinit``): ROCr
+    initialised before HIP, kept (same pin) or shut down and initialised
+    again by HIP (another pin), leaves a process whose device opens and
+    runs its first kernel.  Fresh processes: the init is once per process."""
+    import json
+    import os
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    out = subprocess.run([sys.executable, '-c', _EMBRYO_CHILD, mode],
+                         capture_output=True, text=True, timeout=90,
+                         env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    row = json.loads(out.stdout.strip().splitlines()[-1])
+    assert row['inited'] and row['launched']
+    assert (row['stamp'] is not None) == (mode == 'keep')

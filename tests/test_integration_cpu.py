@@ -366,6 +366,14 @@ def test_zygote_cold_spawn_reaped_like_a_child(stack):
             os.waitpid(pid, os.WNOHANG)
 
 
+def _exited(pid):
+    try:
+        with open('/proc/%d/stat' % pid) as stat:
+            return stat.read().rsplit(')', 1)[1].split()[0] in 'ZX'
+    except OSError:
+        return True
+
+
 def test_dead_embryos_are_skipped_and_replaced(stack):
     """An embryo killed while it waits costs nothing but its speed: the
     zygote finds it gone when it hands it a request, forks the worker the
@@ -375,6 +383,9 @@ def test_dead_embryos_are_skipped_and_replaced(stack):
     killed = wait_for(lambda: manager.zygote.embryo_pids(), timeout=10)
     for pid in killed:
         os.kill(pid, signal.SIGKILL)
+    # gone (or a zombie): its end of the hand-off socket is closed, so the
+    # zygote cannot queue the request to it
+    wait_for(lambda: all(_exited(pid) for pid in killed), timeout=10)
     enqueue(client, 1)
     assert tick(scaler, s) == 1
     wait_for(lambda: client.hget('predict:job0', 'status') == 'done',

@@ -268,3 +268,87 @@ def test_worker_config_reads_model_and_prefers_the_parsed_sizes():
     assert (cfg.dim, cfg.hidden, cfg.layers) == (1024, 2048, 2)
     cfg = rt.WorkerConfig({}, {'worker_id': 'w'})
     assert (cfg.dim, cfg.hidden, cfg.layers) == (4096, 16384, 4)
+
+
+class _FakeHsa(object):
+    def __init__(self):
+        self.calls = []
+
+    def hsa_init(self):
+        self.calls.append('init')
+        return 0
+
+    def hsa_shut_down(self):
+        self.calls.append('shut_down')
+        return 0
+
+
+def _settled(monkeypatch, zygote_rocr, argv, env, delay=0.0):
+    from kiosk_autoscaler_amd.worker import zygote
+    lib = _FakeHsa()
+    monkeypatch.setattr('ctypes.CDLL', lambda *a, **k: lib)
+    if zygote_rocr is None:
+        monkeypatch.delenv('ROCR_VISIBLE_DEVICES', raising=False)
+    else:
+        monkeypatch.setenv('ROCR_VISIBLE_DEVICES', zygote_rocr)
+    pre = zygote._HsaPreinit()
+    pre.DELAY_S = delay
+    pre.start()
+    if delay == 0.0:
+        pre.thread.join()
+    stamp = pre.settle({'argv': argv, 'env': env})
+    return stamp, lib.calls
+
+
+def test_embryo_keeps_rocr_when_the_pin_matches(monkeypatch):
+    """The 1-GPU box: ROCR_VISIBLE_DEVICES=0 and the worker pins GPU 0."""
+    stamp, calls = _settled(monkeypatch, '0',
+                            ['--pin', '{"gpu": 0}'],
+                            {'ROCR_VISIBLE_DEVICES': '0'})
+    assert calls == ['init'] and isinstance(stamp, int)
+
+
+def test_embryo_keeps_rocr_under_hip_level_pinning(monkeypatch):
+    # ROCR unset: the pin is HIP_VISIBLE_DEVICES, applied at hipInit
+    stamp, calls = _settled(monkeypatch, None,
+                            ['--pin', '{"gpu": 5}'], {})
+    assert calls == ['init'] and stamp is not None
+
+
+def test_embryo_shuts_rocr_down_when_the_pin_differs(monkeypatch):
+    """A node filtering at the ROCr level: the worker's GPU 3 re-filters
+    ROCR_VISIBLE_DEVICES, which the early init would have missed."""
+    stamp, calls = _settled(monkeypatch, '0,1,2,3',
+                            ['--pin', '{"gpu": 1}', '--assign',
+                             '{"gpu": 3}'],
+                            {'ROCR_VISIBLE_DEVICES': '0,1,2,3'})
+    assert calls == ['init', 'shut_down'] and stamp is None
+
+
+def test_embryo_request_before_the_delay_skips_the_init(monkeypatch):
+    stamp, calls = _settled(monkeypatch, None, [], {}, delay=30.0)
+    assert calls == [] and stamp is None
+
+
+def test_rocr_embryos_are_made_up_to_the_cap_and_handed_first(monkeypatch):
+    from kiosk_autoscaler_amd.worker import zygote
+    made = []
+
+    def fake_fork(body):
+        made.append(len(made) + 100)
+        return made[-1]
+    monkeypatch.setattr(zygote, '_double_fork', fake_fork)
+    stock = zygote._Embryos(4, rocr=2)
+    for _ in range(4):
+        assert stock.make()
+    assert [r for _, _, r in stock.ready] == [True, True, False, False]
+    sent = []
+    monkeypatch.setattr('socket.send_fds',
+                        lambda sock, bufs, fds: sent.append(sock))
+    assert stock.hand(b'{}', []) == 100
+    # the replacement for a handed-out ROCr embryo initialises ROCr too
+    stock.make()
+    assert [r for _, _, r in stock.ready] == [True, False, False, True]
+    assert stock.hand(b'{}', []) == 101
+    assert stock.hand(b'{}', []) == 104
+    assert stock.hand(b'{}', []) == 102

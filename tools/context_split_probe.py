@@ -25,6 +25,11 @@ hsa = ctypes.CDLL('libhsa-runtime64.so.1', mode=ctypes.RTLD_GLOBAL)
 t.append(time.perf_counter())
 rc_hsa = hsa.hsa_init()
 t.append(time.perf_counter())
+if len(sys.argv) > 2 and sys.argv[2] == 'pre':
+    # an embryo's shape: ROCr initialised well before HIP is
+    time.sleep(1.0)
+    slept = time.perf_counter() - t[-1]
+    t = [x + slept for x in t]
 rc_init = hip.hipInit(0)
 t.append(time.perf_counter())
 rc_set = hip.hipSetDevice(0)
@@ -50,6 +55,8 @@ def main():
     ap.add_argument('--n', type=int, default=12)
     ap.add_argument('--torch', action='store_true')
     ap.add_argument('--gap', type=float, default=0.5)
+    ap.add_argument('--pre', action='store_true',
+                    help='hsa_init, 1 s of sleep, then the HIP calls timed')
     ap.add_argument('--variants', default='',
                     help="comma-separated NAME=VALUE environment variants "
                          "(each its own --n processes; 'default' = as is), "
@@ -67,7 +74,8 @@ def main():
             env[name] = value
         t0 = time.perf_counter()
         out = subprocess.run([sys.executable, '-c', CHILD,
-                              '1' if args.torch else '0'],
+                              '1' if args.torch else '0',
+                              'pre' if args.pre else ''],
                              capture_output=True, text=True, timeout=120,
                              env=env)
         line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() \
