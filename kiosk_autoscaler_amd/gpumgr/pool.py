@@ -134,18 +134,28 @@ class PoolMixin(object):
     def zygote_rocr_embryos(self, template):
         """How many embryos initialise ROCr while they wait (HIP workers
         only; ``ZYGOTE_ROCR_EMBRYOS`` overrides, 0 = none).  Each halves a
-        woken standby's boot (~105 -> ~50 ms, profiles/r5_boot) and takes
+        woken standby's boot (~105 -> ~56 ms, profiles/r5_boot) and takes
         ROCr's init variance (110-300 ms spikes) off the scale-up path, but
-        opens the device: two, so a full node's workers plus these stay
-        well inside a per-device process budget."""
+        opens the devices while it waits.  By default only a manager of one
+        or two slots keeps them: a wider wake is as late as its slowest boot,
+        so a few fast embryos would not move it, and every one more process
+        on the devices counts against their process budget.  Not when
+        ``ROCR_VISIBLE_DEVICES`` lists several devices: each worker re-pins
+        to one of them, so an early init could never be kept."""
         if template is None or template.backend not in ('hip', 'auto') or \
                 not any(getattr(slot, 'kind', 'gpu') != 'cpu'
                         for slot in self.slots):
             return 0
         override = os.environ.get('ZYGOTE_ROCR_EMBRYOS', '')
         if override.strip():
-            return min(self.zygote_embryos(), max(0, int(override)))
-        return min(2, self.zygote_embryos())
+            wanted = max(0, int(override))
+        else:
+            wanted = 2 if len(self.slots) <= 2 else 0
+        rocr = [d for d in os.environ.get('ROCR_VISIBLE_DEVICES',
+                                          '').split(',') if d.strip()]
+        if len(rocr) > 1:
+            return 0
+        return min(self.zygote_embryos(), wanted)
 
     def _check_zygote(self):
         """False (and the zygote forgotten, restarted after a pause) once

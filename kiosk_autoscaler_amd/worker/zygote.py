@@ -404,7 +404,8 @@ class _HsaPreinit(object):
     (profiles/r5_boot/context_split.jsonl) -- and HIP's own set-up after it
     is 4-11 ms: a woken boot goes from ~105 ms to ~50 ms (profiles/r5_boot).
     It maps no HBM (idle-node HBM stays 1 MiB) but opens the KFD, so it is
-    one more process on the device: few of them (the pool's default is 2).
+    one more process on the device: few of them (gpumgr/pool.py
+    ``zygote_rocr_embryos``).
 
     ROCr reads ``ROCR_VISIBLE_DEVICES`` at ``hsa_init``, HIP applies
     ``HIP_VISIBLE_DEVICES`` at ``hipInit``: the embryo initialises under the

@@ -969,3 +969,33 @@ def test_awake_sized_pool_spawns_one_lead_before_the_tick():
     manager._next_tick = now + 2.0
     manager._wake_until = now + 1.0                # an arrival's wake hold
     assert manager._spawn_due(now)
+
+
+def test_rocr_embryos_only_for_small_hip_managers(monkeypatch):
+    """``zygote_rocr_embryos``: two on a HIP manager of one or two slots,
+    none on wider ones, none for CPU workers, none under a multi-device
+    ROCR_VISIBLE_DEVICES filter; ZYGOTE_ROCR_EMBRYOS overrides."""
+    from kiosk_autoscaler_amd.gpumgr import gpus, pool
+
+    class _Tpl(object):
+        def __init__(self, backend):
+            self.backend = backend
+
+    def rocr(n_slots, backend='hip', kind='gpu'):
+        holder = pool.PoolMixin()
+        holder.slots = [gpus.GpuSlot(index=i, visible_id=str(i), kind=kind)
+                        for i in range(n_slots)]
+        return holder.zygote_rocr_embryos(_Tpl(backend))
+
+    monkeypatch.delenv('ZYGOTE_ROCR_EMBRYOS', raising=False)
+    monkeypatch.delenv('ZYGOTE_EMBRYOS', raising=False)
+    monkeypatch.delenv('ROCR_VISIBLE_DEVICES', raising=False)
+    assert rocr(1) == 1 and rocr(2) == 2 and rocr(8) == 0
+    assert rocr(1, backend='cpu') == 0 and rocr(2, kind='cpu') == 0
+    monkeypatch.setenv('ROCR_VISIBLE_DEVICES', '0')
+    assert rocr(1) == 1
+    monkeypatch.setenv('ROCR_VISIBLE_DEVICES', '0,1')
+    assert rocr(2) == 0
+    monkeypatch.delenv('ROCR_VISIBLE_DEVICES')
+    monkeypatch.setenv('ZYGOTE_ROCR_EMBRYOS', '3')
+    assert rocr(8) == 3 and rocr(1) == 1
