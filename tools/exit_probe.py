@@ -13,7 +13,9 @@ Cases: ``ctx`` (HIP context + stream), ``engine`` (+ the production engine,
 (engine closed -- hipFree -- before the exit, timed separately),
 ``torch_engine_rccl`` (the PyTorch engine + RCCL), ``engine_rccl_abort`` /
 ``engine_rccl_destroy`` (the communicator aborted / destroyed after ``go``,
-before the exit; ``teardown_ms``).  One JSON line per case.
+before the exit; ``teardown_ms``), ``rccl`` (context + communicator, no
+engine).  One JSON line per case; ``EXIT_PROBE_TAG`` is copied into it
+(environment variants of one case, run one process each).
 """
 import json
 import os
@@ -24,7 +26,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 CASES = ('ctx', 'engine', 'engine_rccl', 'engine_free', 'torch_engine_rccl',
-         'engine_rccl_abort', 'engine_rccl_destroy')
+         'engine_rccl_abort', 'engine_rccl_destroy', 'rccl')
 
 
 def child(case, mod, wfd, rfd):
@@ -112,6 +114,7 @@ def main():
                 tail = os.read(up_r, 64).decode().strip()
                 info['teardown_ms'] = float(tail) if tail else None
             info.update({'case': case, 'rep': rep,
+                         'tag': os.environ.get('EXIT_PROBE_TAG', ''),
                          'exit_ms': (time.monotonic_ns() - t0) / 1e6,
                          'status': status})
             print(json.dumps(info), flush=True)
