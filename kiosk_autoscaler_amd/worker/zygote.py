@@ -442,8 +442,11 @@ class _HsaPreinit(object):
             # reference-counted: HIP's own hsa_init later returns at once
             lib = ctypes.CDLL('libhsa-runtime64.so.1', mode=ctypes.RTLD_GLOBAL)
             before = _open_fds()
-            if lib.hsa_init() == 0:
-                self.fds = _open_fds() - before
+            status = lib.hsa_init()
+            # kept even after a failed init: the thunk below ROCr caches its
+            # KFD descriptor, and HIP's own init would reuse it
+            self.fds = _open_fds() - before
+            if status == 0:
                 self.lib = lib
                 self.done_ns = time.monotonic_ns()
         except (OSError, AttributeError):
