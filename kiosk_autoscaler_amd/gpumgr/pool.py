@@ -114,7 +114,7 @@ class PoolMixin(object):
         argv = self._interpreter(tpl) + [
             '-m', 'kiosk_autoscaler_amd.worker.zygote', '--backend',
             tpl.backend]
-        rocr = self.zygote_rocr_embryos(tpl)
+        rocr = self._rocr_embryos = self.zygote_rocr_embryos(tpl)
         self.zygote = zygote.ZygoteClient(argv, self._environment(tpl),
                                           embryos=self.zygote_embryos(),
                                           rocr_embryos=rocr)
@@ -549,6 +549,11 @@ class PoolMixin(object):
     # the spawn request (0.5 ms from an embryo) and a boot's jitter, not a
     # poll period
     WAKE_MARGIN_S = 0.05
+    # with ROCr initialised in the embryos the boots are tight (0.049-0.062
+    # s, contexts 11-27 ms): over the 177 such woken boots of round 5, +30 ms
+    # is never late and holds 20 ms a wake less than +50 ms
+    # (tools/wake_lead_replay.py, profiles/r5_boot/README.md section 5)
+    WAKE_MARGIN_ROCR_S = 0.03
 
     def wake_lead(self):
         """Seconds before the next tick an arrival wakes a parked pool:
@@ -569,7 +574,9 @@ class PoolMixin(object):
             return cap
         boots = sorted(self._wake_boots)
         sized = boots[-2] if len(boots) >= 4 else boots[-1]
-        return min(cap, sized + self.WAKE_MARGIN_S)
+        margin = self.WAKE_MARGIN_ROCR_S if getattr(
+            self, '_rocr_embryos', 0) else self.WAKE_MARGIN_S
+        return min(cap, sized + margin)
 
     def _prebuild_spec(self, template):
         """What an arrival-woken standby builds its engine for: the shape

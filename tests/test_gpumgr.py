@@ -912,6 +912,11 @@ def test_sized_pool_retires_standbys_idle_beyond_demand():
     assert not manager._retire_excess(2, now=110.0)    # boot pool: resident
     manager.pool_parks = 1
     assert manager.wake_lead() == pytest.approx(0.12 + manager.WAKE_MARGIN_S)
+    # embryos with ROCr initialised boot tightly: the narrower margin
+    manager._rocr_embryos = 2
+    assert manager.wake_lead() == pytest.approx(
+        0.12 + manager.WAKE_MARGIN_ROCR_S)
+    manager._rocr_embryos = 0
     assert manager._retire_excess(2, now=110.0)
     # 1 (idle 1 s) then 0 (0.5 s); 2 (50 ms) and the booting 3 stay
     assert sorted(manager.standbys) == [2, 3]

@@ -75,11 +75,66 @@ def child(case, mod, wfd, rfd):
     os._exit(0)
 
 
+def _threads(pid):
+    try:
+        return len(os.listdir('/proc/%d/task' % pid))
+    except OSError:
+        return None
+
+
+def _memory(pid):
+    """The child's mappings before its exit: what ``exit_mm`` tears down."""
+    out = {}
+    try:
+        with open('/proc/%d/status' % pid) as f:
+            for line in f:
+                key, _, value = line.partition(':')
+                if key in ('VmRSS', 'RssAnon', 'RssFile', 'RssShmem',
+                           'VmPin', 'VmLck', 'VmSize'):
+                    out[key + '_mb'] = round(int(value.split()[0]) / 1024.0)
+        with open('/proc/%d/maps' % pid) as f:
+            out['maps'] = sum(1 for _ in f)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def _wait_sampling(pid):
+    """``waitpid`` by polling, sampling every 0.5 ms where the exiting
+    process's threads sleep in the kernel (``/proc/<pid>/task/*/wchan`` and
+    the thread state, readable by the owner): ``{state:wchan: samples}``."""
+    import collections
+    where = collections.Counter()
+    while True:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            return status, dict(where.most_common(12))
+        try:
+            tids = os.listdir('/proc/%d/task' % pid)
+        except OSError:
+            tids = []
+        for tid in tids:
+            base = '/proc/%d/task/%s/' % (pid, tid)
+            try:
+                with open(base + 'stat') as f:
+                    state = f.read().rsplit(')', 1)[1].split()[0]
+                with open(base + 'wchan') as f:
+                    chan = f.read().strip() or '-'
+            except OSError:
+                continue
+            where['%s:%s' % (state, chan)] += 1
+        time.sleep(0.0005)
+
+
 def main():
     cases = sys.argv[1].split(',') if len(sys.argv) > 1 else list(CASES)
     os.environ.setdefault('NCCL_MIN_NCHANNELS', '1')
     os.environ.setdefault('NCCL_MAX_NCHANNELS', '1')
     torch_first = any(c.startswith('torch') for c in cases)
+    if os.environ.get('EXIT_PROBE_SLIM') == '1':
+        # the one-ISA RCCL copy the manager writes (what workers load)
+        from kiosk_autoscaler_amd.parallel import rccl_lib
+        print(json.dumps({'rccl_lib': rccl_lib.configure()}), flush=True)
     from kiosk_autoscaler_amd.ops import native
     mod = native.load(torch_first=torch_first)
     mod.fence_dlopen()
@@ -107,12 +162,15 @@ def main():
                 line += chunk
             info = json.loads(line.decode() or '{}')
             time.sleep(0.2)
+            threads = _threads(pid)
+            info['mem'] = _memory(pid)
             t0 = time.monotonic_ns()
             os.write(go_w, b'g')
-            _, status = os.waitpid(pid, 0)
+            status, where = _wait_sampling(pid)
             if 'teardown' in info:
                 tail = os.read(up_r, 64).decode().strip()
                 info['teardown_ms'] = float(tail) if tail else None
+            info.update({'threads': threads, 'where': where})
             info.update({'case': case, 'rep': rep,
                          'tag': os.environ.get('EXIT_PROBE_TAG', ''),
                          'exit_ms': (time.monotonic_ns() - t0) / 1e6,
