@@ -26,7 +26,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 CASES = ('ctx', 'engine', 'engine_rccl', 'engine_free', 'torch_engine_rccl',
-         'engine_rccl_abort', 'engine_rccl_destroy', 'rccl')
+         'engine_rccl_abort', 'engine_rccl_destroy', 'rccl', 'streams_2',
+         'streams_hi_2')
 
 
 def child(case, mod, wfd, rfd):
@@ -46,6 +47,24 @@ def child(case, mod, wfd, rfd):
         engine = mod.Engine(0, 4096, 16384, 4, 2048, 1)
         engine.warmstart()
         keep.append(engine)
+    if case.startswith('streams'):
+        # ``streamsN`` / ``streams_hiN``: N more HIP streams, each used once
+        # (a hardware queue is made at a stream's first use), at normal or
+        # high priority -- does the exit scale with the queues?
+        import ctypes
+        hip = ctypes.CDLL('libamdhip64.so', mode=ctypes.RTLD_GLOBAL)
+        n = int(case.rstrip('_').split('_')[-1].lstrip('streamshi') or 1)
+        buf = ctypes.c_void_p()
+        hip.hipMalloc(ctypes.byref(buf), ctypes.c_size_t(1 << 20))
+        for _ in range(n):
+            stream = ctypes.c_void_p()
+            if '_hi' in case:
+                hip.hipStreamCreateWithPriority(ctypes.byref(stream), 0, -1)
+            else:
+                hip.hipStreamCreate(ctypes.byref(stream))
+            hip.hipMemsetAsync(buf, 0, ctypes.c_size_t(1 << 20), stream)
+            hip.hipStreamSynchronize(stream)
+            keep.append(stream)
     if 'rccl' in case:
         free, total = mod.mem_info()
         before = total - free
