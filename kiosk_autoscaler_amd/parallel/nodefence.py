@@ -83,6 +83,39 @@ def _survivor_rank(rank, excluded):
     return rank - sum(1 for r in excluded if int(r) < rank)
 
 
+# RCCL's per-process init started at process start (start_early_preload)
+_EARLY = {}
+
+
+def start_early_preload(native=None):
+    """Start RCCL's per-process one-time init -- ``ncclGetVersion`` +
+    ``ncclGetUniqueId``: the library's init and its bootstrap network,
+    ~120 ms -- on a thread of its own as the process starts, in parallel with
+    the HIP context and the engine build, instead of after them on the node
+    agent's thread, where it delayed every woken worker's first generation
+    (profiles/r5_fence_lag).  No kernel is loaded here: RCCL's code-object
+    load stays in the generation's init, after READY.  The agent's
+    :meth:`RcclNodeTransport.preload` joins this thread."""
+    if 'thread' in _EARLY:
+        return
+
+    def run():
+        t0 = time.perf_counter()
+        try:
+            mod = native
+            if mod is None:
+                from ..ops import native as native_ops
+                mod = native_ops.load()
+            mod.fence_preload()
+            _EARLY['ms'] = (time.perf_counter() - t0) * 1e3
+        except Exception as err:  # pylint: disable=broad-except
+            _EARLY['error'] = err
+
+    thread = threading.Thread(target=run, name='rccl-preload', daemon=True)
+    _EARLY['thread'] = thread
+    thread.start()
+
+
 # ---------------------------------------------------------------------------
 # transports: make_uid (rank 0) / connect (collective) / allreduce / abort
 # ---------------------------------------------------------------------------
@@ -117,6 +150,12 @@ class RcclNodeTransport(object):
     def preload(self):
         """RCCL's per-process one-time costs (library load + init), paid
         when the agent starts rather than inside a generation: ms."""
+        early = _EARLY.get('thread')
+        if early is not None:
+            early.join()
+            if 'error' in _EARLY:
+                raise _EARLY['error']
+            return _EARLY.get('ms', 0.0)
         preload = getattr(self.native, 'fence_preload', None)
         return preload() if preload is not None else 0.0
 

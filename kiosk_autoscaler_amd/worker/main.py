@@ -400,6 +400,13 @@ def main(argv=None):
     preload_ns = _preload(backend)
     if args.assign and backend == 'hip':
         _open_device_async()
+    if pin and not args.assign and backend == 'hip' and \
+            pin.get('preinit') == 'device' and pin.get('node_fence') and \
+            os.environ.get('FENCE', 'auto') in ('auto', 'rccl'):
+        # RCCL's process init in parallel with the boot below; the node
+        # agent, started after the engine build, joins it
+        from ..parallel.nodefence import start_early_preload
+        start_early_preload()
 
     import logging
     logging.basicConfig(

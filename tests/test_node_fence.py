@@ -1544,3 +1544,38 @@ def test_slow_rccl_inits_hold_up_no_scale_up(resp_server, tmp_path, init_ms):
     assert ready[0]['init_ms'] >= init_ms * 0.9
     done = [e for e in events.records if e['ev'] == 'fence_done']
     assert done and all(e['transport'] == 'rccl' for e in done)
+
+
+def test_early_rccl_preload_is_joined_by_the_agent_preload(monkeypatch):
+    """``start_early_preload`` runs RCCL's process init on its own thread at
+    process start; the transport's ``preload`` joins it (once) instead of
+    running it again, and re-raises its failure."""
+    import threading
+    from kiosk_autoscaler_amd.parallel import nodefence
+    calls = []
+    gate = threading.Event()
+
+    class _Native(object):
+        def fence_preload(self):
+            gate.wait(5)
+            calls.append('preload')
+            return 1.0
+
+    monkeypatch.setattr(nodefence, '_EARLY', {})
+    nodefence.start_early_preload(_Native())
+    nodefence.start_early_preload(_Native())         # once per process
+    transport = nodefence.RcclNodeTransport.__new__(
+        nodefence.RcclNodeTransport)
+    transport.native = _Native()
+    gate.set()
+    assert transport.preload() >= 0.0
+    assert calls == ['preload']
+
+    class _Broken(object):
+        def fence_preload(self):
+            raise RuntimeError('no RCCL')
+
+    monkeypatch.setattr(nodefence, '_EARLY', {})
+    nodefence.start_early_preload(_Broken())
+    with pytest.raises(RuntimeError):
+        transport.preload()
