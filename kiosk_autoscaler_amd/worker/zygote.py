@@ -423,6 +423,7 @@ class _HsaPreinit(object):
         self.lib = None
         self.rocr = None
         self.done_ns = None
+        self.status = None          # hsa_init's, once it ran
         self.fds = set()
 
     def start(self):
@@ -442,7 +443,7 @@ class _HsaPreinit(object):
             # reference-counted: HIP's own hsa_init later returns at once
             lib = ctypes.CDLL('libhsa-runtime64.so.1', mode=ctypes.RTLD_GLOBAL)
             before = _open_fds()
-            status = lib.hsa_init()
+            status = self.status = lib.hsa_init()
             # kept even after a failed init: the thunk below ROCr caches its
             # KFD descriptor, and HIP's own init would reuse it
             self.fds = _open_fds() - before
@@ -460,8 +461,10 @@ class _HsaPreinit(object):
         self.cancel.set()
         self.thread.join()
         if self.lib is None:
-            self._say('no ROCr init before the request')
-            return None
+            if self.status is not None:
+                self._say('hsa_init failed (%d): HIP initialises ROCr'
+                          % self.status)
+            return None      # (or the request came before the init)
         rocr = _worker_rocr(request)
         if rocr == self.rocr:
             return self.done_ns
