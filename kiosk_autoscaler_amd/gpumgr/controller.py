@@ -383,7 +383,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
     def _loop(self):
         while not self._stop.is_set():
             timeout = 0.05
-            for due in (self._wake_at, self._spawn_at,
+            for due in (self._wake_at, self._spawn_at, self._park_at,
                         self._arrival_check_due()):
                 if due is not None:
                     # a deferred arrival wake / standby spawn / queue read:

@@ -52,6 +52,7 @@ class PoolMixin(object):
         self._wake_boots = collections.deque(maxlen=16)
         self._wake_at = None      # a deferred arrival wake
         self._spawn_at = None     # a deferred standby spawn (awake pool)
+        self._park_at = None      # when an idle pool is due to park
         self._next_arrival_check = 0.0
         self._arrival_watch = False   # no demand: queues are polled
         # queue -> length at the last check; reset to empty when demand
@@ -454,6 +455,7 @@ class PoolMixin(object):
         scale-up itself, which is then a cold spawn with the pool refilling
         behind it.  True if standbys were retired."""
         now = time.monotonic()
+        self._park_at = None
         demand = any(r.declared > 0 or any(w.state != EXITED
                                            for w in r.workers.values())
                      for r in self.resources.values())
@@ -506,9 +508,14 @@ class PoolMixin(object):
                 logger.info('Keys arrived: refilling the warm pool ahead of '
                             'the scale-up tick.')
             return False
-        if (self.pool_idle_release_s <= 0 or self.pool_parked or
-                now - self._last_demand < self.pool_idle_release_s or
-                now < self._wake_until):
+        if self.pool_idle_release_s <= 0 or self.pool_parked:
+            return False
+        if now - self._last_demand < self.pool_idle_release_s or \
+                now < self._wake_until:
+            # the loop wakes for it (0.01 s after demand ends, by default)
+            # instead of at its next queue read
+            self._park_at = max(self._last_demand + self.pool_idle_release_s,
+                                self._wake_until)
             return False
         self.pool_parked = True
         self.pool_parks += 1

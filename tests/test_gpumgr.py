@@ -1004,3 +1004,27 @@ def test_rocr_embryos_only_for_small_hip_managers(monkeypatch):
     monkeypatch.delenv('ROCR_VISIBLE_DEVICES')
     monkeypatch.setenv('ZYGOTE_ROCR_EMBRYOS', '3')
     assert rocr(8) == 3 and rocr(1) == 1
+
+
+def test_idle_pool_sets_its_park_instant_for_the_loop():
+    """An idle pool tells the manager's loop when it is due to park
+    (``_park_at``), so it parks ``POOL_IDLE_RELEASE_S`` after demand ends
+    rather than at the next queue read; with demand, or parked, nothing is
+    due (a stale instant would spin the loop)."""
+    import time
+    import types
+    manager = gpumgr.GpuManager(
+        [gpus.GpuSlot(index=0, visible_id='', kind='cpu')],
+        pool_idle_release_s=0.5)
+    manager._last_demand = time.monotonic()
+    assert manager._park_pool() is False
+    assert manager._park_at == pytest.approx(manager._last_demand + 0.5)
+    res = types.SimpleNamespace(declared=1, workers={})
+    manager.resources = {'r': res}
+    assert manager._park_pool() is False and manager._park_at is None
+    res.declared = 0
+    manager._last_demand = time.monotonic() - 1.0
+    assert manager._park_pool() is True and manager.pool_parked
+    assert manager._park_at is None
+    manager._park_pool()
+    assert manager._park_at is None
