@@ -96,7 +96,11 @@ def start_early_preload(native=None):
     (profiles/r5_fence_lag).  No kernel is loaded here: RCCL's code-object
     load stays in the generation's init, after READY.  The agent's
     :meth:`RcclNodeTransport.preload` joins this thread."""
-    if 'thread' in _EARLY:
+    if 'thread' in _EARLY or not _rccl_mapped():
+        # (not mapped: a cold-spawned worker, whose first RCCL call would
+        # also register RCCL's fat binary -- seconds under the runtime lock
+        # every kernel launch waits on, profiles/r4_collision -- in the
+        # middle of its engine build; its agent loads RCCL after the build)
         return
 
     def run():
@@ -114,6 +118,17 @@ def start_early_preload(native=None):
     thread = threading.Thread(target=run, name='rccl-preload', daemon=True)
     _EARLY['thread'] = thread
     thread.start()
+
+
+def _rccl_mapped():
+    """RCCL is already mapped -- and its fat binary registered -- in this
+    process (the zygote dlopens it before forking)."""
+    try:
+        with open('/proc/self/maps') as maps:
+            return any('librccl' in line or 'fake_hip_rccl' in line
+                       for line in maps)
+    except OSError:
+        return False
 
 
 # ---------------------------------------------------------------------------

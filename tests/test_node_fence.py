@@ -1561,7 +1561,11 @@ def test_early_rccl_preload_is_joined_by_the_agent_preload(monkeypatch):
             calls.append('preload')
             return 1.0
 
+    monkeypatch.setattr(nodefence, '_rccl_mapped', lambda: False)
     monkeypatch.setattr(nodefence, '_EARLY', {})
+    nodefence.start_early_preload(_Native())       # RCCL not loaded yet
+    assert nodefence._EARLY == {}
+    monkeypatch.setattr(nodefence, '_rccl_mapped', lambda: True)
     nodefence.start_early_preload(_Native())
     nodefence.start_early_preload(_Native())         # once per process
     transport = nodefence.RcclNodeTransport.__new__(
