@@ -2,6 +2,8 @@
 //
 //   kredis-server [--bind 127.0.0.1] [--port 6379]
 //                 [--sentinel NAME HOST PORT] [--replica HOST:PORT]...
+//                 [--redis-version X.Y]   (5.0: no LMOVE/BLMOVE, integer
+//                                          blocking timeouts, no SCAN TYPE)
 //
 // Semantics follow Redis 7 for every implemented command (reply types,
 // WRONGTYPE, negative list indices, LMOVE/BLMOVE direction arguments, SET
@@ -142,8 +144,13 @@ const char* kWrongType =
 
 class Server {
  public:
-  Server(int dbs, SentinelConfig sentinel)
-      : dbs_(dbs), sentinel_(std::move(sentinel)), started_(now_ms()) {}
+  Server(int dbs, SentinelConfig sentinel, std::string version = "7.2.0")
+      : dbs_(dbs), sentinel_(std::move(sentinel)), started_(now_ms()),
+        version_text_(std::move(version)) {
+    int major = 0, minor = 0;
+    sscanf(version_text_.c_str(), "%d.%d", &major, &minor);
+    version_ = major * 100 + minor;
+  }
 
   int run(const std::string& bind_addr, int port);
 
@@ -175,6 +182,22 @@ class Server {
   std::vector<Db> dbs_;
   SentinelConfig sentinel_;
   int64_t started_;
+  // the Redis version this server answers as (--redis-version): below 6.2
+  // LMOVE/BLMOVE are unknown, below 6.0 blocking timeouts are integers and
+  // SCAN has no TYPE -- a server of the reference's redis~=3.5.3 era
+  std::string version_text_;
+  int version_ = 702;           // major * 100 + minor
+  bool parse_timeout(const std::string& s, double* out) const {
+    if (version_ >= 600) return parse_double(s, out);
+    long long v;
+    if (!parse_ll(s, &v)) return false;
+    *out = static_cast<double>(v);
+    return true;
+  }
+  const char* timeout_error() const {
+    return version_ >= 600 ? "ERR timeout is not a float or out of range"
+                           : "ERR timeout is not an integer or out of range";
+  }
   long long commands_ = 0;
   std::unordered_map<std::string, Handler> table_;
   std::map<int, std::unique_ptr<Client>> clients_;
@@ -293,7 +316,7 @@ void Server::register_commands() {
     r.bulk(std::to_string(ts.tv_nsec / 1000));
   };
   t["INFO"] = [this](Client&, const Args&, Reply& r) {
-    std::string s = "# Server\r\nredis_version:7.2.0-kredis\r\n";
+    std::string s = "# Server\r\nredis_version:" + version_text_ + "-kredis\r\n";
     s += std::string("redis_mode:") +
          (sentinel_.enabled() ? "sentinel" : "standalone") + "\r\n";
     s += "uptime_in_seconds:" + std::to_string((now_ms() - started_) / 1000) +
@@ -410,7 +433,7 @@ void Server::register_commands() {
       std::string opt = upper(a[i]);
       if (opt == "MATCH") match = a[i + 1];
       else if (opt == "COUNT") { if (!parse_ll(a[i + 1], &count) || count < 1) { r.error("ERR syntax error"); return; } }
-      else if (opt == "TYPE") type = a[i + 1];
+      else if (opt == "TYPE" && version_ >= 600) type = a[i + 1];
       else { r.error("ERR syntax error"); return; }
     }
     Db& d = db(c);
@@ -646,6 +669,10 @@ void Server::register_commands() {
   auto moves = [this](Client& c, const Args& a, Reply& r) { try_pop_move(c, a, r, true); };
   for (const char* name : {"LMOVE", "RPOPLPUSH", "BLMOVE", "BRPOPLPUSH", "BLPOP", "BRPOP"})
     t[name] = moves;
+  if (version_ < 602) {          // LMOVE / BLMOVE arrived in Redis 6.2
+    t.erase("LMOVE");
+    t.erase("BLMOVE");
+  }
 
   // ---- hashes
   t["HSET"] = [this](Client& c, const Args& a, Reply& r) {
@@ -861,23 +888,23 @@ bool Server::try_pop_move(Client& c, const Args& a, Reply& r, bool blocking_ok) 
       }
       from_left = wf == "LEFT";
       to_left = wt == "LEFT";
-      if (cmd == "BLMOVE" && !parse_double(a.at(5), &timeout)) {
-        r.error("ERR timeout is not a float or out of range");
+      if (cmd == "BLMOVE" && !parse_timeout(a.at(5), &timeout)) {
+        r.error(timeout_error());
         return true;
       }
     } else {
       from_left = false;
       to_left = true;
-      if (cmd == "BRPOPLPUSH" && !parse_double(a.at(3), &timeout)) {
-        r.error("ERR timeout is not a float or out of range");
+      if (cmd == "BRPOPLPUSH" && !parse_timeout(a.at(3), &timeout)) {
+        r.error(timeout_error());
         return true;
       }
     }
   } else {
     if (a.size() < 3) { r.error("ERR wrong number of arguments"); return true; }
     for (size_t i = 1; i + 1 < a.size(); ++i) srcs.push_back(a[i]);
-    if (!parse_double(a.back(), &timeout)) {
-      r.error("ERR timeout is not a float or out of range");
+    if (!parse_timeout(a.back(), &timeout)) {
+      r.error(timeout_error());
       return true;
     }
     from_left = cmd == "BLPOP";
@@ -1232,10 +1259,12 @@ int main(int argc, char** argv) {
   std::string bind_addr = "127.0.0.1";
   int port = 6379;
   kredis::SentinelConfig sentinel;
+  std::string version = "7.2.0";
   for (int i = 1; i < argc; ++i) {
     std::string arg = argv[i];
     if (arg == "--port" && i + 1 < argc) port = atoi(argv[++i]);
     else if (arg == "--bind" && i + 1 < argc) bind_addr = argv[++i];
+    else if (arg == "--redis-version" && i + 1 < argc) version = argv[++i];
     else if (arg == "--sentinel" && i + 3 < argc) {
       sentinel.name = argv[++i];
       sentinel.host = argv[++i];
@@ -1247,13 +1276,13 @@ int main(int argc, char** argv) {
       sentinel.replicas.emplace_back(hp.substr(0, colon), atoi(hp.c_str() + colon + 1));
     } else if (arg == "--help" || arg == "-h") {
       printf("kredis-server [--bind ADDR] [--port N] [--sentinel NAME HOST PORT] "
-             "[--replica HOST:PORT]...\n");
+             "[--replica HOST:PORT]... [--redis-version X.Y]\n");
       return 0;
     } else {
       fprintf(stderr, "unknown argument %s\n", arg.c_str());
       return 2;
     }
   }
-  kredis::Server server(16, sentinel);
+  kredis::Server server(16, sentinel, version);
   return server.run(bind_addr, port);
 }

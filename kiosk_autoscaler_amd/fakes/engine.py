@@ -58,6 +58,17 @@ def _float(value):
         raise _Reply(ReplyError('ERR timeout is not a float or out of range'))
 
 
+def parse_version(text):
+    """``'5.0.14'`` -> ``(5, 0, 14)``."""
+    parts = []
+    for piece in str(text).split('-')[0].split('.'):
+        try:
+            parts.append(int(piece))
+        except ValueError:
+            break
+    return tuple(parts) or (7, 2, 0)
+
+
 class _Reply(Exception):
     """Short-circuit a handler with a ready reply (usually an error)."""
 
@@ -103,9 +114,20 @@ class RedisEngine(object):
             is what a plain Redis answers (reference ``redis.py:153-155``
             path).
         databases: number of logical dbs.
+        version: the Redis version to answer as (``INFO``'s
+            ``redis_version``).  Below 6.2 ``LMOVE``/``BLMOVE`` are unknown
+            commands; below 6.0 a blocking timeout must be an integer and
+            ``SCAN`` has no ``TYPE`` option -- what a server of the
+            reference's ``redis~=3.5.3`` era (``requirements.txt:3``) does.
     """
 
-    def __init__(self, sentinel_masters=None, databases=16):
+    # first version with the command (absent from this engine's older modes)
+    SINCE = {'LMOVE': (6, 2), 'BLMOVE': (6, 2)}
+
+    def __init__(self, sentinel_masters=None, databases=16,
+                 version='7.2.0'):
+        self.version_text = str(version)
+        self.version = parse_version(version)
         self._dbs = [dict() for _ in range(databases)]
         self._expires = [dict() for _ in range(databases)]
         self._cond = threading.Condition(threading.RLock())
@@ -223,8 +245,20 @@ class RedisEngine(object):
         table = {}
         for attr in dir(self):
             if attr.startswith('cmd_'):
-                table[attr[4:].upper().replace('_', '-')] = getattr(self, attr)
+                name = attr[4:].upper().replace('_', '-')
+                if self.version >= self.SINCE.get(name, (0,)):
+                    table[name] = getattr(self, attr)
         return table
+
+    def _timeout(self, value):
+        """A blocking command's timeout: fractional only since 6.0."""
+        if self.version < (6, 0):
+            try:
+                return float(int(value))
+            except (TypeError, ValueError):
+                raise _Reply(ReplyError(
+                    'ERR timeout is not an integer or out of range'))
+        return _float(value)
 
     # -- connection / server -------------------------------------------------
     def cmd_ping(self, session, args):
@@ -270,11 +304,12 @@ class RedisEngine(object):
             'db%d:keys=%d,expires=%d\r\n' % (i, len(db), len(self._expires[i]))
             for i, db in enumerate(self._dbs) if db)
         role = 'sentinel' if self.sentinel_masters else 'master'
-        text = ('# Server\r\nredis_version:7.2.0-kiosk-amd\r\n'
+        text = ('# Server\r\nredis_version:%s-kiosk-amd\r\n'
                 'redis_mode:%s\r\nuptime_in_seconds:%d\r\n'
                 '# Replication\r\nrole:%s\r\n'
                 '# Stats\r\ntotal_commands_processed:%d\r\n'
                 '# Keyspace\r\n%s' % (
+                    self.version_text,
                     'sentinel' if self.sentinel_masters else 'standalone',
                     int(time.time() - self.started), role,
                     self.commands_processed, keyspace))
@@ -407,7 +442,7 @@ class RedisEngine(object):
                 match = args[i + 1]
             elif opt == b'COUNT':
                 count = max(1, _int(args[i + 1]))
-            elif opt == b'TYPE':
+            elif opt == b'TYPE' and self.version >= (6, 0):
                 kind = args[i + 1].lower()
             else:
                 return ReplyError('ERR syntax error')
@@ -640,17 +675,17 @@ class RedisEngine(object):
     def cmd_blmove(self, session, args):
         src, dst = args[0], args[1]
         frm, to = args[2].upper(), args[3].upper()
-        timeout = _float(args[4])
+        timeout = self._timeout(args[4])
         return self._block(timeout,
                            lambda: self._move(session, src, dst, frm, to))
 
     def cmd_brpoplpush(self, session, args):
-        timeout = _float(args[2])
+        timeout = self._timeout(args[2])
         return self._block(timeout, lambda: self._move(
             session, args[0], args[1], b'RIGHT', b'LEFT'))
 
     def _bpop(self, session, args, left):
-        keys, timeout = args[:-1], _float(args[-1])
+        keys, timeout = args[:-1], self._timeout(args[-1])
 
         def attempt():
             for key in keys:

@@ -92,8 +92,12 @@ def main(argv=None):
     parser = argparse.ArgumentParser(description=__doc__)
     parser.add_argument('--host', default='127.0.0.1')
     parser.add_argument('--port', type=int, default=6379)
+    parser.add_argument('--redis-version', default='7.2.0',
+                        help='answer as this Redis version (5.0: no '
+                             'LMOVE/BLMOVE, integer blocking timeouts)')
     args = parser.parse_args(argv)
-    server = RespServer(host=args.host, port=args.port)
+    server = RespServer(engine=RedisEngine(version=args.redis_version),
+                        host=args.host, port=args.port)
     print('listening on %s:%d' % (server.host, server.port), flush=True)
     try:
         server._server.serve_forever(poll_interval=0.1)

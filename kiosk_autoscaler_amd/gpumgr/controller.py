@@ -675,6 +675,16 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
             elif kind == 'error':
                 logger.error('Worker %s reported: %s', worker.id,
                              message.get('message'))
+            elif kind == 'pull_error':
+                # the worker stays up and retries; surfaced once per burst
+                worker.pull_errors += 1
+                if worker.pull_errors in (1, 10, 100):
+                    logger.error('Worker %s cannot pull keys (%d errors): %s',
+                                 worker.id, worker.pull_errors,
+                                 message.get('message'))
+                    self.events.emit('worker_pull_error', worker=worker.id,
+                                     errors=worker.pull_errors,
+                                     message=message.get('message'))
     # a quarantined worker (its node agent stopped answering) that holds no
     # key and has not exited this long after the drain is hung as a whole:
     # killed (a busy one is the WORKER_TIMEOUT watchdog's)

@@ -145,7 +145,7 @@ class Worker(object):
     __slots__ = ('id', 'resource', 'slot', 'proc', 'state', 'busy',
                  't_assigned', 't_ready', 't_exit', 'exit_code', 'from_pool',
                  'stages', 'last_beat', 'kill_reason', 'fenced_out',
-                 'quarantined_at')
+                 'quarantined_at', 'pull_errors')
 
     def __init__(self, wid, resource, slot, proc, from_pool):
         self.id = wid
@@ -164,6 +164,7 @@ class Worker(object):
         self.kill_reason = None
         self.fenced_out = False     # an agreed membership excluded it
         self.quarantined_at = None  # its node agent stopped answering
+        self.pull_errors = 0        # queue pulls the server rejected
 
     def summary(self):
         return {'id': self.id, 'gpu': self.slot.index, 'pid': self.proc.pid,
@@ -171,4 +172,5 @@ class Worker(object):
                 'from_pool': self.from_pool, 't_assigned': self.t_assigned,
                 't_ready': self.t_ready, 'stages': dict(self.stages),
                 'exit_code': self.exit_code, 'killed': self.kill_reason,
-                'fenced_out': self.fenced_out}
+                'fenced_out': self.fenced_out,
+                'pull_errors': self.pull_errors}

@@ -95,8 +95,30 @@ class WorkerConfig(object):
         self.recycle = bool(assignment.get('recycle', False))
 
 
+def _unknown_command(err):
+    return 'unknown command' in str(err).lower()
+
+
+def _bad_timeout(err):
+    # Redis < 6.0: "ERR timeout is not an integer or out of range"
+    return 'timeout is not' in str(err).lower()
+
+
 class QueueConsumer(object):
-    """Moves items into per-worker processing keys and back out."""
+    """Moves items into per-worker processing keys and back out.
+
+    The move is ``LMOVE q p RIGHT LEFT`` (Redis >= 6.2).  Against an older
+    server -- the reference pins ``redis~=3.5.3``
+    (``/root/reference/requirements.txt:3``), a client of the Redis 5/6.0
+    era -- the first ``ERR unknown command`` switches this consumer, once,
+    to the exactly equivalent ``RPOPLPUSH``; the blocking wait becomes
+    ``BRPOPLPUSH``, and where the server also rejects a fractional timeout
+    (Redis < 6.0) a non-blocking ``RPOPLPUSH`` poll every ``poll_block``
+    seconds.  The processing-key convention the tally counts
+    (``/root/reference/autoscaler/autoscaler.py:67-73``) is unchanged."""
+
+    # blocking-wait modes, newest first
+    BLOCK_MODES = ('blmove', 'brpoplpush', 'poll')
 
     def __init__(self, redis, worker_id, queues, poll_block=0.1):
         self.redis = redis
@@ -105,9 +127,52 @@ class QueueConsumer(object):
         self.poll_block = poll_block
         self._rotate = 0
         self._sweep = 0
+        # capability cache of this consumer's connection
+        self.move_mode = 'lmove'
+        self.block_mode = 'blmove'
 
     def processing_key(self, queue, slot=0):
         return keys.processing_key(queue, self.worker_id, slot)
+
+    def _legacy(self, what, err):
+        logger.warning('redis server rejected %s (%s): worker %s falls back '
+                       'to RPOPLPUSH', what, err, self.worker_id)
+        self.move_mode = 'rpoplpush'
+        if self.block_mode == 'blmove':
+            self.block_mode = 'brpoplpush'
+
+    def _move(self, queue, pkey):
+        if self.move_mode == 'lmove':
+            try:
+                return self.redis.lmove(queue, pkey, 'RIGHT', 'LEFT')
+            except redis_errors.ResponseError as err:
+                if not _unknown_command(err):
+                    raise
+                self._legacy('LMOVE', err)
+        return self.redis.rpoplpush(queue, pkey)
+
+    def _block_move(self, queue, pkey, timeout):
+        if self.block_mode == 'blmove':
+            try:
+                return self.redis.blmove(queue, pkey, timeout, 'RIGHT',
+                                         'LEFT')
+            except redis_errors.ResponseError as err:
+                if not _unknown_command(err):
+                    raise
+                self._legacy('BLMOVE', err)
+        if self.block_mode == 'brpoplpush':
+            try:
+                return self.redis.brpoplpush(queue, pkey, timeout)
+            except redis_errors.ResponseError as err:
+                if not _bad_timeout(err):
+                    raise
+                # an integer timeout would hold a drain for >= 1 s
+                logger.warning('redis server rejected a %.3f s blocking '
+                               'timeout (%s): worker %s polls instead',
+                               timeout, err, self.worker_id)
+                self.block_mode = 'poll'
+        time.sleep(timeout)
+        return self._move(queue, pkey)
 
     def pull(self, limit=1, block=True):
         """Return up to ``limit`` ``(queue, item, processing_key)`` tuples.
@@ -124,7 +189,7 @@ class QueueConsumer(object):
         for queue in self.queues[start:] + self.queues[:start]:
             while len(taken) < limit:
                 pkey = self.processing_key(queue, len(taken))
-                item = self.redis.lmove(queue, pkey, 'RIGHT', 'LEFT')
+                item = self._move(queue, pkey)
                 if item is None:
                     break
                 taken.append((queue, item, pkey))
@@ -132,9 +197,8 @@ class QueueConsumer(object):
             return taken
         queue = self.queues[self._rotate % len(self.queues)]
         self._rotate += 1
-        timeout = self.poll_block
         pkey = self.processing_key(queue, 0)
-        item = self.redis.blmove(queue, pkey, timeout, 'RIGHT', 'LEFT')
+        item = self._block_move(queue, pkey, self.poll_block)
         if item is not None:
             taken.append((queue, item, pkey))
         return taken
@@ -313,6 +377,13 @@ class WorkerRuntime(object):
                     items = consumer.pull(limit=cfg.batch)
                 except redis_errors.ConnectionError as err:
                     logger.warning('redis unavailable (%s); retrying', err)
+                    time.sleep(0.5)
+                    continue
+                except redis_errors.ResponseError as err:
+                    # a protocol error the consumer cannot adapt to must not
+                    # crash-loop the worker: report it and keep trying
+                    logger.error('queue pull failed (%s); retrying', err)
+                    self.channel.emit('pull_error', message=str(err)[:200])
                     time.sleep(0.5)
                     continue
                 if not items:

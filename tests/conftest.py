@@ -35,6 +35,16 @@ def resp_server():
     server.stop()
 
 
+@pytest.fixture
+def legacy_resp_server():
+    """A RESP server answering as Redis 5.0 (the reference's
+    ``redis~=3.5.3`` era): no LMOVE/BLMOVE, integer blocking timeouts."""
+    from kiosk_autoscaler_amd.fakes import RedisEngine, RespServer
+    server = RespServer(engine=RedisEngine(version='5.0.14')).start()
+    yield server
+    server.stop()
+
+
 def kredis_binary():
     """``build/kredis-server``; ``KIOSK_KREDIS_BIN`` selects another build
     (CI runs the RESP suites against ``build/kredis-server-asan``)."""
@@ -43,20 +53,19 @@ def kredis_binary():
     return path if os.path.exists(path) else None
 
 
-@pytest.fixture
-def kredis_server():
-    """The native C++ RESP server (skips if it has not been built)."""
+def _spawn_kredis(extra_args=()):
+    """Start ``kredis-server`` on a free port; returns a handle or None."""
     import socket
     import subprocess
     import time
     binary = kredis_binary()
     if binary is None:
-        pytest.skip('kredis-server not built (python tools/build_native.py)')
+        return None
     sock = socket.socket()
     sock.bind(('127.0.0.1', 0))
     port = sock.getsockname()[1]
     sock.close()
-    proc = subprocess.Popen([binary, '--port', str(port)],
+    proc = subprocess.Popen([binary, '--port', str(port)] + list(extra_args),
                             stdout=subprocess.DEVNULL,
                             stderr=subprocess.DEVNULL)
     deadline = time.time() + 10
@@ -73,9 +82,33 @@ def kredis_server():
     handle = Handle()
     handle.port = port
     handle.proc = proc
-    yield handle
-    proc.terminate()
+    return handle
+
+
+def _stop_kredis(handle):
+    import subprocess
+    handle.proc.terminate()
     try:
-        proc.wait(timeout=5)
+        handle.proc.wait(timeout=5)
     except subprocess.TimeoutExpired:
-        proc.kill()
+        handle.proc.kill()
+
+
+@pytest.fixture
+def kredis_server():
+    """The native C++ RESP server (skips if it has not been built)."""
+    handle = _spawn_kredis()
+    if handle is None:
+        pytest.skip('kredis-server not built (python tools/build_native.py)')
+    yield handle
+    _stop_kredis(handle)
+
+
+@pytest.fixture
+def kredis_legacy_server():
+    """``kredis-server --redis-version 5.0`` (skips if not built)."""
+    handle = _spawn_kredis(['--redis-version', '5.0.14'])
+    if handle is None:
+        pytest.skip('kredis-server not built (python tools/build_native.py)')
+    yield handle
+    _stop_kredis(handle)

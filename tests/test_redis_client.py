@@ -210,3 +210,25 @@ def test_native_scan_survives_deletes_between_pages(kredis_server):
             break
     assert set(names) - deleted <= seen
     assert len(seen) == len(names)          # never duplicated either
+
+
+def test_native_server_redis5_mode(kredis_legacy_server):
+    """``kredis-server --redis-version 5.0``: LMOVE/BLMOVE are unknown,
+    blocking timeouts must be integers, SCAN ignores TYPE -- and the
+    worker's consumer still pulls in FIFO order through RPOPLPUSH."""
+    from kiosk_autoscaler_amd.worker.runtime import QueueConsumer
+    client = StrictRedis(host=kredis_legacy_server.host,
+                         port=kredis_legacy_server.port,
+                         decode_responses=True)
+    assert client.info()['redis_version'].startswith('5.0')
+    with pytest.raises(exceptions.ResponseError, match='unknown command'):
+        client.lmove('q', 'p', 'RIGHT', 'LEFT')
+    with pytest.raises(exceptions.ResponseError, match='not an integer'):
+        client.brpoplpush('q', 'p', 0.005)
+    assert client.brpoplpush('q', 'p', 1) is None       # integer: fine
+    consumer = QueueConsumer(client, 'w-g0-x-9', ['q'], poll_block=0.005)
+    assert consumer.pull(limit=1) == []
+    assert (consumer.move_mode, consumer.block_mode) == ('rpoplpush', 'poll')
+    client.lpush('q', 'a', 'b')
+    taken = [consumer.pull(limit=1)[0][1] for _ in range(2)]
+    assert taken == ['a', 'b']
