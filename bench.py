@@ -800,6 +800,15 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         'baseline_gpu_idle_pct': _r(ref['gpu_idle_pct']),
         'gpu_idle_pct': _r(summary['gpu_idle_pct']),
         'standby_gpu_s': _r(summary['standby_gpu_s']),
+        # where that standby time went, per arrival wake: the hold before
+        # the tick that assigns a woken standby, the drained worker's wait
+        # for the park, and its exit (context + communicator teardown)
+        'standby_split': {k: _r(v) for k, v in
+                          summary['standby_split'].items()},
+        'standby_per_wake_ms': {
+            k[:-2]: _r(1e3 * v / max(1, summary['cold_starts']), 2)
+            for k, v in summary['standby_split'].items()
+            if k.endswith('_s') and k != 'total_s'},
         'gpu_alive_s': _r(summary['gpu_alive_s']),
         'gpu_busy_s': _r(summary['gpu_busy_s']),
         'gpu_idle_incl_standby_pct': _r(summary['gpu_idle_incl_standby_pct']),
@@ -836,6 +845,10 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         # deep idle: times the pool was released, and refilled by a key's
         # arrival ahead of the scale-up tick (POOL_WAKE_POLL_S)
         'pool_parks': sum(1 for e in events if e.get('ev') == 'pool_parked'),
+        # the manager's LLEN reads while the pool was parked (per queue)
+        'idle_queue_reads': {k: _r(v, 2) for k, v in (
+            metrics.idle_queue_reads(events, len(args.queues.split(',')))
+            or {}).items()} or None,
         'pool_arrival_wakes': sum(1 for e in events
                                   if e.get('ev') == 'pool_resumed' and
                                   e.get('reason') == 'arrival'),

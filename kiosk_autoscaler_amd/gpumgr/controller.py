@@ -281,6 +281,8 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                 # deep idle: parked pool, arrival wakes, current wake lead
                 'pool': {'parked': self.pool_parked,
                          'arrival_wakes': self.arrival_wakes,
+                         'queue_reads': self.queue_reads,
+                         'queue_reads_fine': self.queue_reads_fine,
                          'wake_lead_s': (self.wake_lead()
                                          if self.pool_idle_release_s > 0
                                          else None)},

@@ -64,6 +64,11 @@ class PoolMixin(object):
         self._waiting = 0
         self._next_waiting_check = 0.0
         self.arrival_wakes = 0
+        # LLEN commands this manager issued for the pool (arrival watch and
+        # demand sizing), and how many of them fell inside a wake window:
+        # the standing Redis load of an idle node
+        self.queue_reads = 0
+        self.queue_reads_fine = 0
         # worker zygote (worker/zygote.py): spawns fork from a process that
         # imported the worker (and torch, for a plug-in) without the GPU
         self.zygote_enabled = bool(zygote)
@@ -437,6 +442,7 @@ class PoolMixin(object):
                             for q in r.template.queues))
         if not queues:
             return {}
+        self.queue_reads += len(queues)
         try:
             pipe = self.redis.pipeline(transaction=False)
             for queue in queues:
@@ -467,7 +473,9 @@ class PoolMixin(object):
             self._wake_until = 0.0    # the tick scaled: the hold is done
             if self.pool_parked:
                 self.pool_parked = False
-                self.events.emit('pool_resumed')
+                self.events.emit('pool_resumed',
+                                 queue_reads=self.queue_reads,
+                                 queue_reads_fine=self.queue_reads_fine)
                 logger.info('Demand returned: refilling the warm pool.')
             return False
         released = [p for p in self.standbys.values()
@@ -501,6 +509,8 @@ class PoolMixin(object):
                 self.pool_parked = False
                 self.arrival_wakes += 1
                 self.events.emit('pool_resumed', reason='arrival',
+                                 queue_reads=self.queue_reads,
+                                 queue_reads_fine=self.queue_reads_fine,
                                  lead_s=round(self.wake_lead(), 4),
                                  tick_in_s=(round(self._next_tick - now, 4)
                                             if self._next_tick is not None
@@ -527,7 +537,9 @@ class PoolMixin(object):
                 released += 1
             del self.standbys[index]
         self.events.emit('pool_parked', standbys=released,
-                         idle_s=round(now - self._last_demand, 3))
+                         idle_s=round(now - self._last_demand, 3),
+                         queue_reads=self.queue_reads,
+                         queue_reads_fine=self.queue_reads_fine)
         logger.info('No demand for %.0f s: released %d standby process(es).',
                     now - self._last_demand, released)
         return True
@@ -600,15 +612,33 @@ class PoolMixin(object):
         its idle timeout (50 ms) was the real poll period, so a key was
         seen up to 50 ms late instead of ``pool_wake_poll_s``
         (profiles/r5_boot)."""
-        if not self._arrival_watch or self.pool_wake_poll_s <= 0 or \
-                self.redis is None:
+        if not self._arrival_watch or not self._arrival_reads():
             return None
         return self._next_arrival_check
+
+    def _arrival_reads(self):
+        """Whether ``_park_pool`` reads the queues for arrivals on this
+        pass: a deep-idle pool, or standbys whose engines were released.  A
+        resident pool (``POOL_IDLE_RELEASE_S=0``) never does, so its loop
+        must not wake for a read that is never taken (a stale
+        ``_next_arrival_check`` made the loop spin at 1 kHz)."""
+        if self.pool_wake_poll_s <= 0 or self.redis is None:
+            return False
+        if self.pool_idle_release_s > 0:
+            return True
+        return self.pool_mode == 'device' and any(
+            p.booted and not p.engine_cached for p in self.standbys.values())
 
     # queue-read period inside the wake window (the last ``wake_lead()``
     # before a parked pool's tick): an arrival there wakes the pool at once,
     # so each ms it goes unseen is a ms of the standby's boot lost
     ARRIVAL_FINE_S = 0.004
+    # queue-read period of a parked pool outside the wake window while the
+    # next tick is known: a key seen there is woken at the window's start
+    # anyway, so the reads only have to land before it.  10 reads/s per
+    # queue instead of 50 (the reference reads twice per INTERVAL,
+    # autoscaler.py:64-71); the window's first read is never skipped
+    ARRIVAL_FAR_S = 0.1
 
     def _next_arrival_read(self, now):
         """``pool_wake_poll_s`` after ``now``, but never past the start of
@@ -623,7 +653,7 @@ class PoolMixin(object):
             if now >= self._next_tick:
                 return now + period
             return now + min(period, self.ARRIVAL_FINE_S)
-        return min(now + period, window)
+        return min(now + max(period, self.ARRIVAL_FAR_S), window)
 
     def _arrived(self, now):
         """True when a managed queue grew since the last check (read every
@@ -634,6 +664,10 @@ class PoolMixin(object):
                 now < self._next_arrival_check:
             return False
         self._next_arrival_check = self._next_arrival_read(now)
+        if self.pool_parked and self._next_tick is not None and \
+                self._next_tick - self.wake_lead() <= now < self._next_tick:
+            self.queue_reads_fine += len(set(
+                q for r in self.resources.values() for q in r.template.queues))
         lengths = self._queue_lengths()
         if not lengths:
             return False

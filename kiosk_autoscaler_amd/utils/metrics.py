@@ -210,6 +210,16 @@ class _ManagerCollector(object):
         yield GaugeMetricFamily('kiosk_pool_parked', 'deep idle: the standby '
                                 'pool is released (1) or resident (0)',
                                 value=1 if pool.get('parked') else 0)
+        if pool.get('queue_reads') is not None:
+            from prometheus_client.core import CounterMetricFamily
+            reads = CounterMetricFamily(
+                'kiosk_manager_queue_reads', 'LLEN commands the manager '
+                'issued to watch the queues (arrival wake, demand sizing), '
+                'inside / outside the wake window', labels=['window'])
+            fine = pool.get('queue_reads_fine') or 0
+            reads.add_metric(['inside'], fine)
+            reads.add_metric(['outside'], pool['queue_reads'] - fine)
+            yield reads
         if pool.get('wake_lead_s') is not None:
             yield GaugeMetricFamily('kiosk_pool_wake_lead_seconds', 'how '
                                     'long before the next tick an arrival '

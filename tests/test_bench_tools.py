@@ -163,6 +163,46 @@ def test_standby_time_of_a_standby_assigned_while_booting():
         0.2 + 0.2 + 0.15)
 
 
+def test_standby_split_parts_sum_to_the_total():
+    """standby time split into the hold before the tick,
+    the drained worker's wait for the park, and its exit teardown."""
+    events = [
+        _ev('standby_ready', 0.0, pid=1, preinit={'x': 1}),
+        _ev('worker_assigned', 0.04, pid=1, worker='a'),      # hold 40 ms
+        _ev('worker_recycled', 5.0, pid=1),
+        _ev('standby_ready', 5.002, pid=1, recycled=True),
+        _ev('pool_parked', 5.01),                              # park 10 ms
+        _ev('standby_exit', 5.13, pid=1),                      # exit 120 ms
+        _ev('standby_ready', 6.0, pid=2, preinit={'x': 1}),
+        _ev('standby_exit', 6.5, pid=2),                       # other
+    ]
+    split = metrics.standby_split(events, 0, int(20e9))
+    assert split['hold_before_assign_s'] == pytest.approx(0.04)
+    assert split['park_delay_s'] == pytest.approx(0.01)
+    assert split['exit_teardown_s'] == pytest.approx(0.12)
+    assert split['other_s'] == pytest.approx(0.5)
+    assert split['total_s'] == pytest.approx(0.67)
+    assert split['exit_teardown_ms_mean'] == pytest.approx(120.0)
+    assert metrics.standby_gpu(events, 0, int(20e9)) == \
+        pytest.approx(split['total_s'])
+
+
+def test_idle_queue_reads_per_second():
+    events = [
+        _ev('pool_parked', 1.0, queue_reads=100, queue_reads_fine=10),
+        _ev('pool_resumed', 6.0, queue_reads=160, queue_reads_fine=30),
+        _ev('pool_parked', 10.0, queue_reads=200, queue_reads_fine=30),
+        _ev('pool_resumed', 15.0, queue_reads=250, queue_reads_fine=40),
+    ]
+    out = metrics.idle_queue_reads(events, queues=2)
+    assert out['parked_s'] == pytest.approx(10.0)
+    assert out['reads'] == 110
+    assert out['reads_per_s_per_queue'] == pytest.approx(110 / 10.0 / 2)
+    assert out['outside_window_per_s_per_queue'] == pytest.approx(
+        80 / 10.0 / 2)
+    assert metrics.idle_queue_reads([]) is None
+
+
 def test_loadgen_writes_hash_before_key(redis_client):
     gen = LoadGenerator(redis_client, ['predict'], rate=50.0, service_ms=5,
                         seed=1)

@@ -601,11 +601,14 @@ def test_wake_lead_sizes_for_the_second_slowest_recent_boot():
 def test_queue_reads_tighten_inside_the_wake_window():
     """profiles/r5_boot: the loop's 50 ms idle timeout was the real arrival
     poll, so a key 125 ms before the tick was seen 76 ms before it.  While
-    arrivals are watched the loop wakes for each read; reads come every
-    ``pool_wake_poll_s``, one lands on the wake window's start, and inside
-    the window they come every ``ARRIVAL_FINE_S``."""
+    arrivals are watched the loop wakes for each read; one read lands on
+    the wake window's start and inside the window they come every
+    ``ARRIVAL_FINE_S``.  Outside it a parked pool reads every
+    ``ARRIVAL_FAR_S`` (a key seen there is woken at the
+    window's start anyway), and every read is counted."""
     manager = gpumgr.GpuManager([], pool_wake_poll_s=0.02,
-                                pool_wake_lead_s=0.4)
+                                pool_wake_lead_s=0.4,
+                                pool_idle_release_s=0.01)
     manager.redis = object()
     assert manager._arrival_check_due() is None        # demand: no watch
     manager._arrival_watch = True
@@ -615,13 +618,53 @@ def test_queue_reads_tighten_inside_the_wake_window():
     assert manager._next_arrival_read(10.0) == pytest.approx(10.02)
     manager.pool_parked = True
     manager._next_tick = 11.0                 # window opens at 10.6
-    assert manager._next_arrival_read(10.0) == pytest.approx(10.02)
-    assert manager._next_arrival_read(10.59) == pytest.approx(10.6)
+    assert manager._next_arrival_read(10.0) == pytest.approx(
+        10.0 + manager.ARRIVAL_FAR_S)
+    assert manager._next_arrival_read(10.55) == pytest.approx(10.6)
     assert manager._next_arrival_read(10.7) == pytest.approx(
         10.7 + manager.ARRIVAL_FINE_S)
     assert manager._next_arrival_read(11.01) == pytest.approx(11.03)
     manager.redis = None
     assert manager._arrival_check_due() is None
+
+
+def test_parked_pool_reads_the_queue_at_most_12_times_a_second():
+    """over one 5 s tick period a parked pool's reads
+    outside the wake window stay <= 12/s per queue; the fine reads are
+    confined to the window before the tick."""
+    manager = gpumgr.GpuManager([], pool_wake_poll_s=0.02,
+                                pool_wake_lead_s=0.1,
+                                pool_idle_release_s=0.01)
+    manager.pool_parked = True
+    manager._next_tick = 5.0
+    now, reads, fine = 0.0, 0, 0
+    while now < 5.0:
+        if now >= 5.0 - manager.wake_lead():
+            fine += 1
+        reads += 1
+        now = manager._next_arrival_read(now)
+    assert (reads - fine) / (5.0 - manager.wake_lead()) <= 12
+    assert fine <= manager.wake_lead() / manager.ARRIVAL_FINE_S + 1
+
+
+def test_resident_pool_loop_does_not_spin(monkeypatch):
+    """with POOL_IDLE_RELEASE_S=0 (keep the standbys) the
+    arrival read never runs, so the loop must not wake for it: a stale
+    ``_next_arrival_check`` clamped every select to 1 ms (~1 kHz)."""
+    manager = gpumgr.GpuManager([], pool_wake_poll_s=0.02,
+                                pool_idle_release_s=0)
+    manager.redis = object()
+    manager._arrival_watch = True         # no demand
+    manager._next_arrival_check = 0.0     # in the past
+    assert manager._arrival_check_due() is None
+    timeouts = []
+
+    def poll(timeout):
+        timeouts.append(timeout)
+        manager._stop.set()
+    monkeypatch.setattr(manager, 'poll', poll)
+    manager._loop()
+    assert timeouts == [0.05]
 
 
 def test_pci_mapping_verified_and_remapped(monkeypatch):
