@@ -44,6 +44,7 @@ not fit is not started, ``steps`` then reports the cycles actually timed,
 and one JSON line is printed by rank 0 on every path, errors included.
 """
 import argparse
+import collections
 import json
 import os
 import signal
@@ -982,9 +983,23 @@ def rccl_lib_summary(events):
             last = e
     if last is None:
         return None
+    # the library each RCCL generation loaded, and the ladder's moves
+    # (slim copy -> stock library -> shm fallback; gpumgr/nodecomm.py)
+    by_gen = [{'gen': e.get('gen'), 'n': e.get('n'), 'lib': e.get('lib')}
+              for e in events if e.get('ev') == 'node_comm_ready' and
+              e.get('mode', 'init') != 'shrink' and
+              e.get('transport') == 'rccl']
     return {'slim': last.get('slim'), 'cached': last.get('cached'),
             'ms': _r(last.get('ms'), 1), 'error': last.get('error'),
-            'code_object_bytes': last.get('code_object_bytes')}
+            'code_object_bytes': last.get('code_object_bytes'),
+            'ladder': last.get('ladder'),
+            'generation_libs': dict(collections.Counter(
+                str(g['lib']) for g in by_gen)),
+            'generations': by_gen[-8:],
+            'switches': [{'gen': e.get('gen'), 'lib': e.get('lib'),
+                          'previous': e.get('previous')}
+                         for e in events
+                         if e.get('ev') == 'node_comm_library']}
 
 
 def _r(value, nd=4):

@@ -22,6 +22,12 @@
 // FAKE_RCCL_MODE (read at each call): ok | init_error | init_hang |
 // allreduce_hang | finalize_hang.
 //
+// FAKE_RCCL_FAIL_MULTIRANK_FROM=<substring>: a communicator of more than one
+// rank fails its init when THIS copy of the library was loaded from a path
+// containing the substring (dladdr) -- a slim RCCL copy broken only for
+// multi-rank P2P, so the node must move on to the stock library
+// (gpumgr/nodecomm.py's library ladder), not to shared memory.
+//
 // What grows with the rank count on a real node (bootstrap all-gathers, IPC
 // handle exchange, topology search) is modelled by FAKE_RCCL_INIT_PER_RANK_MS:
 // every init settles no sooner than nranks x that after it started, so an
@@ -59,6 +65,7 @@
 #include <string>
 #include <thread>
 
+#include <dlfcn.h>
 #include <strings.h>
 #include <unistd.h>
 
@@ -234,6 +241,19 @@ void drop_ops_of(FakeComm* c) {
   }
 }
 
+// this copy of the library was loaded from a path naming `needle`
+bool loaded_from(const char* needle) {
+  if (!needle || !*needle) return false;
+  Dl_info info;
+  if (!dladdr(reinterpret_cast<void*>(&loaded_from), &info) ||
+      !info.dli_fname) {
+    return false;
+  }
+  return std::strstr(info.dli_fname, needle) != nullptr;
+}
+
+thread_local int t_device = 0;
+
 FakeComm* new_comm(std::unique_ptr<kiosk::ShmComm> shm) {
   auto* c = new FakeComm();
   c->shm = std::move(shm);
@@ -263,6 +283,17 @@ FAKE_API void fake_hip_launch_kernel() {
 FAKE_API void fake_hip_graph_launch() {}
 
 // ---- HIP (host memory stands in for HBM) ---------------------------------
+// per-thread current device, like HIP's (only recorded: there is one "GPU")
+FAKE_API hipError_t hipSetDevice(int device) {
+  if (device < 0) return hipErrorInvalidDevice;
+  t_device = device;
+  return hipSuccess;
+}
+FAKE_API hipError_t hipGetDevice(int* device) {
+  *device = t_device;
+  return hipSuccess;
+}
+FAKE_API int fake_hip_current_device() { return t_device; }
 FAKE_API hipError_t hipStreamCreateWithFlags(hipStream_t* stream,
                                              unsigned int) {
   auto* s = new FakeStream();
@@ -364,6 +395,8 @@ FAKE_API ncclResult_t ncclCommInitRankConfig(ncclComm_t* comm, int nranks,
     c = new_comm(std::move(shm));
     c->rank = rank;
     c->nranks = nranks;
+    if (nranks > 1 && loaded_from(std::getenv("FAKE_RCCL_FAIL_MULTIRANK_FROM")))
+      c->init_fails = true;
     c->ready_at = c->t0 + std::chrono::milliseconds(
                               env_ms("FAKE_RCCL_INIT_PER_RANK_MS") * nranks);
   }

@@ -321,6 +321,12 @@ PYBIND11_MODULE(_kiosk_hip, m) {
       py::arg("w"), py::arg("n"), py::arg("record"), py::arg("nblocks"),
       py::arg("iters"), py::arg("lds_bytes"), py::arg("stream") = 0,
       py::call_guard<py::gil_scoped_release>());
+  // WORKER_PIN=visible: the worker's GPU on the calling thread (the HIP
+  // current device is per thread)
+  m.def(
+      "set_device",
+      [](int device) { check_hip(hipSetDevice(device), "hipSetDevice"); },
+      py::arg("device"), py::call_guard<py::gil_scoped_release>());
   m.def(
       "preinit_device",
       [](int device) {

@@ -20,6 +20,10 @@ void bind_comm(py::module_& m) {
                                            PyExc_RuntimeError);
   m.def("rccl_library", &rccl_library, py::call_guard<py::gil_scoped_release>());
   m.def("rccl_version", &rccl_version, py::call_guard<py::gil_scoped_release>());
+  m.def("fence_use_library", &rccl_use_library, py::arg("path"),
+        py::call_guard<py::gil_scoped_release>());
+  m.def("rccl_loaded_libraries", &rccl_loaded_libraries,
+        py::call_guard<py::gil_scoped_release>());
   m.def("fence_can_shrink", &rccl_can_shrink,
         py::call_guard<py::gil_scoped_release>());
   m.def("fence_warmup", &rccl_warmup, py::arg("timeout") = 60.0,

@@ -4,12 +4,14 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <thread>
+#include <vector>
 
 #include "engine.hpp"
 #include "trace.hpp"
@@ -41,51 +43,76 @@ void bind(void* handle, const char* name, T& slot, bool required) {
   }
 }
 
-RcclApi* load_rccl() {
+// One library path: dlopen + symbol binding, or nullptr with `errors`
+// extended.  A handle is never closed (an RCCL cannot be unloaded safely).
+RcclApi* load_rccl_path(const std::string& path, std::string& errors) {
+  void* handle = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+  if (!handle) {
+    const char* e = dlerror();
+    errors += path + ": " + (e ? e : "?") + "; ";
+    return nullptr;
+  }
+  auto* api = new RcclApi();
+  api->handle = handle;
+  api->path = path;
+  try {
+    bind(handle, "ncclGetVersion", api->GetVersion, true);
+    bind(handle, "ncclGetUniqueId", api->GetUniqueId, true);
+    bind(handle, "ncclCommInitRankConfig", api->CommInitRankConfig, true);
+    bind(handle, "ncclCommGetAsyncError", api->CommGetAsyncError, true);
+    bind(handle, "ncclCommAbort", api->CommAbort, true);
+    bind(handle, "ncclCommDestroy", api->CommDestroy, true);
+    bind(handle, "ncclCommFinalize", api->CommFinalize, true);
+    bind(handle, "ncclAllReduce", api->AllReduce, true);
+    bind(handle, "ncclGetErrorString", api->GetErrorString, true);
+    bind(handle, "ncclCommShrink", api->CommShrink, false);
+  } catch (const std::exception& e) {
+    errors += path + ": " + e.what() + "; ";
+    delete api;
+    return nullptr;
+  }
+  return api;
+}
+
+// Every library loaded so far (path -> api) and the one new communicators
+// use.  The manager can move a node from one RCCL to another between
+// generations (slim copy -> stock library, gpumgr/nodecomm.py): a process
+// that loaded the slim copy loads the stock one beside it (RTLD_LOCAL: two
+// independent copies), and a Fence keeps the api it was built with.
+std::mutex g_api_mu;
+std::vector<RcclApi*> g_apis;
+std::atomic<RcclApi*> g_current{nullptr};
+std::string g_error;
+
+RcclApi* find_loaded(const std::string& path) {
+  for (RcclApi* api : g_apis) {
+    if (api->path == path) return api;
+  }
+  return nullptr;
+}
+
+RcclApi* load_default() {
   std::vector<std::string> candidates;
   if (const char* env = std::getenv("KIOSK_RCCL_LIB")) candidates.push_back(env);
   candidates.push_back("/opt/rocm/lib/librccl.so.1");
   candidates.push_back("librccl.so.1");
   std::string errors;
   for (const auto& path : candidates) {
-    void* handle = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
-    if (!handle) {
-      const char* e = dlerror();
-      errors += path + ": " + (e ? e : "?") + "; ";
-      continue;
+    if (RcclApi* api = find_loaded(path)) return api;
+    if (RcclApi* api = load_rccl_path(path, errors)) {
+      g_apis.push_back(api);
+      return api;
     }
-    auto* api = new RcclApi();
-    api->handle = handle;
-    api->path = path;
-    try {
-      bind(handle, "ncclGetVersion", api->GetVersion, true);
-      bind(handle, "ncclGetUniqueId", api->GetUniqueId, true);
-      bind(handle, "ncclCommInitRankConfig", api->CommInitRankConfig, true);
-      bind(handle, "ncclCommGetAsyncError", api->CommGetAsyncError, true);
-      bind(handle, "ncclCommAbort", api->CommAbort, true);
-      bind(handle, "ncclCommDestroy", api->CommDestroy, true);
-      bind(handle, "ncclCommFinalize", api->CommFinalize, true);
-      bind(handle, "ncclAllReduce", api->AllReduce, true);
-      bind(handle, "ncclGetErrorString", api->GetErrorString, true);
-      bind(handle, "ncclCommShrink", api->CommShrink, false);
-    } catch (const std::exception& e) {
-      errors += path + ": " + e.what() + "; ";
-      delete api;
-      continue;
-    }
-    return api;
   }
-  throw std::runtime_error("no usable RCCL library: " + errors);
+  g_error = "no usable RCCL library: " + errors;
+  return nullptr;
 }
 
-std::once_flag g_once;
-RcclApi* g_api = nullptr;
-std::string g_error;
-
-void check_nccl(ncclResult_t res, const char* what) {
+void check_nccl(ncclResult_t res, const char* what,
+                const RcclApi* api = nullptr) {
   if (res != ncclSuccess && res != ncclInProgress) {
     throw std::runtime_error(std::string(what) + ": " +
-                             rccl().GetErrorString(res));
+                             (api ? *api : rccl()).GetErrorString(res));
   }
 }
 
@@ -98,15 +125,37 @@ double now_s() {
 }  // namespace
 
 const RcclApi& rccl() {
-  std::call_once(g_once, [] {
-    try {
-      g_api = load_rccl();
-    } catch (const std::exception& e) {
-      g_error = e.what();
-    }
-  });
-  if (!g_api) throw std::runtime_error(g_error);
-  return *g_api;
+  RcclApi* api = g_current.load(std::memory_order_acquire);
+  if (api) return *api;
+  std::lock_guard<std::mutex> lock(g_api_mu);
+  api = g_current.load(std::memory_order_relaxed);
+  if (!api) {
+    api = load_default();
+    if (!api) throw std::runtime_error(g_error);
+    g_current.store(api, std::memory_order_release);
+  }
+  return *api;
+}
+
+std::string rccl_use_library(const std::string& path) {
+  if (path.empty()) return rccl().path;
+  std::lock_guard<std::mutex> lock(g_api_mu);
+  RcclApi* api = find_loaded(path);
+  if (!api) {
+    std::string errors;
+    api = load_rccl_path(path, errors);
+    if (!api) throw std::runtime_error("cannot load RCCL " + errors);
+    g_apis.push_back(api);
+  }
+  g_current.store(api, std::memory_order_release);
+  return api->path;
+}
+
+std::vector<std::string> rccl_loaded_libraries() {
+  std::lock_guard<std::mutex> lock(g_api_mu);
+  std::vector<std::string> out;
+  for (RcclApi* api : g_apis) out.push_back(api->path);
+  return out;
 }
 
 std::string rccl_library() { return rccl().path; }
@@ -154,13 +203,13 @@ void Fence::wait_ready(void* comm, double timeout_s, const char* what) {
   const double deadline = now_s() + timeout_s;
   while (true) {
     ncclResult_t state = ncclSuccess;
-    ncclResult_t res = rccl().CommGetAsyncError(
+    ncclResult_t res = api_->CommGetAsyncError(
         static_cast<ncclComm_t>(comm), &state);
     if (res != ncclSuccess) state = res;
     if (state == ncclSuccess) return;
     if (state != ncclInProgress) {
       throw std::runtime_error(std::string(what) + " failed: " +
-                               rccl().GetErrorString(state));
+                               api_->GetErrorString(state));
     }
     if (abort_requested_.load(std::memory_order_relaxed)) {
       throw std::runtime_error(std::string(what) + " aborted on request");
@@ -203,7 +252,17 @@ void Fence::init(const std::string& unique_id) {
   TraceRange range("kiosk.fence.init");
   const int nranks = nranks_, rank = rank_;
   const double timeout_s = timeout_s_;
-  const RcclApi& api = rccl();
+  // every HIP call of this thread goes to the worker's device: with all
+  // managed GPUs visible (WORKER_PIN=visible) that is not ordinal 0, and
+  // the HIP current device is per thread (the node agent's is not the
+  // thread that opened the device)
+  if (const char* dev = std::getenv("KIOSK_DEVICE")) {
+    check_hip(hipSetDevice(std::atoi(dev)), "fence hipSetDevice");
+  }
+  // the library in use now (rccl_use_library); kept for this
+  // communicator's whole life, whatever later generations load
+  api_ = &rccl();
+  const RcclApi& api = *api_;
   check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking),
             "fence stream");
   check_hip(hipMalloc(reinterpret_cast<void**>(&dev_), 128 * sizeof(long long)),
@@ -220,7 +279,7 @@ void Fence::init(const std::string& unique_id) {
   config.commName = "kiosk-fence";
   ncclComm_t comm = nullptr;
   check_nccl(api.CommInitRankConfig(&comm, nranks, id, rank, &config),
-             "ncclCommInitRankConfig");
+             "ncclCommInitRankConfig", api_);
   comm_ = comm;
   wait_ready(comm_, timeout_s, "ncclCommInitRank");
 }
@@ -250,9 +309,9 @@ std::pair<std::vector<long long>, double> Fence::allreduce(
                            hipMemcpyHostToDevice, stream_),
             "fence upload");
   try {
-    check_nccl(rccl().AllReduce(dev_, dev_ + 64, n, ncclInt64, ncclSum,
+    check_nccl(api_->AllReduce(dev_, dev_ + 64, n, ncclInt64, ncclSum,
                                 static_cast<ncclComm_t>(comm_), stream_),
-               "ncclAllReduce");
+               "ncclAllReduce", api_);
     wait_ready(comm_, timeout_s_, "ncclAllReduce enqueue");
   } catch (...) {
     abort();     // a communicator whose collective failed is never reused
@@ -286,7 +345,7 @@ std::pair<std::vector<long long>, double> Fence::allreduce(
 void Fence::shrink(const std::vector<int>& excluded, double timeout_s,
                    bool abort_parent) {
   if (!comm_) throw std::runtime_error("fence communicator is closed");
-  if (!rccl().CommShrink) {
+  if (!api_->CommShrink) {
     throw std::runtime_error("this RCCL has no ncclCommShrink");
   }
   std::vector<bool> gone(nranks_, false);
@@ -300,7 +359,7 @@ void Fence::shrink(const std::vector<int>& excluded, double timeout_s,
   std::vector<int> ex(excluded);
   ncclComm_t next = nullptr;
   const int flags = abort_parent ? NCCL_SHRINK_ABORT : NCCL_SHRINK_DEFAULT;
-  ncclResult_t res = rccl().CommShrink(static_cast<ncclComm_t>(comm_),
+  ncclResult_t res = api_->CommShrink(static_cast<ncclComm_t>(comm_),
                                        ex.data(), static_cast<int>(ex.size()),
                                        &next, nullptr, flags);
   if (res != ncclSuccess && res != ncclInProgress) {
@@ -308,7 +367,7 @@ void Fence::shrink(const std::vector<int>& excluded, double timeout_s,
     // retried on it
     abort();
     throw std::runtime_error(std::string("ncclCommShrink: ") +
-                             rccl().GetErrorString(res));
+                             api_->GetErrorString(res));
   }
   try {
     wait_ready(next, timeout_s, "ncclCommShrink");
@@ -326,7 +385,7 @@ void Fence::shrink(const std::vector<int>& excluded, double timeout_s,
       }
     }
   } catch (...) {
-    if (next) rccl().CommAbort(next);   // the child is ours to abort
+    if (next) api_->CommAbort(next);   // the child is ours to abort
     abort();
     throw;
   }
@@ -339,9 +398,9 @@ void Fence::shrink(const std::vector<int>& excluded, double timeout_s,
   rank_ -= below;
   nranks_ -= static_cast<int>(excluded.size());
   if (abort_parent) {
-    rccl().CommAbort(static_cast<ncclComm_t>(old));   // a peer is gone
+    api_->CommAbort(static_cast<ncclComm_t>(old));   // a peer is gone
   } else {
-    rccl().CommDestroy(static_cast<ncclComm_t>(old));
+    api_->CommDestroy(static_cast<ncclComm_t>(old));
   }
 }
 
@@ -352,7 +411,7 @@ void Fence::request_interrupt() {
 void Fence::abort() {
   void* comm = comm_;
   comm_ = nullptr;   // cleared first: nothing can reach a freed communicator
-  if (comm) rccl().CommAbort(static_cast<ncclComm_t>(comm));
+  if (comm) api_->CommAbort(static_cast<ncclComm_t>(comm));
 }
 
 void Fence::request_abort() {
@@ -363,7 +422,7 @@ void Fence::destroy() {
   if (comm_) {
     bool finalized = false;
     if (!abort_requested_.load(std::memory_order_relaxed) && !stalled_) {
-      rccl().CommFinalize(static_cast<ncclComm_t>(comm_));
+      api_->CommFinalize(static_cast<ncclComm_t>(comm_));
       try {
         wait_ready(comm_, timeout_s_, "ncclCommFinalize");
         finalized = true;
@@ -373,7 +432,7 @@ void Fence::destroy() {
     if (finalized) {
       void* comm = comm_;
       comm_ = nullptr;
-      rccl().CommDestroy(static_cast<ncclComm_t>(comm));
+      api_->CommDestroy(static_cast<ncclComm_t>(comm));
     } else {
       abort();   // a peer is gone: finalize would wait on it
     }

@@ -17,7 +17,12 @@ namespace kiosk {
 
 struct RcclApi;
 const RcclApi& rccl();            // throws if no usable RCCL is found
-std::string rccl_library();       // path actually loaded
+std::string rccl_library();       // path new communicators use
+// Make `path` the library new communicators use (loading it beside any
+// other already loaded); "" = the default (KIOSK_RCCL_LIB, then ROCm's).
+// Returns the path in use.  Communicators built earlier keep theirs.
+std::string rccl_use_library(const std::string& path);
+std::vector<std::string> rccl_loaded_libraries();
 int rccl_version();
 bool rccl_can_shrink();
 std::string rccl_unique_id();     // 128 raw bytes
@@ -86,6 +91,7 @@ class Fence {
   void wait_ready(void* comm, double timeout_s, const char* what);
   void init(const std::string& unique_id);   // constructor body
 
+  const RcclApi* api_ = nullptr;  // the library this communicator uses
   void* comm_ = nullptr;        // ncclComm_t
   hipStream_t stream_ = nullptr;
   long long* dev_ = nullptr;    // send [64] + recv [64]

@@ -238,13 +238,29 @@ std::vector<uint8_t> strip_debug(const std::vector<uint8_t>& in) {
       eh.e_shstrndx >= eh.e_shnum) {
     throw std::runtime_error("bad section header table");
   }
+  // every offset below comes from the (untrusted) code object: checked
+  // against the buffer before it is dereferenced
+  const uint64_t size = in.size();
+  auto fits = [size](uint64_t off, uint64_t len) {
+    return off <= size && len <= size - off;
+  };
+  if (eh.e_phnum &&
+      (eh.e_phentsize != sizeof(Elf64_Phdr) ||
+       !fits(eh.e_phoff, uint64_t(eh.e_phnum) * sizeof(Elf64_Phdr)))) {
+    throw std::runtime_error("bad program header table");
+  }
   std::vector<Elf64_Shdr> sh(eh.e_shnum);
   std::memcpy(sh.data(), in.data() + eh.e_shoff, eh.e_shnum * sizeof(Elf64_Shdr));
   const Elf64_Shdr& strsec = sh[eh.e_shstrndx];
+  if (!fits(strsec.sh_offset, strsec.sh_size)) {
+    throw std::runtime_error("section name table out of bounds");
+  }
   auto name = [&](const Elf64_Shdr& s) {
-    const uint64_t at = strsec.sh_offset + s.sh_name;
-    if (at >= in.size()) return std::string();
-    return std::string(reinterpret_cast<const char*>(in.data() + at));
+    // bounded by the string table, never past its end
+    if (s.sh_name >= strsec.sh_size) return std::string();
+    const char* at = reinterpret_cast<const char*>(in.data() +
+                                                   strsec.sh_offset + s.sh_name);
+    return std::string(at, strnlen(at, strsec.sh_size - s.sh_name));
   };
   std::vector<int> remap(eh.e_shnum, -1);
   std::vector<int> kept;
@@ -253,6 +269,10 @@ std::vector<uint8_t> strip_debug(const std::vector<uint8_t>& in) {
   for (int i = 0; i < eh.e_shnum; ++i) {
     const bool alloc = sh[i].sh_flags & SHF_ALLOC;
     const bool drop = !alloc && name(sh[i]).rfind(".debug", 0) == 0;
+    if (sh[i].sh_type != SHT_NOBITS && !fits(sh[i].sh_offset, sh[i].sh_size)) {
+      throw std::runtime_error("section " + std::to_string(i) +
+                               " out of bounds");
+    }
     if (alloc) {
       last_alloc = i;
       if (sh[i].sh_type != SHT_NOBITS) {
@@ -274,8 +294,12 @@ std::vector<uint8_t> strip_debug(const std::vector<uint8_t>& in) {
   }
   for (int i = 0; i < eh.e_phnum; ++i) {
     const auto ph = load<Elf64_Phdr>(in.data() + eh.e_phoff + i * sizeof(Elf64_Phdr));
+    if (!fits(ph.p_offset, ph.p_filesz)) {
+      throw std::runtime_error("segment out of bounds");
+    }
     loaded_end = std::max<uint64_t>(loaded_end, ph.p_offset + ph.p_filesz);
   }
+  if (loaded_end > size) throw std::runtime_error("loaded image out of bounds");
   std::vector<uint8_t> out(in.begin(), in.begin() + loaded_end);
   std::vector<Elf64_Shdr> new_sh;
   for (int i : kept) {
@@ -378,13 +402,22 @@ int run(int argc, char** argv) {
   }
   const auto* shdrs = reinterpret_cast<const Elf64_Shdr*>(s.data + eh.e_shoff);
   const Elf64_Shdr& strsec = shdrs[eh.e_shstrndx];
+  if (strsec.sh_offset > s.size || strsec.sh_size > s.size - strsec.sh_offset) {
+    throw std::runtime_error("section name table out of bounds");
+  }
   const Elf64_Shdr* fat = nullptr;
+  static const char kFat[] = ".hip_fatbin";
   for (int i = 0; i < eh.e_shnum; ++i) {
+    // a name is compared only within the string table
+    if (shdrs[i].sh_name >= strsec.sh_size ||
+        strsec.sh_size - shdrs[i].sh_name < sizeof(kFat)) {
+      continue;
+    }
     const char* nm = reinterpret_cast<const char*>(s.data + strsec.sh_offset +
                                                    shdrs[i].sh_name);
-    if (std::strcmp(nm, ".hip_fatbin") == 0) fat = &shdrs[i];
+    if (std::memcmp(nm, kFat, sizeof(kFat)) == 0) fat = &shdrs[i];
   }
-  if (!fat || fat->sh_offset + fat->sh_size > s.size) {
+  if (!fat || fat->sh_offset > s.size || fat->sh_size > s.size - fat->sh_offset) {
     throw std::runtime_error("no .hip_fatbin section");
   }
   const uint8_t* sec = s.data + fat->sh_offset;

@@ -427,10 +427,15 @@ def generation_stats(events):
     by_n = collections.defaultdict(lambda: {
         'count': 0, 'init_ms': [], 'phases': collections.defaultdict(list),
         'transports': collections.Counter(), 'link_types': set(),
-        'non_gpu_peers': 0, 'non_xgmi_links': 0, 'allreduce_us': []})
+        'non_gpu_peers': 0, 'non_xgmi_links': 0, 'allreduce_us': [],
+        'libs': collections.Counter()})
     for e in inits:
         row = by_n[str(int(e.get('n') or 0))]
         row['count'] += 1
+        # the RCCL library the generation's ranks loaded (the ladder:
+        # slim copy, then stock; gpumgr/nodecomm.py)
+        if e.get('lib'):
+            row['libs'][str(e['lib'])] += 1
         row['init_ms'].append(float(e.get('init_ms') or 0.0))
         for rank in e.get('ranks') or ():
             for phase, ms in (rank.get('init') or {}).items():
@@ -461,6 +466,7 @@ def generation_stats(events):
             'non_gpu_peers': row['non_gpu_peers'],
             'non_xgmi_links': row['non_xgmi_links'],
             'allreduce_us_mean': _mean(row['allreduce_us']),
+            'libs': dict(row['libs']),
         }
     largest = None
     if inits:

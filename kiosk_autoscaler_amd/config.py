@@ -192,6 +192,11 @@ EXTRA_DEFAULTS = (
     # a cold PyTorch spawn can take far longer than a key: set start apart)
     ('WORKER_TIMEOUT', str, '0'),
     ('WORKER_RECYCLE', bool, True),         # drained worker -> warm pool
+    # how a worker is pinned to its GPU: isolate (HIP_VISIBLE_DEVICES=<i>),
+    # visible (every managed GPU visible, the device chosen in-process, so
+    # RCCL sees its peers), auto (isolate; visible from the next spawns on
+    # once a multi-rank generation reports a non-xGMI peer path)
+    ('WORKER_PIN', str, 'auto'),
     ('METRICS_PORT', str, '0'),             # Prometheus [addr:]port (0 = off)
     ('LOG_FILE', str, 'autoscaler.log'),
 )

@@ -174,7 +174,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                  fence_fallback='shm', fence_fallback_after=2,
                  fence_init_timeout=12.0, fence_transport=None,
                  zygote=False, pool_wake_poll_s=0.0, pool_wake_hold_s=0.0,
-                 pool_wake_lead_s=0.0):
+                 pool_wake_lead_s=0.0, pin_mode='auto'):
         self.slots = list(slots)
         self.redis = redis_client
         self.state_ttl = int(state_ttl)
@@ -195,6 +195,13 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                                 & 0xfffff)
         self._stopping = False
         self.history = []   # exited workers, for accounting
+        # WORKER_PIN: isolate | visible | auto (isolate until a multi-rank
+        # generation reports a non-xGMI peer path, then visible)
+        if pin_mode not in ('isolate', 'visible', 'auto'):
+            raise ValueError('WORKER_PIN must be isolate, visible or auto, '
+                             'got %r' % (pin_mode,))
+        self.pin_auto = pin_mode == 'auto'
+        self.pin_mode = 'visible' if pin_mode == 'visible' else 'isolate'
         self._init_pool(pool_size, pool_template, pool_mode, recycle,
                         pool_idle_release_s, pool_wake_poll_s,
                         pool_wake_hold_s, pool_wake_lead_s, zygote)
@@ -269,6 +276,45 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
     def patch_namespaced_job(self, name, namespace, body):
         return self._patch('job', name, namespace, body)
 
+    def pin_fields(self):
+        """The pin of a process spawned now: ``{}`` (isolate: the worker
+        sets ``HIP_VISIBLE_DEVICES`` to its GPU alone) or ``{'visible':
+        [every managed GPU]}`` (the worker keeps them all visible and
+        selects its own in-process, ``worker/pinning.py``)."""
+        if self.pin_mode != 'visible':
+            return {}
+        return {'visible': [s.visible_id for s in self.slots
+                            if getattr(s, 'kind', 'gpu') == 'gpu' and
+                            s.visible_id not in (None, '')]}
+
+    def note_peer_path(self, gen, n, detail):
+        """A multi-rank generation's RCCL reported a peer path that is not
+        xGMI peer-to-peer.  With ``WORKER_PIN=auto`` the manager moves to
+        the ``visible`` pin: processes spawned from now on see every managed
+        GPU (RCCL may not pick P2P to a device its process cannot see), and
+        idle standbys of the old pin are retired so their replacements join
+        the next generation.  Called under the manager lock."""
+        if not self.pin_auto or self.pin_mode == 'visible' or n < 2:
+            return False
+        self.pin_mode = 'visible'
+        self.events.emit('pin_mode', mode='visible', reason=detail, gen=gen,
+                         n=n)
+        logger.warning('Generation %s (%d ranks) reported %s: spawning '
+                       'workers with every managed GPU visible from now on.',
+                       gen, n, detail)
+        stale = [index for index, proc in self.standbys.items()
+                 if getattr(proc, 'pin_mode', 'isolate') != 'visible']
+        for index in stale:
+            proc = self.standbys.pop(index)
+            if proc.popen.poll() is None:
+                proc.pipe.send({'cmd': 'exit'})
+                self.retiring.append(proc)
+        if stale:
+            self.events.emit('standby_retired', standbys=len(stale),
+                             reason='pin mode')
+            self._publish_pool()
+        return True
+
     def status(self):
         with self.lock:
             return {
@@ -278,6 +324,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                              for index, p in self.standbys.items()],
                 'node_comm': (self.node.summary() if self.node is not None
                               else None),
+                'pin_mode': self.pin_mode,
                 # deep idle: parked pool, arrival wakes, current wake lead
                 'pool': {'parked': self.pool_parked,
                          'arrival_wakes': self.arrival_wakes,
@@ -326,15 +373,26 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
             return None
         # (traced for the fake RCCL of the CPU stack too: same log lines)
         self._configure_rccl_trace()
+        ladder = [p for p in os.environ.get('KIOSK_RCCL_LADDER', '').split(
+            os.pathsep) if p]
         if os.environ.get('KIOSK_NATIVE') == 'fake' or \
                 not any(getattr(s, 'kind', 'gpu') == 'gpu'
                         for s in self.slots):
-            return None      # the fake-HIP CPU stack keeps its own library
+            # the fake-HIP CPU stack keeps its own library (a test may give
+            # it a ladder of copies)
+            self.node.rccl_libs = ladder
+            return None
         from ..parallel import rccl_lib
         info = rccl_lib.configure(log=logger)
+        if not ladder and info.get('slim') and info.get('lib'):
+            # slim copy first, then the library it was made from: a slim
+            # copy broken for multi-rank P2P ends on stock RCCL, not on shm
+            ladder = [info['lib'], rccl_lib.source_library()]
+        self.node.rccl_libs = ladder
         self.events.emit('rccl_lib', lib=info.get('lib'),
                          slim=info.get('slim'), cached=info.get('cached'),
                          ms=info.get('ms'), error=info.get('error'),
+                         ladder=ladder,
                          code_object_bytes=info.get('slim_code_object_bytes'))
         return info
 
@@ -517,6 +575,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
             'recycle': self._recycle_ok(resource),
             'node_fence': self.node is not None,
         }
+        assign.update(self.pin_fields())
         proc = self._take_standby(resource.template, slot)
         from_pool = proc is not None
         sizing = None

@@ -106,6 +106,15 @@ class NodeComm(object):
         self.can_shrink = False
         self.fallback_used = None
         self.last_error = None   # why the last generation / shrink failed
+        # RCCL library ladder: the libraries an RCCL
+        # generation may load, best first -- the one-ISA slim copy, then
+        # ROCm's stock library.  ``fallback_after`` failed generations on
+        # one move the node to the next; only when the last fails too does
+        # the ``fallback`` transport (shm) take over.  Empty: every process
+        # loads its default (KIOSK_RCCL_LIB, else ROCm's).
+        self.rccl_libs = []
+        self.lib_index = 0
+        self.lib_switches = 0
 
     # ------------------------------------------------------------------
     @property
@@ -149,8 +158,41 @@ class NodeComm(object):
                 'quarantines': self.quarantines,
                 'fallbacks': self.fallbacks,
                 'rccl_retries': self.rccl_retries,
+                'rccl_lib': self.current_lib(),
+                'lib_switches': self.lib_switches,
                 'gen_timeout': self.gen_timeout,
                 'last_error': self.last_error}
+
+    def current_lib(self):
+        """The RCCL library the next RCCL generation asks its ranks to use
+        (None: their default)."""
+        if not self.rccl_libs or \
+                self.transport_override not in (None, 'rccl'):
+            return None
+        return self.rccl_libs[min(self.lib_index, len(self.rccl_libs) - 1)]
+
+    def _next_lib(self, reason, now):
+        """After ``fallback_after`` failed RCCL generations: move to the
+        next library of the ladder.  False when none is left."""
+        if self.transport_override not in (None, 'rccl') or \
+                self.lib_index + 1 >= len(self.rccl_libs):
+            return False
+        old = self.rccl_libs[self.lib_index]
+        self.lib_index += 1
+        new = self.rccl_libs[self.lib_index]
+        self.lib_switches += 1
+        self.failures = 0
+        self.retry_at = now
+        # processes spawned from now on load it first (zygote children
+        # load it beside the copy the zygote mapped, at their connect)
+        import os
+        os.environ['KIOSK_RCCL_LIB'] = new
+        self.m.events.emit('node_comm_library', gen=self.gen, lib=new,
+                           previous=old, reason=reason)
+        logger.warning('Node communicator: RCCL from %s failed %d '
+                       'generations; trying %s.', old, self.fallback_after,
+                       new)
+        return True
 
     def _bound(self):
         """slot index -> the process currently serving that slot."""
@@ -422,6 +464,11 @@ class NodeComm(object):
         n = len(members)
         warm = all(getattr(proc, 'rccl_inits', 0) > 0 for _, proc in members)
         rccl = self.transport_override in (None, 'rccl')
+        lib = self.current_lib()
+        # a library switch loads a library new to every rank: the longer
+        # first-generation budget
+        warm = warm and all(getattr(proc, 'rccl_lib', None) == lib
+                            for _, proc in members) if lib else warm
         self.gen_timeout = self.init_timeout if warm or not rccl else \
             self.first_init_timeout
         for rank, (_, proc) in enumerate(members):
@@ -429,11 +476,13 @@ class NodeComm(object):
                        'nranks': n, 'timeout': self.gen_timeout}
             if self.transport_override:
                 message['transport'] = self.transport_override
+            if lib:
+                message['lib'] = lib
             proc.pipe.send(message)
         self.m.events.emit('node_comm_init', gen=self.gen, n=n,
                            slots=[index for index, _ in members],
                            pids=[proc.pid for _, proc in members],
-                           transport=self.transport_override)
+                           transport=self.transport_override, lib=lib)
         logger.info('Node communicator generation %d: %d ranks.', self.gen, n)
         self.m._publish_pool()
 
@@ -503,7 +552,10 @@ class NodeComm(object):
             self.failed_total += 1
             self.retry_at = now + min(30.0, 0.25 * 2 ** min(self.failures - 1,
                                                              8))
-            if (self.fallback and self.transport_override != self.fallback
+            if self.failures >= self.fallback_after and \
+                    self._next_lib(reason, now):
+                pass
+            elif (self.fallback and self.transport_override != self.fallback
                     and self.fallback_used is None and
                     self.failures >= self.fallback_after):
                 self.transport_override = self.fallback
@@ -577,6 +629,7 @@ class NodeComm(object):
             self.ready_ranks[rank] = message
             if message.get('transport') == 'rccl':
                 proc.rccl_inits = getattr(proc, 'rccl_inits', 0) + 1
+                proc.rccl_lib = message.get('lib') or self.current_lib()
             if self.verdict is not None:
                 self.verdict['reported'].add(rank)
                 return
@@ -593,9 +646,13 @@ class NodeComm(object):
                 else:
                     self.failures = 0
                     self.generations += 1
+                libs = sorted({str(r.get('lib')) for r in
+                               self.ready_ranks.values() if r.get('lib')})
                 self.m.events.emit('node_comm_ready', gen=self.gen,
                                    sub=self.sub, n=len(self.members),
                                    init_ms=init_ms, transport=self.transport,
+                                   lib=(libs[0] if len(libs) == 1 else
+                                        libs or None),
                                    mode='shrink' if shrunk else 'init',
                                    ranks=self._rank_table())
                 logger.info('Node communicator generation %d.%d ready (%d '
@@ -680,11 +737,16 @@ class NodeComm(object):
                            non_gpu_peer=flagged, non_xgmi_links=links,
                            memory_bytes=rccl.get('memory_bytes'),
                            allreduce_us=message.get('allreduce_us'))
-        if flagged or (links and int(message.get('n') or 0) > 1):
+        n = int(message.get('n') or 0)
+        if flagged or (links and n > 1):
             logger.warning('Node communicator generation %s rank %s: RCCL '
                            'path is not xGMI peer-to-peer (%s; links %s).',
                            message.get('gen'), message.get('rank'),
                            ', '.join(flagged) or 'P2P', links)
+            note = getattr(self.m, 'note_peer_path', None)
+            if note is not None and n > 1:
+                note(message.get('gen'), n, 'peer path %s; links %s' % (
+                    ', '.join(flagged) or 'P2P', links))
 
     # ------------------------------------------------------------------
     def can_fence(self, procs):

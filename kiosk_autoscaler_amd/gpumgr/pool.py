@@ -121,11 +121,16 @@ class PoolMixin(object):
             '-m', 'kiosk_autoscaler_amd.worker.zygote', '--backend',
             tpl.backend]
         rocr = self._rocr_embryos = self.zygote_rocr_embryos(tpl)
+        # each ROCr embryo initialises its slot's GPU only (lowest slots
+        # first: the slots a scale-up takes first)
+        gpus = [s.visible_id for s in self.slots
+                if getattr(s, 'kind', 'gpu') == 'gpu'][:rocr]
         self.zygote = zygote.ZygoteClient(argv, self._environment(tpl),
                                           embryos=self.zygote_embryos(),
-                                          rocr_embryos=rocr)
+                                          rocr_embryos=rocr, rocr_gpus=gpus)
         self.events.emit('zygote_spawn', pid=self.zygote.pid,
-                         embryos=self.zygote_embryos(), rocr_embryos=rocr)
+                         embryos=self.zygote_embryos(), rocr_embryos=rocr,
+                         rocr_gpus=gpus)
 
     def zygote_embryos(self):
         """Pre-forked workers the zygote keeps (one per GPU slot, at most
@@ -139,15 +144,15 @@ class PoolMixin(object):
 
     def zygote_rocr_embryos(self, template):
         """How many embryos initialise ROCr while they wait (HIP workers
-        only; ``ZYGOTE_ROCR_EMBRYOS`` overrides, 0 = none).  Each halves a
-        woken standby's boot (~105 -> ~56 ms, profiles/r5_boot) and takes
-        ROCr's init variance (110-300 ms spikes) off the scale-up path, but
-        opens the devices while it waits.  By default only a manager of one
-        or two slots keeps them: a wider wake is as late as its slowest boot,
-        so a few fast embryos would not move it, and every one more process
-        on the devices counts against their process budget.  Not when
-        ``ROCR_VISIBLE_DEVICES`` lists several devices: each worker re-pins
-        to one of them, so an early init could never be kept."""
+        only; ``ZYGOTE_ROCR_EMBRYOS`` overrides, 0 = none): one per GPU slot
+        (at most the embryo count), each bound to its slot's GPU
+        (``ROCR_VISIBLE_DEVICES=<gpu>`` for its ``hsa_init``), so it opens
+        that device alone -- not every device of the node -- and a worker of
+        that slot keeps the init.  Each halves a woken standby's boot (~105
+        -> ~56 ms, profiles/r5_boot) and takes ROCr's init variance
+        (110-300 ms spikes) off the scale-up path, on every slot of an
+        8-GPU node (round 5 kept them to managers of one
+        or two slots because an unbound embryo opened every device)."""
         if template is None or template.backend not in ('hip', 'auto') or \
                 not any(getattr(slot, 'kind', 'gpu') != 'cpu'
                         for slot in self.slots):
@@ -156,11 +161,8 @@ class PoolMixin(object):
         if override.strip():
             wanted = max(0, int(override))
         else:
-            wanted = 2 if len(self.slots) <= 2 else 0
-        rocr = [d for d in os.environ.get('ROCR_VISIBLE_DEVICES',
-                                          '').split(',') if d.strip()]
-        if len(rocr) > 1:
-            return 0
+            wanted = sum(1 for slot in self.slots
+                         if getattr(slot, 'kind', 'gpu') == 'gpu')
         return min(self.zygote_embryos(), wanted)
 
     def _check_zygote(self):
@@ -237,6 +239,7 @@ class PoolMixin(object):
             pin = {'gpu': slot.visible_id, 'slot': slot.index,
                    'cpus': slot.cpus, 'preinit': self.pool_mode,
                    'node_fence': self.node is not None}
+            pin.update(self.pin_fields())
             if prebuild:
                 pin['prebuild'] = self._prebuild_spec(template)
             args += ['--pin', json.dumps(pin)]
@@ -280,6 +283,7 @@ class PoolMixin(object):
         proc.woken = woken
         proc.slot = slot.index if slot is not None else None
         proc.via = via
+        proc.pin_mode = getattr(self, 'pin_mode', 'isolate')
         self.events.emit('process_spawn', role=role, pid=popen.pid,
                          slot=proc.slot, via=via,
                          embryo=bool(getattr(popen, 'embryo', False)),
@@ -563,39 +567,52 @@ class PoolMixin(object):
                 self._wake_at = min(self._wake_at, self._next_tick - lead)
         self._wake()
 
-    # margin of the wake lead over the boot it is sized for: the manager's
-    # loop wakes on time (``_loop`` sleeps to ``_wake_at``), so this covers
-    # the spawn request (0.5 ms from an embryo) and a boot's jitter, not a
-    # poll period
+    # margin of the wake lead over the boot it is sized for, from the
+    # measured spread (not constants fitted on one box):
+    # FLOOR covers the spawn request (0.5 ms from an embryo) and the loop's
+    # wake-up; SPREAD_K times the distance between the sized boot and the
+    # median boot covers the jitter the recent boots show, so a busier
+    # 8-GPU host with concurrent boots gets a wider margin by itself.
+    # Replayed over round 5's 576 woken boots (tools/wake_lead_replay.py):
+    # late 4.6 ms / hold 84 ms a wake against 3.9 / 83 for the former fixed
+    # +50 ms; over the ROCr-embryo boots 0 late and 25 ms hold against 32
+    # for the former fixed +30 ms
+    WAKE_MARGIN_FLOOR_S = 0.01
+    WAKE_SPREAD_K = 3.0
+    WAKE_MARGIN_MAX_S = 0.06
+    # (while fewer than 4 boots are known: the slowest plus this)
     WAKE_MARGIN_S = 0.05
-    # with ROCr initialised in the embryos the boots are tight (0.049-0.062
-    # s, contexts 11-27 ms): over the 177 such woken boots of round 5, +30 ms
-    # is never late and holds 20 ms a wake less than +50 ms
-    # (tools/wake_lead_replay.py, profiles/r5_boot/README.md section 5)
-    WAKE_MARGIN_ROCR_S = 0.03
+
+    def wake_margin(self, boots=None):
+        """Seconds of lead beyond the sized boot (see the constants)."""
+        boots = sorted(self._wake_boots if boots is None else boots)
+        if len(boots) < 4:
+            return self.WAKE_MARGIN_S
+        sized, median = boots[-2], boots[len(boots) // 2]
+        return min(self.WAKE_MARGIN_MAX_S,
+                   max(self.WAKE_MARGIN_FLOOR_S,
+                       self.WAKE_MARGIN_FLOOR_S +
+                       self.WAKE_SPREAD_K * (sized - median)))
 
     def wake_lead(self):
         """Seconds before the next tick an arrival wakes a parked pool:
         ``pool_wake_lead_s`` until woken standbys have been timed, then the
         second slowest of the last 16 spawn -> booted+prebuilt times (the
-        slowest while fewer than 4 are known) plus ``WAKE_MARGIN_S``, never
-        above ``pool_wake_lead_s``.  Every second of lead beyond the boot is
-        a standby holding its GPU unassigned; a boot slower than the lead is
-        late by the difference.  The boot's spread is the HIP context
-        (50-70 ms, now and then 150 ms, once in a while 0.5 s:
+        slowest while fewer than 4 are known) plus :meth:`wake_margin`,
+        never above ``pool_wake_lead_s``.  Every second of lead beyond the
+        boot is a standby holding its GPU unassigned; a boot slower than
+        the lead is late by the difference.  The boot's spread is the HIP
+        context (50-70 ms, now and then 150 ms, once in a while 0.5 s:
         profiles/r4_boot, profiles/r5_boot), so the slowest sample is an
         outlier the next wakes rarely repeat: over 576 woken boots of rounds
-        4-5, the second slowest of 16 + 50 ms is late less often and by less
-        than the slowest of 8 + 30 ms (3.9 against 4.4 ms a wake) and holds
-        10 ms less (83 against 94 ms a wake; tools/wake_lead_replay.py)."""
+        4-5, the second slowest of 16 is late less often and by less than
+        the slowest of 8 and holds less (tools/wake_lead_replay.py)."""
         cap = self.pool_wake_lead_s
         if cap <= 0 or not self._wake_boots:
             return cap
         boots = sorted(self._wake_boots)
         sized = boots[-2] if len(boots) >= 4 else boots[-1]
-        margin = self.WAKE_MARGIN_ROCR_S if getattr(
-            self, '_rocr_embryos', 0) else self.WAKE_MARGIN_S
-        return min(cap, sized + margin)
+        return min(cap, sized + self.wake_margin(boots))
 
     def _prebuild_spec(self, template):
         """What an arrival-woken standby builds its engine for: the shape
@@ -691,6 +708,9 @@ class PoolMixin(object):
         proc = self.standbys.get(slot.index)
         if proc is None or proc.popen.poll() is not None:
             return None
+        if getattr(proc, 'pin_mode', 'isolate') != \
+                getattr(self, 'pin_mode', 'isolate'):
+            return None      # pinned the old way (WORKER_PIN=auto switched)
         del self.standbys[slot.index]
         self._publish_pool()
         return proc
@@ -834,6 +854,8 @@ class PoolMixin(object):
         proc.recycles += 1
         if (self._recycle_ok(resource) and slot.index not in self.standbys
                 and len(self.standbys) < self.pool_size and
+                getattr(proc, 'pin_mode', 'isolate') ==
+                getattr(self, 'pin_mode', 'isolate') and
                 not getattr(proc, 'node_quarantined', False)):
             proc.role = 'standby'
             proc.slot = slot.index

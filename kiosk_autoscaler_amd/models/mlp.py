@@ -164,7 +164,9 @@ class HipMlpEngine(object):
             stage('native_loaded')
         self.cfg = cfg
         self.reused = False     # served an earlier assignment (engine cache)
-        self.engine = mod.Engine(0, cfg.dim, cfg.hidden, cfg.layers,
+        from ..worker.pinning import device_ordinal
+        self.engine = mod.Engine(device_ordinal(), cfg.dim, cfg.hidden,
+                                 cfg.layers,
                                  max(cfg.rows * cfg.batch, 256), cfg.seed)
         self.pass_ms = {}
         if stage:

@@ -82,6 +82,15 @@ class _Carver(object):
         return view.view(tuple(int(d) for d in shape))
 
 
+def _select_device(torch):
+    """``WORKER_PIN=visible`` (every managed GPU visible): the worker's own
+    GPU is ``KIOSK_DEVICE``; with the default pin it is the only one."""
+    from ..worker.pinning import device_ordinal
+    ordinal = device_ordinal()
+    if ordinal != torch.cuda.current_device():
+        torch.cuda.set_device(ordinal)
+
+
 class TorchKioskEngine(object):
     name = 'torch-kiosk'
     # no collective of its own: the worker caps the node communicator's
@@ -97,6 +106,7 @@ class TorchKioskEngine(object):
         (profiles/r4_comgr, profiles/r5_boot)."""
         import torch
         torch.cuda.init()
+        _select_device(torch)
         native.load().prepare_kernels()
 
     def __init__(self, cfg, stage=None):
@@ -105,7 +115,8 @@ class TorchKioskEngine(object):
             raise RuntimeError('TorchKioskEngine needs a GPU')
         self.torch = torch
         self.mod = native.load()       # after torch: one HIP runtime
-        self.device = torch.device('cuda')
+        _select_device(torch)
+        self.device = torch.device('cuda', torch.cuda.current_device())
         self.dim, self.hidden, self.layers = cfg.dim, cfg.hidden, cfg.layers
         self.max_rows = max(int(cfg.rows) * int(cfg.batch), 256)
         self.seed = int(cfg.seed)

@@ -159,9 +159,6 @@ class RcclNodeTransport(object):
         parsed = self.trace.take()
         return summary(parsed) if parsed is not None else None
 
-    def make_uid(self, gen):
-        return self.native.fence_unique_id().hex()
-
     def preload(self):
         """RCCL's per-process one-time costs (library load + init), paid
         when the agent starts rather than inside a generation: ms."""
@@ -174,13 +171,36 @@ class RcclNodeTransport(object):
         preload = getattr(self.native, 'fence_preload', None)
         return preload() if preload is not None else 0.0
 
+    def use_library(self, lib):
+        """Make ``lib`` the RCCL this process's next communicator uses
+        (the manager's library ladder, gpumgr/nodecomm.py); loaded beside
+        any other already mapped.  Returns the library in use."""
+        use = getattr(self.native, 'fence_use_library', None)
+        if use is None:
+            return None
+        return use(lib or '')
+
+    @property
+    def library(self):
+        try:
+            return self.native.rccl_library()
+        except Exception:  # pylint: disable=broad-except
+            return None
+
+    def make_uid(self, gen, lib=None):
+        if lib:
+            self.use_library(lib)
+        return self.native.fence_unique_id().hex()
+
     def connect(self, gen, rank, nranks, uid, should_abort=None,
-                timeout=None):
+                timeout=None, lib=None):
         # two-phase: the object exists before the collective blocks, so a
         # peer death can abort it from the reader thread (request_abort);
         # an abort that raced ahead of the assignment is caught by the
         # check right after it.  ``timeout``: this connect's bound (a
         # first generation's is longer); collectives keep ``self.timeout``
+        if lib:
+            self.use_library(lib)
         self.comm = self.native.Fence(nranks, rank, timeout or self.timeout)
         if should_abort is not None and should_abort():
             self.comm.request_abort()
@@ -641,12 +661,17 @@ class NodeFenceAgent(object):
         try:
             if self._aborted(gen):
                 raise FenceError('generation %d aborted' % gen)
+            lib = message.get('lib') if self.transport.name == 'rccl' \
+                else None
             if rank == 0:
-                uid = self.transport.make_uid(gen)
+                uid = (self.transport.make_uid(gen, lib=lib) if lib else
+                       self.transport.make_uid(gen))
                 self._emit('comm_uid', gen=gen, uid=uid)
             else:
                 uid = self._wait_uid(gen, timeout)
             extra = {'timeout': timeout} if timeout else {}
+            if lib:
+                extra['lib'] = lib
             self.transport.connect(gen, rank, nranks, uid,
                                    should_abort=lambda: self._aborted(gen),
                                    **extra)
@@ -666,6 +691,9 @@ class NodeFenceAgent(object):
         # the peer transports are known after the first collective (RCCL
         # connects lazily): reported then, once per generation
         self._info_due = (gen, 0)
+        library = getattr(self.transport, 'library', None)
+        if library:
+            extra['lib'] = library
         self._emit('comm_ready', gen=gen, rank=rank, ok=True, init_ms=init_ms,
                    transport=self.transport.name, n=nranks, sub=0,
                    mode='init',

@@ -51,16 +51,32 @@ def source_library(env=None):
     return os.path.realpath(env.get('KIOSK_RCCL_SRC') or STOCK)
 
 
-def _key(src, isa, strip):
+# bumped whenever the slim copy's layout changes (a copy made
+# by an earlier, buggy tool must not be loaded after the tool is fixed)
+FORMAT_VERSION = 2
+
+
+def _tool_id(tool=None):
+    """Content hash of the slimming tool: a rebuilt tool makes a new copy."""
+    tool = tool or TOOL
+    try:
+        with open(tool, 'rb') as handle:
+            return hashlib.sha1(handle.read()).hexdigest()[:12]
+    except OSError:
+        return 'none'
+
+
+def _key(src, isa, strip, tool=None):
     st = os.stat(src)
-    text = '%s|%d|%d|%s|%d' % (src, st.st_size, st.st_mtime_ns, isa,
-                               int(strip))
+    text = '%s|%d|%d|%s|%d|v%d|%s' % (src, st.st_size, st.st_mtime_ns, isa,
+                                      int(strip), FORMAT_VERSION,
+                                      _tool_id(tool))
     return hashlib.sha1(text.encode()).hexdigest()[:16]
 
 
-def slim_dir(src, isa='gfx950', strip=True, env=None):
+def slim_dir(src, isa='gfx950', strip=True, env=None, tool=None):
     return os.path.join(cache_root(env), 'rccl-%s-%s' % (
-        isa, _key(src, isa, strip)))
+        isa, _key(src, isa, strip, tool)))
 
 
 def _link_share(target_dir, src):
@@ -103,7 +119,7 @@ def ensure_slim(src=None, isa='gfx950', strip=True, env=None, tool=None,
     tool = tool or TOOL
     t0 = time.monotonic()
     try:
-        directory = slim_dir(src, isa, strip, env)
+        directory = slim_dir(src, isa, strip, env, tool)
     except OSError as err:
         return None, {'error': 'source RCCL: %s' % err, 'src': src}
     path = os.path.join(directory, 'lib', 'librccl.so.1')

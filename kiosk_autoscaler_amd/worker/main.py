@@ -81,19 +81,24 @@ def _resolve_engine(backend):
 
 
 def _engine_collectives():
-    """Whether the engine runs collectives of its own: the built-in one
-    does not; a plug-in says so with a ``collectives`` attribute on its
-    factory (:class:`..models.torch_kiosk.TorchKioskEngine`: False),
-    assumed True when absent.  Only the factory's module is imported
-    (torch for a PyTorch engine, which the worker imports anyway)."""
+    """Whether the engine runs collectives of its own.  Decided WITHOUT
+    importing the engine (a plug-in imported here ran before the
+    GPU pin and the comgr preference, so a module-level ``torch`` import --
+    or a HIP call -- initialised the runtime on the wrong device): the
+    built-in engine and the known torch engines run none
+    (``NO_COLLECTIVES``); any other plug-in is assumed to."""
     spec = os.environ.get('WORKER_ENGINE')
     if not spec:
         return False
-    try:
-        from ..models.plugin import load_factory
-        return bool(getattr(load_factory(spec), 'collectives', True))
-    except Exception:  # pylint: disable=broad-except
-        return True
+    return spec not in NO_COLLECTIVES
+
+
+# engines known to run no collective of their own (the fence is then the
+# process's only RCCL user: one channel suffices)
+NO_COLLECTIVES = frozenset([
+    'kiosk_autoscaler_amd.models.torch_kiosk:TorchKioskEngine',
+    'kiosk_autoscaler_amd.models.torch_engine:TorchMlpEngine',
+])
 
 
 def _imports_torch():
@@ -134,6 +139,7 @@ def _warm_torch():
     import torch
     if not torch.cuda.is_available():
         return {}
+    _torch_device(torch)
     t0 = time.monotonic_ns()
     hook = None
     spec = os.environ.get('WORKER_ENGINE')
@@ -154,13 +160,33 @@ def _warm_torch():
     return {'torch_warm_start': t0, 'torch_warm_done': time.monotonic_ns()}
 
 
+def _torch_device(torch):
+    """``WORKER_PIN=visible``: torch's current device is this worker's GPU
+    (``KIOSK_DEVICE``) on the calling thread, not ordinal 0."""
+    if os.environ.get('KIOSK_DEVICE') is not None:
+        from .pinning import device_ordinal
+        torch.cuda.set_device(device_ordinal())
+
+
+def _bind_device(mod):
+    """``WORKER_PIN=visible``: the HIP current device is per thread; the
+    main thread selects the worker's GPU once the device is open (the
+    helper thread that opened it selected it for itself)."""
+    if os.environ.get('KIOSK_DEVICE') is not None and \
+            hasattr(mod, 'set_device'):
+        from .pinning import device_ordinal
+        mod.set_device(device_ordinal())
+
+
 def _open_device_async():
     from ..ops import native
+    from .pinning import device_ordinal
     mod = native.load()
 
     def run():
         try:
-            _DEVICE_OPEN['stages'] = dict(mod.preinit_device(0))
+            _DEVICE_OPEN['stages'] = dict(mod.preinit_device(
+                device_ordinal()))
             _DEVICE_OPEN['stages'].update(_warm_torch())
         except Exception as err:  # pylint: disable=broad-except
             # the engine's own init reports the failure
@@ -175,6 +201,9 @@ def _join_device_open(stage=None):
     if thread is None:
         return
     thread.join()
+    if 'error' not in _DEVICE_OPEN:
+        from ..ops import native
+        _bind_device(native.load())
     if stage:
         for name, t in sorted(_DEVICE_OPEN.get('stages', {}).items(),
                               key=lambda kv: kv[1]):
@@ -190,12 +219,14 @@ _CHANNEL = []
 
 def _device_pci(backend, preinit=None):
     """PCI address of the device this process drives (HIP ordinal 0 under
-    its HIP_VISIBLE_DEVICES pin), or None before it opened a context."""
+    its HIP_VISIBLE_DEVICES pin, ``KIOSK_DEVICE`` with every managed GPU
+    visible), or None before it opened a context."""
     if backend != 'hip' or not (preinit or _ENGINES):
         return None
     try:
         from ..ops import native
-        return native.load().device_pci_bus_id(0)
+        from .pinning import device_ordinal
+        return native.load().device_pci_bus_id(device_ordinal())
     except Exception:  # pylint: disable=broad-except
         return None
 
@@ -396,7 +427,8 @@ def main(argv=None):
         # pin before anything can initialise HIP (HIP_VISIBLE_DEVICES is
         # read once, at runtime init) and before the heavy imports
         apply_assignment_env({'gpu': early.get('gpu'),
-                              'cpus': early.get('cpus')})
+                              'cpus': early.get('cpus'),
+                              'visible': early.get('visible')})
     preload_ns = _preload(backend)
     if args.assign and backend == 'hip':
         _open_device_async()
@@ -422,7 +454,8 @@ def main(argv=None):
         from ..ops import native
         try:
             mod = native.load()
-            preinit = dict(mod.preinit_device(0))
+            from .pinning import device_ordinal
+            preinit = dict(mod.preinit_device(device_ordinal()))
             if os.environ.get('KIOSK_EMBRYO_HSA_NS'):
                 # ROCr was initialised while this process waited as an
                 # embryo (worker/zygote.py _HsaPreinit)
@@ -488,7 +521,8 @@ def main(argv=None):
                      recycles=recycles)
         gc.collect()
         pin = {'gpu': assignment.get('gpu'), 'slot': assignment.get('slot'),
-               'cpus': assignment.get('cpus')}
+               'cpus': assignment.get('cpus'),
+               'visible': assignment.get('visible')}
         assignment = None
     _join_device_open()     # never exit under a running device open
     if backend == 'hip':

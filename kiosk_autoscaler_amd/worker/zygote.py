@@ -106,7 +106,8 @@ class ZygoteLost(OSError):
 class ZygoteClient(object):
     """Manager side: start the zygote, fork workers from it."""
 
-    def __init__(self, argv, env, timeout=10.0, embryos=0, rocr_embryos=0):
+    def __init__(self, argv, env, timeout=10.0, embryos=0, rocr_embryos=0,
+                 rocr_gpus=()):
         import subprocess
         self.sock, child = socket.socketpair(socket.AF_UNIX,
                                              socket.SOCK_SEQPACKET)
@@ -116,7 +117,9 @@ class ZygoteClient(object):
         self.popen = subprocess.Popen(
             list(argv) + ['--zygote-fd', str(child.fileno()),
                           '--embryos', str(int(embryos)),
-                          '--rocr-embryos', str(int(rocr_embryos))], env=env,
+                          '--rocr-embryos', str(int(rocr_embryos)),
+                          '--rocr-gpus', ','.join(str(g) for g in
+                                                  rocr_gpus)], env=env,
             pass_fds=(child.fileno(),), close_fds=True,
             start_new_session=True)
         child.close()
@@ -368,12 +371,13 @@ def _double_fork(body):
     return int(data) if data else None
 
 
-def _embryo(esock, rocr=False):
+def _embryo(esock, rocr=False, gpu=None):
     """A pre-forked worker waiting for its request (profiles/r5_boot: the
     double ``fork`` of a torch-sized zygote, ~20 ms, was on every woken
     standby's critical path).  It holds no GPU memory and no pipe of the
     manager's until the request comes; the zygote going away ends it.
-    ``rocr``: it initialises ROCr while it waits (:class:`_HsaPreinit`)."""
+    ``rocr``: it initialises ROCr while it waits (:class:`_HsaPreinit`),
+    for GPU ``gpu`` alone when given."""
     try:
         os.setsid()
     except OSError:
@@ -387,7 +391,7 @@ def _embryo(esock, rocr=False):
                 pass
     signal.signal(signal.SIGTERM, signal.SIG_DFL)
     if rocr:
-        _PREINIT.start()
+        _PREINIT.start(gpu)
     try:
         payload, fds, _flags, _addr = socket.recv_fds(esock, MAX_MSG, 4)
     except OSError:
@@ -407,11 +411,18 @@ class _HsaPreinit(object):
     one more process on the device: few of them (gpumgr/pool.py
     ``zygote_rocr_embryos``).
 
-    ROCr reads ``ROCR_VISIBLE_DEVICES`` at ``hsa_init``, HIP applies
-    ``HIP_VISIBLE_DEVICES`` at ``hipInit``: the embryo initialises under the
-    zygote's environment and, at the hand-off, keeps that runtime only if
-    the worker's pin gives the same ``ROCR_VISIBLE_DEVICES``; otherwise it
-    shuts ROCr down again and HIP initialises it afresh."""
+    ROCr reads ``ROCR_VISIBLE_DEVICES`` (and its ``HSA_*`` settings) at
+    ``hsa_init``, HIP applies ``HIP_VISIBLE_DEVICES`` at ``hipInit``.  An
+    embryo bound to a slot's GPU (``gpu``, the zygote's ``--rocr-gpus``)
+    initialises ROCr for that device alone -- ``ROCR_VISIBLE_DEVICES=<gpu>``
+    -- instead of opening every device of the node; a worker for that GPU
+    then pins at the ROCr level too, so the init is kept.  At the hand-off
+    the runtime is kept only if the worker's environment -- the request's,
+    with its assignment's template env and pin applied -- has the same
+    ``ROCR_*`` / ``HSA_*`` variables the init ran under (an
+    ``HSA_*`` setting of another template was silently ignored); otherwise
+    ROCr is shut down again and HIP initialises it afresh (a bound embryo
+    handed another GPU's request included)."""
 
     # seconds an embryo waits before its init: the replacement forked right
     # after a hand-off stays clear of the woken worker's own boot
@@ -422,13 +433,19 @@ class _HsaPreinit(object):
         self.cancel = None
         self.lib = None
         self.rocr = None
+        self.gpu = None             # the slot GPU it is bound to, or None
+        self.snapshot = {}          # ROCR_* / HSA_* the init runs under
         self.done_ns = None
         self.status = None          # hsa_init's, once it ran
         self.fds = set()
 
-    def start(self):
+    def start(self, gpu=None):
         import threading
+        if gpu is not None:
+            self.gpu = str(gpu)
+            os.environ['ROCR_VISIBLE_DEVICES'] = self.gpu
         self.rocr = os.environ.get('ROCR_VISIBLE_DEVICES')
+        self.snapshot = _rocr_env(os.environ)
         self.cancel = threading.Event()
         self.thread = threading.Thread(target=self._run, daemon=True)
         self.thread.start()
@@ -465,15 +482,21 @@ class _HsaPreinit(object):
                 self._say('hsa_init failed (%d): HIP initialises ROCr'
                           % self.status)
             return None      # (or the request came before the init)
-        rocr = _worker_rocr(request)
-        if rocr == self.rocr:
+        gpu = _request_gpu(request)
+        if self.gpu is not None and gpu == self.gpu:
+            # the worker pins its GPU at the ROCr level, as the init did
+            request.setdefault('env', {})['ROCR_VISIBLE_DEVICES'] = self.gpu
+        worker = _rocr_env(_worker_env(request))
+        if worker == self.snapshot and \
+                (self.gpu is None or gpu == self.gpu):
             return self.done_ns
         self.lib.hsa_shut_down()
         self.lib = None
         # (self.fds stay open: the thunk below ROCr keeps its KFD descriptor
         # across a shut-down and reuses it at the next init)
-        self._say('ROCr shut down: the worker pins ROCR_VISIBLE_DEVICES=%s, '
-                  'initialised with %s' % (rocr, self.rocr))
+        self._say('ROCr shut down: the worker runs with %s (GPU %s), the '
+                  'init ran with %s (GPU %s)' % (worker, gpu, self.snapshot,
+                                                 self.gpu))
         return None
 
     @staticmethod
@@ -499,43 +522,86 @@ def _open_fds():
     return found
 
 
-def _worker_rocr(request):
-    """The ``ROCR_VISIBLE_DEVICES`` the worker of ``request`` will run with
-    (worker/pinning.py applies the ``--assign`` or ``--pin`` GPU)."""
-    from .pinning import apply_assignment_env, parse_assignment
-    env = {k: str(v) for k, v in request.get('env', {}).items()}
+def _rocr_env(env):
+    """The variables ROCr reads at ``hsa_init``."""
+    return {k: str(v) for k, v in env.items()
+            if k.startswith(('ROCR_', 'HSA_'))}
+
+
+def _request_assignment(request):
+    """The ``--assign`` (else ``--pin``) payload of a fork request."""
+    from .pinning import parse_assignment
     argv = list(request.get('argv', ()))
-    early = None
-    for flag in ('--pin', '--assign'):
+    for flag in ('--assign', '--pin'):
         if flag in argv and argv.index(flag) + 1 < len(argv):
             try:
-                early = parse_assignment(argv[argv.index(flag) + 1])
+                return parse_assignment(argv[argv.index(flag) + 1])
             except ValueError:
-                early = None
+                return None
+    return None
+
+
+def _request_gpu(request):
+    early = _request_assignment(request) or {}
+    gpu = early.get('gpu')
+    return None if gpu in (None, '') else str(gpu)
+
+
+def _worker_env(request):
+    """The environment the worker of ``request`` will run with: the
+    request's, then its assignment's template env and GPU pin
+    (worker/pinning.py), as the worker applies them before HIP starts."""
+    from .pinning import apply_assignment_env
+    env = {k: str(v) for k, v in request.get('env', {}).items()}
+    early = _request_assignment(request)
     if early:
-        apply_assignment_env({'gpu': early.get('gpu')}, env)
-    return env.get('ROCR_VISIBLE_DEVICES')
+        apply_assignment_env({'gpu': early.get('gpu'),
+                              'visible': early.get('visible'),
+                              'template': early.get('template') or {}}, env)
+    return env
 
 
 class _Embryos(object):
     """The zygote's stock of pre-forked workers (``--embryos``), of which
-    up to ``rocr`` initialise ROCr while they wait and are handed out
-    first."""
+    up to ``rocr`` initialise ROCr while they wait.  With ``gpus`` (the
+    slots' GPUs, ``--rocr-gpus``) each ROCr embryo is bound to one of them
+    and initialises ROCr for that device only; a request goes to the embryo
+    bound to its GPU, else to a plain one, else to any (which then shuts
+    its ROCr down, :meth:`_HsaPreinit.settle`)."""
 
-    def __init__(self, target, rocr=0):
+    def __init__(self, target, rocr=0, gpus=None):
         self.target = max(0, int(target))
+        self.gpus = [str(g) for g in gpus or ()]
         self.rocr = max(0, int(rocr))
-        self.ready = []             # [(pid, socket, rocr)]
+        if self.gpus:
+            self.rocr = min(self.rocr, len(self.gpus))
+        self.ready = []             # [(pid, socket, rocr)]; rocr: bool/gpu
 
     def pids(self):
         return [pid for pid, _, _ in self.ready]
 
+    def _next_rocr(self):
+        """What the next embryo initialises: False, True (unbound) or the
+        GPU whose ROCr embryo is missing."""
+        held = [r for _, _, r in self.ready if r]
+        if len(held) >= self.rocr:
+            return False
+        if not self.gpus:
+            return True
+        missing = list(self.gpus[:self.rocr])
+        for r in held:
+            if r in missing:
+                missing.remove(r)
+        return missing[0] if missing else False
+
     def make(self):
-        rocr = sum(1 for _, _, r in self.ready if r) < self.rocr
+        rocr = self._next_rocr()
+        gpu = rocr if isinstance(rocr, str) else None
         ours, theirs = socket.socketpair(socket.AF_UNIX,
                                          socket.SOCK_SEQPACKET)
         try:
-            pid = _double_fork(lambda: (ours.close(), _embryo(theirs, rocr)))
+            pid = _double_fork(lambda: (ours.close(),
+                                        _embryo(theirs, bool(rocr), gpu)))
         finally:
             theirs.close()
         if pid is None:
@@ -543,6 +609,16 @@ class _Embryos(object):
             return False
         self.ready.append((pid, ours, rocr))
         return True
+
+    def _pick(self, gpu):
+        """Index of the embryo for a request on ``gpu``."""
+        for i, (_, _, r) in enumerate(self.ready):
+            if r is True or (r and r == gpu):
+                return i           # unbound ROCr, or bound to this GPU
+        for i, (_, _, r) in enumerate(self.ready):
+            if not r:
+                return i           # a plain embryo
+        return 0                   # another GPU's: it shuts its ROCr down
 
     def top_up(self, sock):
         """Refill the stock, yielding to a waiting request."""
@@ -559,10 +635,13 @@ class _Embryos(object):
     def hand(self, payload, fds):
         """Give the request to a waiting embryo: its pid, or None (none
         left, or every one died)."""
+        gpu = None
+        try:
+            gpu = _request_gpu(json.loads(payload))
+        except (ValueError, TypeError):
+            pass
         while self.ready:
-            first = next((i for i, (_, _, r) in enumerate(self.ready) if r),
-                         0)
-            pid, esock, _ = self.ready.pop(first)
+            pid, esock, _ = self.ready.pop(self._pick(gpu))
             try:
                 socket.send_fds(esock, [payload], list(fds))
                 return pid
@@ -573,8 +652,8 @@ class _Embryos(object):
         return None
 
 
-def _serve(sock, embryos=0, rocr_embryos=0):
-    stock = _Embryos(embryos, rocr_embryos)
+def _serve(sock, embryos=0, rocr_embryos=0, rocr_gpus=None):
+    stock = _Embryos(embryos, rocr_embryos, rocr_gpus)
     reported = []
     while True:
         stock.top_up(sock)
@@ -621,6 +700,8 @@ def main(argv=None):
     parser.add_argument('--backend', default='cpu')
     parser.add_argument('--embryos', type=int, default=0)
     parser.add_argument('--rocr-embryos', type=int, default=0)
+    parser.add_argument('--rocr-gpus', default='',
+                        help='comma list: the GPU each ROCr embryo binds to')
     args = parser.parse_args(argv)
     sock = socket.socket(fileno=args.zygote_fd)
     t0 = time.monotonic()
@@ -638,7 +719,8 @@ def main(argv=None):
     signal.signal(signal.SIGCHLD, signal.SIG_DFL)
     sock.send(json.dumps({'ready': True,
                           'preload_s': time.monotonic() - t0}).encode())
-    return _serve(sock, args.embryos, args.rocr_embryos)
+    return _serve(sock, args.embryos, args.rocr_embryos,
+                  [g for g in args.rocr_gpus.split(',') if g.strip()])
 
 
 if __name__ == '__main__':

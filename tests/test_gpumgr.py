@@ -61,6 +61,74 @@ def test_pinning_env():
     assert 'HIP_VISIBLE_DEVICES' not in env
 
 
+def test_pin_modes_select_the_device():
+    """WORKER_PIN=isolate makes the worker's GPU the only
+    visible one (ordinal 0); WORKER_PIN=visible keeps every managed GPU
+    visible and selects the worker's in-process (KIOSK_DEVICE), at the ROCr
+    level too when the node filters there."""
+    from kiosk_autoscaler_amd.worker.pinning import device_ordinal
+    env = {'KIOSK_DEVICE': '3'}
+    apply_assignment_env({'gpu': '5'}, env)
+    assert env['HIP_VISIBLE_DEVICES'] == '5' and 'KIOSK_DEVICE' not in env
+    assert device_ordinal(env) == 0
+    env = {}
+    apply_assignment_env({'gpu': '5', 'visible': ['2', '3', '5', '7']}, env)
+    assert env['HIP_VISIBLE_DEVICES'] == '2,3,5,7'
+    assert env['KIOSK_DEVICE'] == '2' and device_ordinal(env) == 2
+    env = {'ROCR_VISIBLE_DEVICES': '0,1,2,3', 'HIP_VISIBLE_DEVICES': '1'}
+    apply_assignment_env({'gpu': '0', 'visible': ['0', '1', '2', '3']}, env)
+    assert env['ROCR_VISIBLE_DEVICES'] == '0,1,2,3'
+    assert 'HIP_VISIBLE_DEVICES' not in env and device_ordinal(env) == 0
+
+
+def test_manager_switches_to_visible_pin_on_a_non_p2p_peer_path():
+    """WORKER_PIN=auto: a multi-rank generation whose RCCL reports a peer
+    path other than xGMI P2P moves the manager to the visible pin: the
+    next spawns and assignments list every managed GPU, idle standbys of
+    the old pin are retired, and the event says why."""
+    from kiosk_autoscaler_amd.gpumgr.gpus import GpuSlot
+    from kiosk_autoscaler_amd.gpumgr.nodecomm import NodeComm
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    events = EventLog(source='test')
+    events.keep = True
+    slots = [GpuSlot(i, str(i)) for i in range(4)]
+    manager = gpumgr.GpuManager(slots, events=events, pin_mode='auto',
+                                pool_size=4)
+    assert manager.pin_mode == 'isolate' and manager.pin_fields() == {}
+
+    class Proc(object):
+        def __init__(self):
+            self.sent = []
+            self.pin_mode = 'isolate'
+            self.pid = 1
+            self.slot = 0
+            self.popen = type('P', (), {'poll': lambda self: None})()
+            self.pipe = type('Q', (), {'send': lambda q, m: self.sent.append(
+                m)})()
+    idle = Proc()
+    manager.standbys[0] = idle
+    manager.node = NodeComm(manager)
+    # a one-rank report never switches
+    manager.node._on_comm_info(idle, {'gen': 1, 'rank': 0, 'n': 1, 'rccl': {
+        'non_gpu_peer': ['SHM'], 'link_types': ['PHB']}})
+    assert manager.pin_mode == 'isolate'
+    manager.node._on_comm_info(idle, {'gen': 2, 'rank': 0, 'n': 8, 'rccl': {
+        'transports': {'SHM': 1}, 'non_gpu_peer': ['SHM'],
+        'link_types': ['PHB']}})
+    assert manager.pin_mode == 'visible'
+    assert manager.pin_fields() == {'visible': ['0', '1', '2', '3']}
+    assert idle.sent == [{'cmd': 'exit'}] and 0 not in manager.standbys
+    kinds = [e['ev'] for e in events.records]
+    assert 'pin_mode' in kinds and 'node_comm_info' in kinds
+    fixed = gpumgr.GpuManager(slots, pin_mode='isolate')
+    fixed.node = NodeComm(fixed)
+    fixed.node._on_comm_info(idle, {'gen': 2, 'rank': 0, 'n': 8, 'rccl': {
+        'non_gpu_peer': ['SHM']}})
+    assert fixed.pin_mode == 'isolate'
+    with pytest.raises(ValueError):
+        gpumgr.GpuManager(slots, pin_mode='bogus')
+
+
 def test_body_validation():
     assert desired_from_body('deployment', {'spec': {'replicas': '3'}}) == 3
     for body in ({}, {'spec': {'parallelism': 1}}, {'spec': {'replicas': -1}},
@@ -561,7 +629,7 @@ def test_arrival_wake_waits_for_the_lead_before_the_tick(resp_server):
         # under the 0.4 s cap)
         until(lambda: len(manager._wake_boots) == 2)
         assert manager.wake_lead() == min(0.4, max(manager._wake_boots) +
-                                          manager.WAKE_MARGIN_S)
+                                          manager.wake_margin())
         # a woken standby that serves and is recycled is timed once, not
         # again (spawn -> recycled) when it reports as a standby after it
         manager.patch_namespaced_deployment('lead', 'default',
@@ -583,19 +651,36 @@ def test_wake_lead_sizes_for_the_second_slowest_recent_boot():
     for it: the lead follows the second slowest of the last 16 woken boots
     (the slowest while fewer than 4 are known), plus the margin, capped."""
     manager = gpumgr.GpuManager([], pool_wake_lead_s=0.75)
-    margin = manager.WAKE_MARGIN_S
     assert manager.wake_lead() == 0.75               # nothing timed yet
     for boot in (0.10, 0.55):
         manager._wake_boots.append(boot)
-    assert manager.wake_lead() == pytest.approx(0.55 + margin)
+    assert manager.wake_lead() == pytest.approx(0.55 + manager.WAKE_MARGIN_S)
     for boot in (0.11, 0.09, 0.12):
         manager._wake_boots.append(boot)
-    assert manager.wake_lead() == pytest.approx(0.12 + margin)
+    assert manager.wake_lead() == pytest.approx(0.12 + manager.wake_margin())
     for _ in range(16):                  # the outlier ages out of the window
         manager._wake_boots.append(0.1)
-    assert manager.wake_lead() == pytest.approx(0.1 + margin)
+    assert manager.wake_lead() == pytest.approx(0.1 + manager.wake_margin())
     manager._wake_boots.extend([0.9, 0.9])
     assert manager.wake_lead() == 0.75               # the cap
+
+
+def test_wake_margin_follows_the_measured_spread():
+    """the margin is derived from the boots' spread --
+    tight boots (ROCr embryos) get the floor, a host whose boots scatter
+    (8 concurrent boots) a wider margin, capped -- not fixed constants."""
+    manager = gpumgr.GpuManager([], pool_wake_lead_s=0.75)
+    tight = [0.055, 0.056, 0.055, 0.057, 0.056, 0.055]
+    assert manager.wake_margin(tight) == pytest.approx(
+        manager.WAKE_MARGIN_FLOOR_S)
+    spread = [0.10, 0.11, 0.105, 0.112, 0.118, 0.16]
+    wide = manager.wake_margin(spread)
+    assert wide == pytest.approx(manager.WAKE_MARGIN_FLOOR_S +
+                                 manager.WAKE_SPREAD_K * (0.118 - 0.112))
+    assert wide > manager.wake_margin(tight)
+    assert manager.wake_margin([0.1, 0.1, 0.1, 0.4, 0.5]) == \
+        manager.WAKE_MARGIN_MAX_S
+    assert manager.wake_margin([0.1, 0.1]) == manager.WAKE_MARGIN_S
 
 
 def test_queue_reads_tighten_inside_the_wake_window():
@@ -955,11 +1040,6 @@ def test_sized_pool_retires_standbys_idle_beyond_demand():
     assert not manager._retire_excess(2, now=110.0)    # boot pool: resident
     manager.pool_parks = 1
     assert manager.wake_lead() == pytest.approx(0.12 + manager.WAKE_MARGIN_S)
-    # embryos with ROCr initialised boot tightly: the narrower margin
-    manager._rocr_embryos = 2
-    assert manager.wake_lead() == pytest.approx(
-        0.12 + manager.WAKE_MARGIN_ROCR_S)
-    manager._rocr_embryos = 0
     assert manager._retire_excess(2, now=110.0)
     # 1 (idle 1 s) then 0 (0.5 s); 2 (50 ms) and the booting 3 stay
     assert sorted(manager.standbys) == [2, 3]
@@ -1019,10 +1099,11 @@ def test_awake_sized_pool_spawns_one_lead_before_the_tick():
     assert manager._spawn_due(now)
 
 
-def test_rocr_embryos_only_for_small_hip_managers(monkeypatch):
-    """``zygote_rocr_embryos``: two on a HIP manager of one or two slots,
-    none on wider ones, none for CPU workers, none under a multi-device
-    ROCR_VISIBLE_DEVICES filter; ZYGOTE_ROCR_EMBRYOS overrides."""
+def test_rocr_embryos_one_per_gpu_slot(monkeypatch):
+    """``zygote_rocr_embryos``: one per GPU slot at
+    every slot count, bound to that slot's GPU (worker/zygote.py), none for
+    CPU workers, a multi-device ROCR_VISIBLE_DEVICES filter included (each
+    embryo re-binds to its slot's device); ZYGOTE_ROCR_EMBRYOS overrides."""
     from kiosk_autoscaler_amd.gpumgr import gpus, pool
 
     class _Tpl(object):
@@ -1038,12 +1119,10 @@ def test_rocr_embryos_only_for_small_hip_managers(monkeypatch):
     monkeypatch.delenv('ZYGOTE_ROCR_EMBRYOS', raising=False)
     monkeypatch.delenv('ZYGOTE_EMBRYOS', raising=False)
     monkeypatch.delenv('ROCR_VISIBLE_DEVICES', raising=False)
-    assert rocr(1) == 1 and rocr(2) == 2 and rocr(8) == 0
+    assert rocr(1) == 1 and rocr(2) == 2 and rocr(8) == 8
     assert rocr(1, backend='cpu') == 0 and rocr(2, kind='cpu') == 0
-    monkeypatch.setenv('ROCR_VISIBLE_DEVICES', '0')
-    assert rocr(1) == 1
     monkeypatch.setenv('ROCR_VISIBLE_DEVICES', '0,1')
-    assert rocr(2) == 0
+    assert rocr(2) == 2
     monkeypatch.delenv('ROCR_VISIBLE_DEVICES')
     monkeypatch.setenv('ZYGOTE_ROCR_EMBRYOS', '3')
     assert rocr(8) == 3 and rocr(1) == 1

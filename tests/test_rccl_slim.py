@@ -288,6 +288,74 @@ def test_sanitized_slim_survives_malformed_libraries(tmp_path, asan_tool,
                                          proc.stderr[-2000:])
 
 
+def _code_object_corruptions(code):
+    """Corrupted copies of a gfx950 code object (the debug
+    stripper trusted the object's program-header, section and name
+    offsets)."""
+    shoff, = struct.unpack_from('<Q', code, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from('<HHH', code, 0x3a)
+
+    def patched(offset, fmt, value):
+        blob = bytearray(code)
+        struct.pack_into(fmt, blob, offset, value)
+        return bytes(blob)
+    names, secs = _sections_of(code)
+    debug = next(i for i, n in enumerate(names) if n.startswith('.debug'))
+    sec = shoff + debug * shentsize
+    strsec = shoff + shstrndx * shentsize
+    return {
+        'phoff_past_end': patched(0x20, '<Q', len(code) + 4096),
+        'phnum_huge': patched(0x38, '<H', 0xfff0),
+        'section_offset_past_end': patched(sec + 0x18, '<Q', 1 << 40),
+        'section_size_huge': patched(sec + 0x20, '<Q', 1 << 40),
+        'section_name_past_strtab': patched(sec, '<I', 0xffffff00),
+        'strtab_size_huge': patched(strsec + 0x20, '<Q', 1 << 40),
+    }
+
+
+def test_sanitized_slim_refuses_corrupted_code_objects(tmp_path, asan_tool):
+    """The gfx950 code object itself corrupted: the stripper refuses it
+    (exit 2) without an out-of-bounds read under ASan+UBSan."""
+    tmp = str(tmp_path)
+    code = _code_object(tmp, 'k950', 5)
+    env = dict(os.environ, ASAN_OPTIONS='detect_leaks=1:exitcode=99',
+               UBSAN_OPTIONS='halt_on_error=1:exitcode=98')
+    for name, blob in _code_object_corruptions(code).items():
+        bundle = _bundle([('host-x86_64-unknown-linux-gnu-', b''),
+                          ('hipv4-amdgcn-amd-amdhsa--gfx950', blob)])
+        sub = os.path.join(tmp, name)
+        os.makedirs(sub)
+        lib = _library(sub, bundle, slack=len(bundle))
+        proc = subprocess.run([asan_tool, '--src', lib, '--out',
+                               os.path.join(sub, 'out.so')], env=env,
+                              capture_output=True, text=True, timeout=120)
+        assert 'Sanitizer' not in proc.stderr, (name, proc.stderr[-3000:])
+        # a name past the string table reads as empty (bounded): that
+        # section is kept, the object is still slimmed
+        want = 0 if name == 'section_name_past_strtab' else 2
+        assert proc.returncode == want, (name, proc.returncode,
+                                         proc.stderr[-2000:])
+
+
+def test_slim_cache_key_follows_the_tool(tmp_path, tool):
+    """a copy written by an earlier build of the tool is not
+    loaded after the tool changes (its content hash is in the key)."""
+    import shutil
+    tmp = str(tmp_path)
+    other = os.path.join(tmp, 'tool-copy')
+    shutil.copy(tool, other)
+    lib = os.path.join(tmp, 'lib.so')
+    with open(lib, 'wb') as f:
+        f.write(b'x')
+    same = rccl_lib.slim_dir(lib, tool=other) == rccl_lib.slim_dir(lib,
+                                                                    tool=tool)
+    assert same
+    with open(other, 'ab') as f:
+        f.write(b'rebuilt')
+    assert rccl_lib.slim_dir(lib, tool=other) != rccl_lib.slim_dir(lib,
+                                                                    tool=tool)
+
+
 def test_slim_refuses_a_bundle_without_the_isa(tmp_path, tool):
     tmp = str(tmp_path)
     bundle = _bundle([('host-x86_64-unknown-linux-gnu-', b''),

@@ -283,7 +283,10 @@ class _FakeHsa(object):
         return 0
 
 
-def _settled(monkeypatch, zygote_rocr, argv, env, delay=0.0):
+def _settled(monkeypatch, zygote_rocr, argv, env, delay=0.0, gpu=None):
+    """An embryo's ROCr init under the zygote's environment, then its
+    hand-off of a request whose env is the manager's (the zygote's, as
+    ``_spawn`` passes it) with ``env`` on top."""
     from kiosk_autoscaler_amd.worker import zygote
     lib = _FakeHsa()
     monkeypatch.setattr('ctypes.CDLL', lambda *a, **k: lib)
@@ -291,43 +294,106 @@ def _settled(monkeypatch, zygote_rocr, argv, env, delay=0.0):
         monkeypatch.delenv('ROCR_VISIBLE_DEVICES', raising=False)
     else:
         monkeypatch.setenv('ROCR_VISIBLE_DEVICES', zygote_rocr)
+    request_env = {k: v for k, v in os.environ.items()
+                   if k != 'ROCR_VISIBLE_DEVICES'}
+    request_env.update(env)
     pre = zygote._HsaPreinit()
     pre.DELAY_S = delay
-    pre.start()
+    pre.start(gpu)
+    if gpu is not None:
+        # (the embryo process binds itself: undo it for the next test)
+        monkeypatch.setenv('ROCR_VISIBLE_DEVICES', str(gpu))
     if delay == 0.0:
         pre.thread.join()
-    stamp = pre.settle({'argv': argv, 'env': env})
-    return stamp, lib.calls
+    request = {'argv': argv, 'env': request_env}
+    stamp = pre.settle(request)
+    return stamp, lib.calls, request
 
 
 def test_embryo_keeps_rocr_when_the_pin_matches(monkeypatch):
     """The 1-GPU box: ROCR_VISIBLE_DEVICES=0 and the worker pins GPU 0."""
-    stamp, calls = _settled(monkeypatch, '0',
-                            ['--pin', '{"gpu": 0}'],
-                            {'ROCR_VISIBLE_DEVICES': '0'})
+    stamp, calls, _ = _settled(monkeypatch, '0',
+                               ['--pin', '{"gpu": 0}'],
+                               {'ROCR_VISIBLE_DEVICES': '0'})
     assert calls == ['init'] and isinstance(stamp, int)
 
 
 def test_embryo_keeps_rocr_under_hip_level_pinning(monkeypatch):
     # ROCR unset: the pin is HIP_VISIBLE_DEVICES, applied at hipInit
-    stamp, calls = _settled(monkeypatch, None,
-                            ['--pin', '{"gpu": 5}'], {})
+    stamp, calls, _ = _settled(monkeypatch, None,
+                               ['--pin', '{"gpu": 5}'], {})
     assert calls == ['init'] and stamp is not None
 
 
 def test_embryo_shuts_rocr_down_when_the_pin_differs(monkeypatch):
     """A node filtering at the ROCr level: the worker's GPU 3 re-filters
     ROCR_VISIBLE_DEVICES, which the early init would have missed."""
-    stamp, calls = _settled(monkeypatch, '0,1,2,3',
-                            ['--pin', '{"gpu": 1}', '--assign',
-                             '{"gpu": 3}'],
-                            {'ROCR_VISIBLE_DEVICES': '0,1,2,3'})
+    stamp, calls, _ = _settled(monkeypatch, '0,1,2,3',
+                               ['--pin', '{"gpu": 1}', '--assign',
+                                '{"gpu": 3}'],
+                               {'ROCR_VISIBLE_DEVICES': '0,1,2,3'})
     assert calls == ['init', 'shut_down'] and stamp is None
 
 
 def test_embryo_request_before_the_delay_skips_the_init(monkeypatch):
-    stamp, calls = _settled(monkeypatch, None, [], {}, delay=30.0)
+    stamp, calls, _ = _settled(monkeypatch, None, [], {}, delay=30.0)
     assert calls == [] and stamp is None
+
+
+def test_slot_bound_embryo_keeps_rocr_for_its_gpu(monkeypatch):
+    """an embryo bound to GPU 6 initialises ROCr with
+    ROCR_VISIBLE_DEVICES=6 (that device alone); a worker for GPU 6 keeps
+    the init and pins at the ROCr level too."""
+    stamp, calls, request = _settled(monkeypatch, None,
+                                     ['--pin', '{"gpu": "6"}'], {}, gpu='6')
+    assert calls == ['init'] and stamp is not None
+    assert request['env']['ROCR_VISIBLE_DEVICES'] == '6'
+    from kiosk_autoscaler_amd.worker.zygote import _worker_env
+    worker = _worker_env(request)
+    assert worker['ROCR_VISIBLE_DEVICES'] == '6'
+    assert 'HIP_VISIBLE_DEVICES' not in worker
+
+
+def test_slot_bound_embryo_of_another_gpu_is_shut_down(monkeypatch):
+    """A slot-bound embryo handed a request for another GPU shuts its
+    ROCr down instead of keeping a runtime that opened the wrong device."""
+    stamp, calls, request = _settled(monkeypatch, None,
+                                     ['--pin', '{"gpu": "2"}'], {}, gpu='6')
+    assert calls == ['init', 'shut_down'] and stamp is None
+    assert 'ROCR_VISIBLE_DEVICES' not in request['env']
+
+
+def test_embryo_of_another_template_shuts_rocr_down(monkeypatch):
+    """an HSA_* setting the assignment's template env changes
+    (SDMA off here) was silently ignored by a kept init."""
+    import json
+    assign = {'gpu': '6', 'template': {'env': {'HSA_ENABLE_SDMA': '0'}}}
+    stamp, calls, _ = _settled(monkeypatch, None,
+                               ['--assign', json.dumps(assign)], {},
+                               gpu='6')
+    assert calls == ['init', 'shut_down'] and stamp is None
+
+
+def test_requests_go_to_the_embryo_bound_to_their_gpu(monkeypatch):
+    import json
+    from kiosk_autoscaler_amd.worker import zygote
+    made = []
+    monkeypatch.setattr(zygote, '_double_fork',
+                        lambda body: made.append(len(made) + 200) or made[-1])
+    stock = zygote._Embryos(4, rocr=2, gpus=['0', '1'])
+    for _ in range(4):
+        assert stock.make()
+    assert [r for _, _, r in stock.ready] == ['0', '1', False, False]
+    monkeypatch.setattr('socket.send_fds', lambda sock, bufs, fds: None)
+
+    def req(gpu):
+        return json.dumps({'argv': ['--pin', json.dumps({'gpu': gpu})],
+                           'env': {}}).encode()
+    assert stock.hand(req('1'), []) == 201      # bound to GPU 1
+    assert stock.hand(req('5'), []) == 202      # no GPU 5 embryo: a plain one
+    stock.make()                                 # GPU 1's replacement
+    assert [r for _, _, r in stock.ready] == ['0', False, '1']
+    assert stock.hand(req('1'), []) == 204
 
 
 def test_rocr_embryos_are_made_up_to_the_cap_and_handed_first(monkeypatch):
@@ -411,3 +477,25 @@ def test_pull_error_does_not_crash_the_worker(redis_client, monkeypatch):
     assert run.run() == 0
     assert len(calls) == 2
     assert [e for e, _ in channel.events].count('pull_error') == 2
+
+
+def test_channel_cap_is_decided_without_importing_the_plugin(monkeypatch,
+                                                              tmp_path):
+    """deciding the RCCL channel cap must not import a user
+    plug-in (its module-level imports would run before the GPU pin)."""
+    import sys
+    from kiosk_autoscaler_amd.worker import main as worker_main
+    mod = tmp_path / 'sideeffect_plugin.py'
+    mod.write_text('import os\nos.environ["PLUGIN_IMPORTED"] = "1"\n'
+                   'def factory(cfg, stage=None):\n    return None\n')
+    monkeypatch.syspath_prepend(str(tmp_path))
+    monkeypatch.delenv('PLUGIN_IMPORTED', raising=False)
+    monkeypatch.setenv('WORKER_ENGINE', 'sideeffect_plugin:factory')
+    assert worker_main._engine_collectives() is True
+    assert 'PLUGIN_IMPORTED' not in os.environ
+    assert 'sideeffect_plugin' not in sys.modules
+    monkeypatch.setenv('WORKER_ENGINE', 'kiosk_autoscaler_amd.models.'
+                       'torch_kiosk:TorchKioskEngine')
+    assert worker_main._engine_collectives() is False
+    monkeypatch.delenv('WORKER_ENGINE')
+    assert worker_main._engine_collectives() is False

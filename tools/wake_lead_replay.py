@@ -47,6 +47,18 @@ def second_slowest(window, min_samples=4):
     return est
 
 
+def spread_margin(k=3.0, floor=0.01, hi=0.06, window=16):
+    """gpumgr/pool.py ``wake_lead`` since round 6: second slowest of the
+    window plus ``floor + k * (second slowest - median)``, clamped."""
+    def est(hist):
+        recent = sorted(hist[-window:])
+        if len(recent) < 4:
+            return recent[-1] + 0.05
+        sized, median = recent[-2], recent[len(recent) // 2]
+        return sized + min(hi, max(floor, floor + k * (sized - median)))
+    return est
+
+
 ESTIMATORS = {
     'slowest of 8': slowest(8),
     'slowest of 16': slowest(16),
@@ -89,6 +101,12 @@ def main(argv=None):
         with open(args.dump, 'w') as fh:
             json.dump({'runs': runs}, fh)
     print('%d runs, %d woken boots' % (len(runs), sum(map(len, runs))))
+    for k in (1.0, 2.0, 3.0):
+        row = replay(runs, spread_margin(k), 0.0)
+        print('second slowest of 16 + spread margin (k=%g): late %5.2f '
+              'ms/wake (%d of %d), hold %5.1f ms/wake' % (
+                  k, row['late_ms_per_wake'], row['late_wakes'],
+                  row['wakes'], row['hold_ms_per_wake']))
     for name, est in ESTIMATORS.items():
         for margin in (0.03, 0.04, 0.05):
             row = replay(runs, est, margin)
