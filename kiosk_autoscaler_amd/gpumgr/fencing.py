@@ -165,21 +165,29 @@ class FencingMixin(object):
         (fence_wanted stays set) while a generation is being built or
         shrunk, another resource's epoch is in flight, or a member runs on a
         process that is not a rank yet (a replacement awaiting the regrow)."""
-        if not resource.fence_wanted or not self.node.ready or \
-                self.node.inflight is not None:
+        if not resource.fence_wanted:
             return
         members = sorted((w.id for w in resource.ready()),
                          key=lambda wid: resource.workers[wid].slot.index)
+        inflight = self.node.inflight
+        if not members and (inflight is None or
+                            inflight['resource'] is not resource):
+            # nobody left to agree with: the empty set is published at
+            # once, whether or not a communicator exists (a deep-idle pool
+            # retires the last worker's process right after its drain)
+            resource.fence_wanted = False
+            if resource.fenced_members:
+                resource.fenced_members = []
+                resource.fenced_epoch = resource.epoch
+                self._publish_active(resource)
+            return
+        if not self.node.ready or inflight is not None:
+            return
         if not self.node.can_fence([resource.workers[wid].proc
                                     for wid in members]):
             return
         resource.fence_wanted = False
         if members == resource.fenced_members:
-            return
-        if not members:
-            resource.fenced_members = []
-            resource.fenced_epoch = resource.epoch
-            self._publish_active(resource)
             return
         self.node.fence(resource, members)
 

@@ -854,6 +854,7 @@ class PoolMixin(object):
         proc.recycles += 1
         if (self._recycle_ok(resource) and slot.index not in self.standbys
                 and len(self.standbys) < self.pool_size and
+                not self._parks_on_recycle() and
                 getattr(proc, 'pin_mode', 'isolate') ==
                 getattr(self, 'pin_mode', 'isolate') and
                 not getattr(proc, 'node_quarantined', False)):
@@ -870,6 +871,23 @@ class PoolMixin(object):
             # its GPU is held until the process is gone (standby_exit)
             self.events.emit('worker_retired', worker=worker.id,
                              gpu=slot.index, pid=proc.pid)
+
+    # a release delay this short is the deep-idle default (0.01 s): the
+    # drained worker would be parked before anything could assign it
+    PARK_AT_ONCE_S = 0.05
+
+    def _parks_on_recycle(self):
+        """A drained worker comes back when deep idle would park the pool
+        on this very pass (no resource declares or runs a worker, no
+        arrival's wake is held): it is retired at once instead of kept as a
+        standby for ``POOL_IDLE_RELEASE_S`` first -- its exit starts ~10 ms
+        earlier on every wake (standby time)."""
+        if not 0 < self.pool_idle_release_s <= self.PARK_AT_ONCE_S or \
+                time.monotonic() < self._wake_until:
+            return False
+        return not any(r.declared > 0 or any(w.state != EXITED
+                                             for w in r.workers.values())
+                       for r in self.resources.values())
 
     ORPHAN_SCAN_S = 5.0
 

@@ -593,13 +593,14 @@ from kiosk_autoscaler_amd.worker import zygote
 mod = native.load()
 pre = zygote._HsaPreinit()
 pre.DELAY_S = 0.0
-pre.start()
+request_env = dict(os.environ)
+pre.start('0')                      # bound to GPU 0: ROCR_VISIBLE_DEVICES=0
 pre.thread.join()
 inited = pre.lib is not None
 if sys.argv[1] == 'shut':
-    pre.rocr = 'another pin'        # the worker's pin differs: shut down
-stamp = pre.settle({'argv': ['--pin', '{"gpu": 0}'],
-                    'env': dict(os.environ)})
+    # the worker's ROCr settings differ from the init's: shut down
+    request_env['HSA_KIOSK_TEST_SETTING'] = 'another'
+stamp = pre.settle({'argv': ['--pin', '{"gpu": 0}'], 'env': request_env})
 for fd in range(3, 1024):               # as zygote._child does
     if fd not in pre.fds:
         try:

@@ -1150,3 +1150,25 @@ def test_idle_pool_sets_its_park_instant_for_the_loop():
     assert manager._park_at is None
     manager._park_pool()
     assert manager._park_at is None
+
+
+def test_drained_worker_retires_at_once_when_the_pool_parks_anyway():
+    """with the deep-idle default (0.01 s) a worker
+    drained by the scale to zero is retired at once instead of kept as a
+    standby until the park; a longer POOL_IDLE_RELEASE_S, a held wake or
+    remaining demand keep it."""
+    manager = gpumgr.GpuManager([], pool_idle_release_s=0.01)
+    assert manager._parks_on_recycle()
+    tpl = gpumgr.WorkerTemplate(queues=['q'], backend='cpu')
+    manager.register('deployment', 'ns', 'w', tpl)
+    assert manager._parks_on_recycle()
+    manager.resources[('deployment', 'ns', 'w')].declared = 1
+    assert not manager._parks_on_recycle()
+    manager.resources[('deployment', 'ns', 'w')].declared = 0
+    manager._wake_until = time.monotonic() + 5.0
+    assert not manager._parks_on_recycle()
+    manager._wake_until = 0.0
+    assert not gpumgr.GpuManager([], pool_idle_release_s=0.3)\
+        ._parks_on_recycle()
+    assert not gpumgr.GpuManager([], pool_idle_release_s=0)\
+        ._parks_on_recycle()
