@@ -141,7 +141,7 @@ __device__ __forceinline__ void mfma_drain() {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 }
 
-// Diagnostic builds only (tools/gemm_ablate.hip): bit 0 drops the 4-wave
+// Diagnostic builds only (tools/probes/gemm_ablate.hip): bit 0 drops the 4-wave
 // kernel's in-loop DMA, bit 1 its in-loop LDS reads.  Results are wrong in such builds; 0 in the product.
 #ifndef KIOSK_GEMM_ABLATE
 #define KIOSK_GEMM_ABLATE 0
@@ -168,7 +168,7 @@ __device__ __forceinline__ void mfma_drain() {
 #ifndef KIOSK_W4_STAGGER_SEL
 #define KIOSK_W4_STAGGER_SEL 1     // 0: odd waves lag; 1: waves 2, 3 lag
 #endif
-// Experiment (tools/gemm_ablate.hip A/B, off in the product): stage the
+// Experiment (tools/probes/gemm_ablate.hip A/B, off in the product): stage the
 // k-loop's operand pieces through VGPRs -- buffer_load_dwordx4 into
 // registers in half-step h, ds_write_b128 into the ring in half-step h + 1 --
 // instead of LDS-DMA, whose issue holds the wave ~60 cycles among MFMAs.

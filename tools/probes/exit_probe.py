@@ -22,7 +22,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 CASES = ('ctx', 'engine', 'engine_rccl', 'engine_free', 'torch_engine_rccl',

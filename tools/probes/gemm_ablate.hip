@@ -2,7 +2,7 @@
 // removed (-DKIOSK_GEMM_ABLATE=<bits>, see gemm256.hip).  Numerics are
 // meaningless in ablated builds; only the timing is reported.
 //   hipcc -O3 --offload-arch=gfx950 -DKIOSK_GEMM_ABLATE=1 \
-//     -I csrc/kernels tools/gemm_ablate.hip -o build/gemm_ablate_1
+//     -I csrc/kernels tools/probes/gemm_ablate.hip -o build/gemm_ablate_1
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -10,7 +10,7 @@
 #include <cstring>
 #include <vector>
 
-#include "../csrc/kernels/gemm256.hip"
+#include "../../csrc/kernels/gemm256.hip"
 
 #define CHECK(x)                                                      \
   do {                                                                \

@@ -14,7 +14,7 @@
 // the only thing competing with the MFMAs.
 //
 //   hipcc -O3 --offload-arch=gfx950 -I csrc/kernels \
-//     tools/mfma_dma_probe.hip -o build/mfma_dma_probe
+//     tools/probes/mfma_dma_probe.hip -o build/mfma_dma_probe
 //   build/mfma_dma_probe [steps]
 #include <hip/hip_runtime.h>
 #include <stdio.h>

@@ -16,8 +16,8 @@ def stages(t0, dim=4096, hidden=16384, layers=4, rows=2048):
     torch.zeros(1, device='cuda')
     torch.cuda.synchronize()
     out['cuda_ready'] = time.perf_counter() - t0
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(
-        __file__))))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__)))))
     from kiosk_autoscaler_amd.models.torch_engine import TorchMlpEngine
 
     class Cfg(object):

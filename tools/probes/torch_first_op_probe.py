@@ -16,7 +16,7 @@ import subprocess
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 ORDERS = ['h2d,graph,d2h,event', 'graph,h2d,d2h,event',
           'event,h2d,graph,d2h', 'd2h,h2d,graph,event']
 
