@@ -8,6 +8,10 @@
 #                                                  the driver's bench command
 #                                                  once per env variant
 #   tools/gpu_run.sh round  TAG STEPS WARMUP [...] tests, then bench
+#   tools/gpu_run.sh args   TAG STEPS WARMUP NAME -- BENCH_ARGS..
+#                                                  the driver's bench command
+#                                                  plus bench arguments (the
+#                                                  opt-in modes), one variant
 #   tools/gpu_run.sh slots  TAG N STEPS -- BENCH_ARGS..
 #                                                  N worker slots on the one
 #                                                  device (BENCH_GPU_IDS)
@@ -69,6 +73,14 @@ case $recipe in
     run_tests; rc=$?
     fatal $rc && { echo "stopping after the GPU tests ($rc)"; exit $rc; }
     run_bench "$steps" "$warmup" "$@" ;;
+  args)
+    steps=$1; warmup=$2; name=$3; shift 4    # (the -- separator)
+    dir=$out/$name; mkdir -p "$dir"
+    KIOSK_BENCH_OUT=$dir timeout -k 10 560 python -u bench.py --gpus 1 \
+      --steps "$steps" --warmup "$warmup" --budget-s 520 "$@" \
+      > "$dir/bench.json" 2> "$dir/bench.err" \
+      || { rc=$?; tail -30 "$dir/bench.err"; exit $rc; }
+    tail -1 "$dir/bench.json" | cut -c1-400 ;;
   slots)
     n=$1; steps=$2; shift 3            # (the -- separator)
     ids=$(python3 -c "print(','.join(['0'] * $n))")
