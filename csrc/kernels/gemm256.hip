@@ -175,6 +175,11 @@ __device__ __forceinline__ void mfma_drain() {
 #ifndef KIOSK_W4_REGSTAGE
 #define KIOSK_W4_REGSTAGE 0
 #endif
+// gemm256p_kernel: the MFMA index at which waves 4-7 start their DMA
+// issues within a half-step (waves 0-3 start at 0)
+#ifndef KIOSK_PAIR_STAGGER
+#define KIOSK_PAIR_STAGGER 12
+#endif
 
 // Counted waits go through the builtin (not inline asm) so hipcc's waitcnt
 // pass sees them and adds no conservative lgkmcnt(0) of its own.  gfx9
@@ -1058,6 +1063,258 @@ hipError_t launch_m32(const uint16_t* A, const uint16_t* B, uint16_t* C,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Two waves per SIMD (gemm_set_pair): the 4-wave
+// kernel's 256x256 tile, ring, swizzle and counted waits with 8 waves of
+// 128x64 outputs each (2 x 4 waves, 8 x 4 tiles of v_mfma_f32_16x16x32_bf16,
+// 128 AGPRs).  The 4-wave kernel loses ~20 % of the matrix pipe to its own
+// LDS-DMA issue: one wave per SIMD has nothing to run while its DMA issue
+// holds it (profiles/r4_mfma_dma, the ablation's +21 % without in-loop
+// DMA).  Here a wave issues half the DMA pieces (4 per half-step) and its
+// SIMD partner's MFMAs run while it is held.  The partners are staggered
+// (waves 4-7 issue their DMA later in the half-step, MI355X_MICROARCH.md
+// "Two waves per SIMD" item 9) so they are not both held at once.  LDS
+// reads per CU rise from 64 to 96 KiB per half-step (384 of the 1024
+// cycles at 256 B/clk) -- within the array's budget.
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256p_kernel(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+    uint16_t* __restrict__ C, const float* __restrict__ bias,
+    const uint16_t* __restrict__ R, int M, int N, int K, int lda,
+    int group_m) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TM = 8, TN = 4;            // 16x16 tiles per wave
+  const int split = static_cast<int>(blockIdx.y);
+  A += static_cast<size_t>(split) * K;
+  B += static_cast<size_t>(split) * K;
+  const int tiles_n = N / 256;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int ntiles = tiles_m * tiles_n;
+  int m0 = 0, n0 = 0;
+  {
+    const int wg = xcd_remap(static_cast<int>(blockIdx.x), ntiles);
+    const int per_group = group_m * tiles_n;
+    const int group = wg / per_group;
+    const int first_m = group * group_m;
+    const int gsize = min(tiles_m - first_m, group_m);
+    const int in_group = wg - group * per_group;
+    m0 = (first_m + in_group % gsize) * BM;
+    n0 = (in_group / gsize) * 256;
+  }
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int lane = static_cast<int>(threadIdx.x & 63);
+  constexpr int kUnit = BM * 128;
+  const int steps = K / 64;
+  f32x4 acc[TM][TN];
+
+  // a group (one operand of one 64-deep step) is 32 pieces of 8 rows x
+  // 128 B; wave w issues pieces 4w .. 4w + 3 (the 4-wave kernel's LDS image)
+  int voff_a[4], voff_b[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = (wave * 4 + p) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int ra = m0 + r < M ? m0 + r : M - 1;
+    const int rb = n0 + r < N ? n0 + r : N - 1;
+    voff_a[p] = (ra * lda + c * 8) * 2;
+    voff_b[p] = (rb * lda + c * 8) * 2;
+  }
+  const auto rsrc_a = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(A), 0, 0x7fffffff, 0x00020000);
+  const auto rsrc_b = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(B), 0, 0x7fffffff, 0x00020000);
+  auto dma = [&](int g, int p) {
+    const int t = min(g >> 1, steps - 1);
+    char* lds = smem + (g % 5) * kUnit + (wave * 4 + p) * 1024;
+    if (g & 1)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_b, (lds_void_t*)lds, 16,
+                                               voff_b[p], t * 128, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_a, (lds_void_t*)lds, 16,
+                                               voff_a[p], t * 128, 0, 0);
+  };
+  const int fr = lane & 15;
+  const int sw = (fr >> 1) & 7;
+  const int lane_a = (wm * 128 + fr) * 128, lane_b = (wn * 64 + fr) * 128;
+  const int lane_a0 = lane_a + (((lane >> 4) ^ sw) << 4);
+  const int lane_a1 = lane_a + (((4 + (lane >> 4)) ^ sw) << 4);
+  const int lane_b0 = lane_b + (((lane >> 4) ^ sw) << 4);
+  const int lane_b1 = lane_b + (((4 + (lane >> 4)) ^ sw) << 4);
+  // fragment r of half h: r < TN -> B tile r, else A tile r - TN
+  auto read = [&](auto hh, int t, int r, bf16x8 (&wb)[TN],
+                  bf16x8 (&xa)[TM]) {
+    constexpr bool kHi = decltype(hh)::value != 0;
+    if (r < TN) {
+      const char* base = smem + __builtin_amdgcn_readfirstlane(
+                                    ((2 * t + 1) % 5) * kUnit) +
+                         (kHi ? lane_b1 : lane_b0);
+      wb[r] = *reinterpret_cast<const bf16x8*>(base + r * 2048);
+    } else {
+      const char* base = smem + __builtin_amdgcn_readfirstlane(
+                                    ((2 * t) % 5) * kUnit) +
+                         (kHi ? lane_a1 : lane_a0);
+      xa[r - TN] = *reinterpret_cast<const bf16x8*>(base + (r - TN) * 2048);
+    }
+  };
+  // half-step h = 2t + odd: 32 MFMAs; the 4 DMA pieces of group h + 4 at
+  // MFMAs kOff + 0, 5, 10, 15 (waves 4-7 later than 0-3); the 12 reads of
+  // half h + 1 in the first 24 MFMAs (every other one)
+  auto half = [&](auto first, auto odd, auto off, int t,
+                  const bf16x8 (&wb)[TN], const bf16x8 (&xa)[TM],
+                  bf16x8 (&wb_next)[TN], bf16x8 (&xa_next)[TM]) {
+    constexpr bool kOdd = decltype(odd)::value;
+    constexpr int kOff = decltype(off)::value;
+    const int h = 2 * t + kOdd;
+    __builtin_amdgcn_sched_barrier(0);
+    // (lgkmcnt 0 too: every LDS read of this wave has returned before
+    // the barrier lets another wave's DMA reuse a unit)
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(kOdd ? 4 : 8));
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const int tn = kOdd ? t + 1 : t;
+    using HH = std::integral_constant<int, kOdd ? 0 : 1>;
+#pragma unroll
+    for (int u = 0; u < TM * TN; ++u) {
+      if constexpr (decltype(first)::value)
+        mfma_agpr_first(acc[u / TN][u % TN], wb[u % TN], xa[u / TN]);
+      else
+        mfma_agpr(acc[u / TN][u % TN], wb[u % TN], xa[u / TN]);
+      if (u >= kOff && (u - kOff) % 5 == 0 && (u - kOff) < 20)
+        dma(h + 4, (u - kOff) / 5);
+      if (u % 2 == 0 && u < 24) read(HH(), tn, u / 2, wb_next, xa_next);
+    }
+  };
+  auto mainloop = [&](auto off) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) dma(g, p);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(8));
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 wb0[TN], xa0[TM], wb1[TN], xa1[TM];
+#pragma unroll
+    for (int r = 0; r < TM + TN; ++r)
+      read(std::integral_constant<int, 0>(), 0, r, wb0, xa0);
+    half(std::true_type(), std::false_type(), off, 0, wb0, xa0, wb1, xa1);
+    half(std::false_type(), std::true_type(), off, 0, wb1, xa1, wb0, xa0);
+    for (int t = 1; t < steps; ++t) {
+      half(std::false_type(), std::false_type(), off, t, wb0, xa0, wb1, xa1);
+      half(std::false_type(), std::true_type(), off, t, wb1, xa1, wb0, xa0);
+    }
+  };
+  if (wave >= 4)
+    mainloop(std::integral_constant<int, KIOSK_PAIR_STAGGER>());
+  else
+    mainloop(std::integral_constant<int, 0>());
+  // drain the tail DMAs before the workgroup's LDS can be released
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  mfma_drain();
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" : "+a"(acc[i][j]));
+
+  // Epilogue: the 4-wave kernel's (lane l: row l & 15, columns 4(l >> 4)..
+  // +3 of each 16x16 tile; v_permlane16_swap pairs -> 16-B stores)
+  auto pack2 = [](float lo, float hi) {
+    return f32_to_bf16(lo) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
+  };
+  const int g = lane >> 4;
+  const bool odd = (g & 1) != 0;
+  auto finish = [&](int m, int nb, const f32x4& a, float (&v)[4]) {
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    if (EPI != EPI_NONE) {
+      const float4 b = *reinterpret_cast<const float4*>(bias + nb);
+      v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+    }
+    if (EPI == EPI_BIAS_GELU) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+    }
+    if (EPI == EPI_BIAS_RESIDUAL) {
+      const uint2 res = *reinterpret_cast<const uint2*>(
+          R + static_cast<size_t>(m) * N + nb);
+      v[0] += bf16_to_f32(res.x & 0xffff);
+      v[1] += bf16_to_f32(res.x >> 16);
+      v[2] += bf16_to_f32(res.y & 0xffff);
+      v[3] += bf16_to_f32(res.y >> 16);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (TM * 16) + i * 16 + (lane & 15);
+    if (m >= M) continue;
+    if (EPI == EPI_PARTIAL) {
+      float* P = reinterpret_cast<float*>(C) +
+                 static_cast<size_t>(split) * M * N;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nb = n0 + wn * (TN * 16) + j * 16 + g * 4;
+        *reinterpret_cast<float4*>(P + static_cast<size_t>(m) * N + nb) =
+            float4{acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      continue;
+    }
+#pragma unroll
+    for (int jp = 0; jp < TN; jp += 2) {
+      const int base = n0 + wn * (TN * 16) + jp * 16;
+      float v0[4], v1[4];
+      finish(m, base + g * 4, acc[i][jp], v0);
+      finish(m, base + 16 + g * 4, acc[i][jp + 1], v1);
+      const auto x0 = __builtin_amdgcn_permlane16_swap(
+          pack2(v0[0], v0[1]), pack2(v1[0], v1[1]), false, false);
+      const auto x1 = __builtin_amdgcn_permlane16_swap(
+          pack2(v0[2], v0[3]), pack2(v1[2], v1[3]), false, false);
+      const uint4 out = uint4{x0[0], x1[0], x0[1], x1[1]};
+      const int col = odd ? base + 16 + (g - 1) * 4 : base + g * 4;
+      *reinterpret_cast<uint4*>(C + static_cast<size_t>(m) * N + col) = out;
+    }
+    // one row of tiles at a time: bounds the AGPR -> VGPR copies
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// 0: one wave per SIMD (gemm256_kernel<., 256, 4>); 1: gemm256p_kernel
+// wherever the 4-wave one-tile kernel runs
+int g_pair = 0;
+
+template <int EPI>
+hipError_t configure_pair() {
+  hipError_t err = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&gemm256p_kernel<EPI>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256, 4>::kLdsBytes);
+  return err == hipSuccess ? prepare_kernel(&gemm256p_kernel<EPI>) : err;
+}
+
+hipError_t launch_pair(const uint16_t* A, const uint16_t* B, uint16_t* C,
+                       const float* bias, const uint16_t* R, int M, int N,
+                       int K, int lda, int splits, int epilogue,
+                       hipStream_t stream) {
+  const int blocks = ((M + BM - 1) / BM) * (N / 256);
+  const dim3 grid(blocks, splits), block(512);
+  constexpr int lds = Geo<256, 4>::kLdsBytes;
+  switch (epilogue) {
+    case EPI_NONE:
+      return launch_kernel(&gemm256p_kernel<EPI_NONE>, grid, block, lds,
+                           stream, A, B, C, bias, R, M, N, K, lda, g_group_m);
+    case EPI_BIAS_GELU:
+      return launch_kernel(&gemm256p_kernel<EPI_BIAS_GELU>, grid, block, lds,
+                           stream, A, B, C, bias, R, M, N, K, lda, g_group_m);
+    case EPI_BIAS_RESIDUAL:
+      return launch_kernel(&gemm256p_kernel<EPI_BIAS_RESIDUAL>, grid, block,
+                           lds, stream, A, B, C, bias, R, M, N, K, lda,
+                           g_group_m);
+    case EPI_PARTIAL:
+      return launch_kernel(&gemm256p_kernel<EPI_PARTIAL>, grid, block, lds,
+                           stream, A, B, C, bias, R, M, N, K, lda, g_group_m);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
 template <int EPI, int BN, int W>
 hipError_t configure256() {
   hipError_t err = hipFuncSetAttribute(
@@ -1082,6 +1339,9 @@ hipError_t launch256(const uint16_t* A, const uint16_t* B, uint16_t* C,
                      int K, int lda, int splits, int epilogue,
                      hipStream_t stream) {
   if constexpr (BN == 256 && W == 4) {
+    if (g_pair)
+      return launch_pair(A, B, C, bias, R, M, N, K, lda, splits, epilogue,
+                         stream);
     if (g_mfma32)
       return launch_m32(A, B, C, bias, R, M, N, K, lda, splits, epilogue,
                         stream);
@@ -1269,6 +1529,10 @@ hipError_t gemm256_prepare() {
   if (err == hipSuccess) err = configure_m32<EPI_BIAS_GELU>();
   if (err == hipSuccess) err = configure_m32<EPI_BIAS_RESIDUAL>();
   if (err == hipSuccess) err = configure_m32<EPI_PARTIAL>();
+  if (err == hipSuccess) err = configure_pair<EPI_NONE>();
+  if (err == hipSuccess) err = configure_pair<EPI_BIAS_GELU>();
+  if (err == hipSuccess) err = configure_pair<EPI_BIAS_RESIDUAL>();
+  if (err == hipSuccess) err = configure_pair<EPI_PARTIAL>();
   if (err == hipSuccess) err = configure_fused4<EPI_NONE>();
   if (err == hipSuccess) err = configure_fused4<EPI_BIAS_GELU>();
   if (err == hipSuccess) err = configure_fused4<EPI_BIAS_RESIDUAL>();
@@ -1355,6 +1619,8 @@ int gemm_group_m() { return g_group_m; }
 void gemm_set_splitk_fused(int mode) { g_splitk_fused = mode ? 1 : 0; }
 
 void gemm_set_mfma32(int on) { g_mfma32 = on ? 1 : 0; }
+void gemm_set_pair(int on) { g_pair = on ? 1 : 0; }
+int gemm_pair() { return g_pair; }
 int gemm_mfma32() { return g_mfma32; }
 int gemm_splitk_fused() { return g_splitk_fused; }
 

@@ -214,6 +214,8 @@ PYBIND11_MODULE(_kiosk_hip, m) {
   m.def("gemm_splitk_fused", &kiosk::gemm_splitk_fused);
   m.def("gemm_set_mfma32", &kiosk::gemm_set_mfma32, py::arg("on"));
   m.def("gemm_mfma32", &kiosk::gemm_mfma32);
+  m.def("gemm_set_pair", &kiosk::gemm_set_pair, py::arg("on"));
+  m.def("gemm_pair", &kiosk::gemm_pair);
   m.attr("sum_blocks") = kiosk::kSumBlocks;
 
   m.def("gemm_shape_ok", &kiosk::gemm_shape_ok);

@@ -121,10 +121,9 @@ class PoolMixin(object):
             '-m', 'kiosk_autoscaler_amd.worker.zygote', '--backend',
             tpl.backend]
         rocr = self._rocr_embryos = self.zygote_rocr_embryos(tpl)
-        # each ROCr embryo initialises its slot's GPU only (lowest slots
-        # first: the slots a scale-up takes first)
-        gpus = [s.visible_id for s in self.slots
-                if getattr(s, 'kind', 'gpu') == 'gpu'][:rocr]
+        # each ROCr embryo initialises one GPU only (lowest slots first: the
+        # slots a scale-up takes first)
+        gpus = self._distinct_gpus()[:rocr]
         self.zygote = zygote.ZygoteClient(argv, self._environment(tpl),
                                           embryos=self.zygote_embryos(),
                                           rocr_embryos=rocr, rocr_gpus=gpus)
@@ -144,8 +143,8 @@ class PoolMixin(object):
 
     def zygote_rocr_embryos(self, template):
         """How many embryos initialise ROCr while they wait (HIP workers
-        only; ``ZYGOTE_ROCR_EMBRYOS`` overrides, 0 = none): one per GPU slot
-        (at most the embryo count), each bound to its slot's GPU
+        only; ``ZYGOTE_ROCR_EMBRYOS`` overrides, 0 = none): one per GPU
+        device (at most the embryo count), each bound to that GPU
         (``ROCR_VISIBLE_DEVICES=<gpu>`` for its ``hsa_init``), so it opens
         that device alone -- not every device of the node -- and a worker of
         that slot keeps the init.  Each halves a woken standby's boot (~105
@@ -161,9 +160,20 @@ class PoolMixin(object):
         if override.strip():
             wanted = max(0, int(override))
         else:
-            wanted = sum(1 for slot in self.slots
-                         if getattr(slot, 'kind', 'gpu') == 'gpu')
-        return min(self.zygote_embryos(), wanted)
+            # one per device: slots that share a device (a one-GPU
+            # rehearsal of eight slots) share its embryo, so the device's
+            # process count stays within its budget (16 on the pool)
+            wanted = len(self._distinct_gpus())
+        return min(self.zygote_embryos(), wanted, len(self._distinct_gpus()))
+
+    def _distinct_gpus(self):
+        """The managed GPU slots' devices, first occurrence order."""
+        out = []
+        for slot in self.slots:
+            if getattr(slot, 'kind', 'gpu') == 'gpu' and \
+                    slot.visible_id not in out:
+                out.append(slot.visible_id)
+        return out
 
     def _check_zygote(self):
         """False (and the zygote forgotten, restarted after a pause) once

@@ -540,6 +540,61 @@ def test_gemm256_mfma32_splitk_and_forward_shapes(mod, epilogue):
         torch.testing.assert_close(c.float(), ref, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize('M,N,K', [(256, 256, 64), (300, 512, 192),
+                                   (777, 768, 192), (2048, 1024, 4096),
+                                   (1, 256, 64)])
+@pytest.mark.parametrize('epilogue', ['none', 'gelu', 'residual'])
+def test_gemm256_pair_kernel(mod, M, N, K, epilogue):
+    """gemm_set_pair(1): the 256x256 tile on 8 waves, two per SIMD
+    (gemm256p_kernel, 128x64 AGPR tiles) against the fp32 reference --
+    ragged M, one row, a single 64-deep step -- and bit-identical to the
+    4-wave kernel (same MFMAs in the same K order per output)."""
+    from kiosk_autoscaler_amd.ops import kernels
+    a = rand_bf16(M, K, seed=61)
+    b = rand_bf16(N, K, scale=0.1, seed=62)
+    bias = torch.randn(N, device='cuda')
+    res = rand_bf16(M, N, seed=63)
+    ref = a.float() @ b.float().t()
+    if epilogue != 'none':
+        ref = ref + bias
+    if epilogue == 'gelu':
+        ref = gelu_tanh(ref)
+    if epilogue == 'residual':
+        ref = ref + res.float()
+    c4 = kernels.gemm(a, b, bias=bias, residual=res, epilogue=epilogue,
+                      variant='256w4')
+    mod.gemm_set_pair(1)
+    try:
+        c8 = kernels.gemm(a, b, bias=bias, residual=res, epilogue=epilogue,
+                          variant='256w4')
+    finally:
+        mod.gemm_set_pair(0)
+    torch.testing.assert_close(c8.float(), ref, atol=3e-2, rtol=2e-2)
+    assert torch.equal(c8, c4)
+
+
+@pytest.mark.parametrize('epilogue', ['gelu', 'residual'])
+def test_gemm256_pair_splitk_and_forward_shapes(mod, epilogue):
+    """The worker's two GEMMs on the two-waves-per-SIMD kernel: the
+    up-projection (512 tiles) and the split-K down-projection (fp32 partial
+    planes + the reduce), elementwise against fp32."""
+    from kiosk_autoscaler_amd.ops import kernels
+    for M, N, K in ((2048, 16384, 4096), (2048, 4096, 16384)):
+        a = rand_bf16(M, K, seed=71)
+        b = rand_bf16(N, K, scale=0.02, seed=72)
+        bias = torch.randn(N, device='cuda')
+        res = rand_bf16(M, N, seed=73)
+        ref = a.float() @ b.float().t() + bias
+        ref = gelu_tanh(ref) if epilogue == 'gelu' else ref + res.float()
+        mod.gemm_set_pair(1)
+        try:
+            c = kernels.gemm(a, b, bias=bias, residual=res,
+                             epilogue=epilogue)
+        finally:
+            mod.gemm_set_pair(0)
+        torch.testing.assert_close(c.float(), ref, atol=3e-2, rtol=2e-2)
+
+
 def test_splitk_dispatch(mod):
     assert mod.gemm_pick_variant(2048, 4096, 16384, True) == 4
     assert mod.gemm_pick_variant(2048, 4096, 16384, False) == 3

@@ -1110,9 +1110,10 @@ def test_rocr_embryos_one_per_gpu_slot(monkeypatch):
         def __init__(self, backend):
             self.backend = backend
 
-    def rocr(n_slots, backend='hip', kind='gpu'):
+    def rocr(n_slots, backend='hip', kind='gpu', same_device=False):
         holder = pool.PoolMixin()
-        holder.slots = [gpus.GpuSlot(index=i, visible_id=str(i), kind=kind)
+        holder.slots = [gpus.GpuSlot(index=i, visible_id='0' if same_device
+                                     else str(i), kind=kind)
                         for i in range(n_slots)]
         return holder.zygote_rocr_embryos(_Tpl(backend))
 
@@ -1121,11 +1122,14 @@ def test_rocr_embryos_one_per_gpu_slot(monkeypatch):
     monkeypatch.delenv('ROCR_VISIBLE_DEVICES', raising=False)
     assert rocr(1) == 1 and rocr(2) == 2 and rocr(8) == 8
     assert rocr(1, backend='cpu') == 0 and rocr(2, kind='cpu') == 0
+    # eight slots on one device (the one-GPU rehearsal): one embryo, the
+    # device's process budget (16) is not spent on them
+    assert rocr(8, same_device=True) == 1
     monkeypatch.setenv('ROCR_VISIBLE_DEVICES', '0,1')
     assert rocr(2) == 2
     monkeypatch.delenv('ROCR_VISIBLE_DEVICES')
     monkeypatch.setenv('ZYGOTE_ROCR_EMBRYOS', '3')
-    assert rocr(8) == 3 and rocr(1) == 1
+    assert rocr(8) == 3 and rocr(1) == 1 and rocr(8, same_device=True) == 1
 
 
 def test_idle_pool_sets_its_park_instant_for_the_loop():

@@ -32,6 +32,10 @@ def main():
     parser.add_argument('--mfma32', action='store_true',
                         help='add <name>_m32 arms of the 4-wave kernels on '
                              'v_mfma_f32_32x32x16_bf16 (gemm_set_mfma32)')
+    parser.add_argument('--pair', action='store_true',
+                        help='add <name>_pair arms: the 4-wave path on the '
+                             '8-wave, two-waves-per-SIMD kernel '
+                             '(gemm_set_pair)')
     args = parser.parse_args()
     group_ms = [int(g) for g in args.group_m.split(',') if g]
     default_gm = mod.gemm_group_m()
@@ -133,6 +137,15 @@ def main():
                         fn()
                         mod.gemm_set_mfma32(0)
                     fns[base + '_m32'] = arm32
+        if args.pair:
+            for base in ('native_gelu_auto', 'native256w4', 'native256w4_gelu',
+                         'native256splitk'):
+                if base in fns:
+                    def arm_pair(fn=fns[base]):
+                        mod.gemm_set_pair(1)
+                        fn()
+                        mod.gemm_set_pair(0)
+                    fns[base + '_pair'] = arm_pair
         if args.only:
             keep = set(args.only.split(','))
             fns = {k: v for k, v in fns.items() if k in keep}
