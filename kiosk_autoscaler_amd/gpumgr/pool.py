@@ -583,12 +583,13 @@ class PoolMixin(object):
     # wake-up; SPREAD_K times the distance between the sized boot and the
     # median boot covers the jitter the recent boots show, so a busier
     # 8-GPU host with concurrent boots gets a wider margin by itself.
-    # Replayed over round 5's 576 woken boots (tools/wake_lead_replay.py):
-    # late 4.6 ms / hold 84 ms a wake against 3.9 / 83 for the former fixed
-    # +50 ms; over the ROCr-embryo boots 0 late and 25 ms hold against 32
-    # for the former fixed +30 ms
+    # Replayed (tools/wake_lead_replay.py) over round 5's 576 woken boots
+    # without ROCr embryos: late 5.1 ms / hold 79 ms a wake against 3.9 / 83
+    # for the former fixed +50 ms; over the ROCr-embryo boots (round 5: 50,
+    # round 6: 24) never late, hold 22-26 ms a wake against 32 for the
+    # former fixed +30 ms.  K = 3 held 7 ms a wake more on round 6's boots
     WAKE_MARGIN_FLOOR_S = 0.01
-    WAKE_SPREAD_K = 3.0
+    WAKE_SPREAD_K = 1.5
     WAKE_MARGIN_MAX_S = 0.06
     # (while fewer than 4 boots are known: the slowest plus this)
     WAKE_MARGIN_S = 0.05

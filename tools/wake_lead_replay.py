@@ -47,7 +47,7 @@ def second_slowest(window, min_samples=4):
     return est
 
 
-def spread_margin(k=3.0, floor=0.01, hi=0.06, window=16):
+def spread_margin(k=1.5, floor=0.01, hi=0.06, window=16):
     """gpumgr/pool.py ``wake_lead`` since round 6: second slowest of the
     window plus ``floor + k * (second slowest - median)``, clamped."""
     def est(hist):
@@ -101,7 +101,7 @@ def main(argv=None):
         with open(args.dump, 'w') as fh:
             json.dump({'runs': runs}, fh)
     print('%d runs, %d woken boots' % (len(runs), sum(map(len, runs))))
-    for k in (1.0, 2.0, 3.0):
+    for k in (1.0, 1.5, 2.0, 3.0):
         row = replay(runs, spread_margin(k), 0.0)
         print('second slowest of 16 + spread margin (k=%g): late %5.2f '
               'ms/wake (%d of %d), hold %5.1f ms/wake' % (
