@@ -175,11 +175,6 @@ __device__ __forceinline__ void mfma_drain() {
 #ifndef KIOSK_W4_REGSTAGE
 #define KIOSK_W4_REGSTAGE 0
 #endif
-// gemm256p_kernel: the MFMA index at which waves 4-7 start their DMA
-// issues within a half-step (waves 0-3 start at 0)
-#ifndef KIOSK_PAIR_STAGGER
-#define KIOSK_PAIR_STAGGER 12
-#endif
 
 // Counted waits go through the builtin (not inline asm) so hipcc's waitcnt
 // pass sees them and adds no conservative lgkmcnt(0) of its own.  gfx9
@@ -1076,7 +1071,7 @@ hipError_t launch_m32(const uint16_t* A, const uint16_t* B, uint16_t* C,
 // "Two waves per SIMD" item 9) so they are not both held at once.  LDS
 // reads per CU rise from 64 to 96 KiB per half-step (384 of the 1024
 // cycles at 256 B/clk) -- within the array's budget.
-template <int EPI>
+template <int EPI, int kStagger, int kPrio>
 __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
     uint16_t* __restrict__ C, const float* __restrict__ bias,
@@ -1204,10 +1199,14 @@ __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
       half(std::false_type(), std::true_type(), off, t, wb1, xa1, wb0, xa0);
     }
   };
-  if (wave >= 4)
-    mainloop(std::integral_constant<int, KIOSK_PAIR_STAGGER>());
-  else
+  if (wave >= 4) {
+    // static priority for the later-dispatched half (MI355X_MICROARCH.md
+    // "Two waves per SIMD" item 4): one s_setprio before the loop
+    if constexpr (kPrio) __builtin_amdgcn_s_setprio(1);
+    mainloop(std::integral_constant<int, kStagger>());
+  } else {
     mainloop(std::integral_constant<int, 0>());
+  }
   // drain the tail DMAs before the workgroup's LDS can be released
   __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
   mfma_drain();
@@ -1277,39 +1276,92 @@ __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
   }
 }
 
-// 0: one wave per SIMD (gemm256_kernel<., 256, 4>); 1: gemm256p_kernel
-// wherever the 4-wave one-tile kernel runs
+// 0: one wave per SIMD (gemm256_kernel<., 256, 4>); 1..5: gemm256p_kernel
+// wherever the 4-wave one-tile kernel runs, with the DMA stagger of waves
+// 4-7 (MFMA index) and static priority of this table (A/B arms)
 int g_pair = 0;
+constexpr int kPairModes = 5;
+
+template <int EPI, int kMode>
+struct PairCfg {
+  static constexpr int kStagger = kMode == 2 ? 0 : kMode == 3 ? 6 :
+                                  kMode == 4 ? 16 : 12;
+  static constexpr int kPrio = kMode == 5 ? 1 : 0;
+  static constexpr auto kernel =
+      &gemm256p_kernel<EPI, kStagger, kPrio>;
+};
+
+template <int EPI, int kMode>
+hipError_t configure_pair_mode() {
+  constexpr auto k = PairCfg<EPI, kMode>::kernel;
+  hipError_t err = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(k),
+      hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256, 4>::kLdsBytes);
+  return err == hipSuccess ? prepare_kernel(k) : err;
+}
 
 template <int EPI>
 hipError_t configure_pair() {
-  hipError_t err = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&gemm256p_kernel<EPI>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256, 4>::kLdsBytes);
-  return err == hipSuccess ? prepare_kernel(&gemm256p_kernel<EPI>) : err;
+  hipError_t err = configure_pair_mode<EPI, 1>();
+  if (err == hipSuccess) err = configure_pair_mode<EPI, 2>();
+  if (err == hipSuccess) err = configure_pair_mode<EPI, 3>();
+  if (err == hipSuccess) err = configure_pair_mode<EPI, 4>();
+  if (err == hipSuccess) err = configure_pair_mode<EPI, 5>();
+  return err;
+}
+
+template <int EPI, int kMode>
+hipError_t launch_pair_mode(const uint16_t* A, const uint16_t* B, uint16_t* C,
+                            const float* bias, const uint16_t* R, int M,
+                            int N, int K, int lda, int splits,
+                            hipStream_t stream) {
+  const int blocks = ((M + BM - 1) / BM) * (N / 256);
+  const dim3 grid(blocks, splits), block(512);
+  constexpr int lds = Geo<256, 4>::kLdsBytes;
+  return launch_kernel(PairCfg<EPI, kMode>::kernel, grid, block, lds, stream,
+                       A, B, C, bias, R, M, N, K, lda, g_group_m);
+}
+
+template <int EPI>
+hipError_t launch_pair_epi(const uint16_t* A, const uint16_t* B, uint16_t* C,
+                           const float* bias, const uint16_t* R, int M, int N,
+                           int K, int lda, int splits, hipStream_t stream) {
+  switch (g_pair) {
+    case 2:
+      return launch_pair_mode<EPI, 2>(A, B, C, bias, R, M, N, K, lda, splits,
+                                      stream);
+    case 3:
+      return launch_pair_mode<EPI, 3>(A, B, C, bias, R, M, N, K, lda, splits,
+                                      stream);
+    case 4:
+      return launch_pair_mode<EPI, 4>(A, B, C, bias, R, M, N, K, lda, splits,
+                                      stream);
+    case 5:
+      return launch_pair_mode<EPI, 5>(A, B, C, bias, R, M, N, K, lda, splits,
+                                      stream);
+    default:
+      return launch_pair_mode<EPI, 1>(A, B, C, bias, R, M, N, K, lda, splits,
+                                      stream);
+  }
 }
 
 hipError_t launch_pair(const uint16_t* A, const uint16_t* B, uint16_t* C,
                        const float* bias, const uint16_t* R, int M, int N,
                        int K, int lda, int splits, int epilogue,
                        hipStream_t stream) {
-  const int blocks = ((M + BM - 1) / BM) * (N / 256);
-  const dim3 grid(blocks, splits), block(512);
-  constexpr int lds = Geo<256, 4>::kLdsBytes;
   switch (epilogue) {
     case EPI_NONE:
-      return launch_kernel(&gemm256p_kernel<EPI_NONE>, grid, block, lds,
-                           stream, A, B, C, bias, R, M, N, K, lda, g_group_m);
+      return launch_pair_epi<EPI_NONE>(A, B, C, bias, R, M, N, K, lda, splits,
+                                       stream);
     case EPI_BIAS_GELU:
-      return launch_kernel(&gemm256p_kernel<EPI_BIAS_GELU>, grid, block, lds,
-                           stream, A, B, C, bias, R, M, N, K, lda, g_group_m);
+      return launch_pair_epi<EPI_BIAS_GELU>(A, B, C, bias, R, M, N, K, lda,
+                                            splits, stream);
     case EPI_BIAS_RESIDUAL:
-      return launch_kernel(&gemm256p_kernel<EPI_BIAS_RESIDUAL>, grid, block,
-                           lds, stream, A, B, C, bias, R, M, N, K, lda,
-                           g_group_m);
+      return launch_pair_epi<EPI_BIAS_RESIDUAL>(A, B, C, bias, R, M, N, K,
+                                                lda, splits, stream);
     case EPI_PARTIAL:
-      return launch_kernel(&gemm256p_kernel<EPI_PARTIAL>, grid, block, lds,
-                           stream, A, B, C, bias, R, M, N, K, lda, g_group_m);
+      return launch_pair_epi<EPI_PARTIAL>(A, B, C, bias, R, M, N, K, lda,
+                                          splits, stream);
     default:
       return hipErrorInvalidValue;
   }
@@ -1619,7 +1671,9 @@ int gemm_group_m() { return g_group_m; }
 void gemm_set_splitk_fused(int mode) { g_splitk_fused = mode ? 1 : 0; }
 
 void gemm_set_mfma32(int on) { g_mfma32 = on ? 1 : 0; }
-void gemm_set_pair(int on) { g_pair = on ? 1 : 0; }
+void gemm_set_pair(int mode) {
+  g_pair = mode < 0 ? 0 : (mode > kPairModes ? 1 : mode);
+}
 int gemm_pair() { return g_pair; }
 int gemm_mfma32() { return g_mfma32; }
 int gemm_splitk_fused() { return g_splitk_fused; }
