@@ -1276,24 +1276,18 @@ __global__ __launch_bounds__(512, 1) void gemm256p_kernel(
   }
 }
 
-// 0: one wave per SIMD (gemm256_kernel<., 256, 4>); 1..5: gemm256p_kernel
-// wherever the 4-wave one-tile kernel runs, with the DMA stagger of waves
-// 4-7 (MFMA index) and static priority of this table (A/B arms)
+// 0: one wave per SIMD (gemm256_kernel<., 256, 4>); 1: gemm256p_kernel
+// wherever the 4-wave one-tile kernel runs -- an A/B arm, off: it measured
+// 0.6 % faster on the plain up-projection and 2.5-4 % slower everywhere
+// else (profiles/r6_gemm_pair/)
 int g_pair = 0;
-constexpr int kPairModes = 5;
+// the best of the five stagger / priority arms measured: waves 4-7 start
+// their DMA at MFMA 12 of a half-step and run at s_setprio 1
+constexpr int kPairStagger = 12, kPairPrio = 1;
 
-template <int EPI, int kMode>
-struct PairCfg {
-  static constexpr int kStagger = kMode == 2 ? 0 : kMode == 3 ? 6 :
-                                  kMode == 4 ? 16 : 12;
-  static constexpr int kPrio = kMode == 5 ? 1 : 0;
-  static constexpr auto kernel =
-      &gemm256p_kernel<EPI, kStagger, kPrio>;
-};
-
-template <int EPI, int kMode>
-hipError_t configure_pair_mode() {
-  constexpr auto k = PairCfg<EPI, kMode>::kernel;
+template <int EPI>
+hipError_t configure_pair() {
+  constexpr auto k = &gemm256p_kernel<EPI, kPairStagger, kPairPrio>;
   hipError_t err = hipFuncSetAttribute(
       reinterpret_cast<const void*>(k),
       hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256, 4>::kLdsBytes);
@@ -1301,48 +1295,15 @@ hipError_t configure_pair_mode() {
 }
 
 template <int EPI>
-hipError_t configure_pair() {
-  hipError_t err = configure_pair_mode<EPI, 1>();
-  if (err == hipSuccess) err = configure_pair_mode<EPI, 2>();
-  if (err == hipSuccess) err = configure_pair_mode<EPI, 3>();
-  if (err == hipSuccess) err = configure_pair_mode<EPI, 4>();
-  if (err == hipSuccess) err = configure_pair_mode<EPI, 5>();
-  return err;
-}
-
-template <int EPI, int kMode>
-hipError_t launch_pair_mode(const uint16_t* A, const uint16_t* B, uint16_t* C,
-                            const float* bias, const uint16_t* R, int M,
-                            int N, int K, int lda, int splits,
-                            hipStream_t stream) {
-  const int blocks = ((M + BM - 1) / BM) * (N / 256);
-  const dim3 grid(blocks, splits), block(512);
-  constexpr int lds = Geo<256, 4>::kLdsBytes;
-  return launch_kernel(PairCfg<EPI, kMode>::kernel, grid, block, lds, stream,
-                       A, B, C, bias, R, M, N, K, lda, g_group_m);
-}
-
-template <int EPI>
 hipError_t launch_pair_epi(const uint16_t* A, const uint16_t* B, uint16_t* C,
                            const float* bias, const uint16_t* R, int M, int N,
                            int K, int lda, int splits, hipStream_t stream) {
-  switch (g_pair) {
-    case 2:
-      return launch_pair_mode<EPI, 2>(A, B, C, bias, R, M, N, K, lda, splits,
-                                      stream);
-    case 3:
-      return launch_pair_mode<EPI, 3>(A, B, C, bias, R, M, N, K, lda, splits,
-                                      stream);
-    case 4:
-      return launch_pair_mode<EPI, 4>(A, B, C, bias, R, M, N, K, lda, splits,
-                                      stream);
-    case 5:
-      return launch_pair_mode<EPI, 5>(A, B, C, bias, R, M, N, K, lda, splits,
-                                      stream);
-    default:
-      return launch_pair_mode<EPI, 1>(A, B, C, bias, R, M, N, K, lda, splits,
-                                      stream);
-  }
+  const int blocks = ((M + BM - 1) / BM) * (N / 256);
+  const dim3 grid(blocks, splits), block(512);
+  constexpr int lds = Geo<256, 4>::kLdsBytes;
+  return launch_kernel(&gemm256p_kernel<EPI, kPairStagger, kPairPrio>, grid,
+                       block, lds, stream, A, B, C, bias, R, M, N, K, lda,
+                       g_group_m);
 }
 
 hipError_t launch_pair(const uint16_t* A, const uint16_t* B, uint16_t* C,
@@ -1671,9 +1632,7 @@ int gemm_group_m() { return g_group_m; }
 void gemm_set_splitk_fused(int mode) { g_splitk_fused = mode ? 1 : 0; }
 
 void gemm_set_mfma32(int on) { g_mfma32 = on ? 1 : 0; }
-void gemm_set_pair(int mode) {
-  g_pair = mode < 0 ? 0 : (mode > kPairModes ? 1 : mode);
-}
+void gemm_set_pair(int on) { g_pair = on ? 1 : 0; }
 int gemm_pair() { return g_pair; }
 int gemm_mfma32() { return g_mfma32; }
 int gemm_splitk_fused() { return g_splitk_fused; }

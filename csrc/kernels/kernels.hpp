@@ -81,8 +81,8 @@ int gemm_splitk_fused();
 // (gemm256m32_kernel, profiles/r4_mfma_dma); 0: on 16x16x32
 void gemm_set_mfma32(int on);
 int gemm_mfma32();
-// 1..5: the 4-wave one-tile GEMM path runs gemm256p_kernel (8 waves, two per
-// SIMD, 128x64 AGPR tiles; the modes are stagger / priority A/B arms)
+// 1: the 4-wave one-tile GEMM path runs gemm256p_kernel (8 waves, two per
+// SIMD, 128x64 AGPR tiles; an A/B arm, profiles/r6_gemm_pair)
 void gemm_set_pair(int on);
 int gemm_pair();
 // tile rows per group in the 256-row kernels' tile order (default 4)

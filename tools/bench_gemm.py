@@ -32,13 +32,13 @@ def main():
     parser.add_argument('--mfma32', action='store_true',
                         help='add <name>_m32 arms of the 4-wave kernels on '
                              'v_mfma_f32_32x32x16_bf16 (gemm_set_mfma32)')
-    parser.add_argument('--pair', default='',
-                        help='comma-separated gemm_set_pair modes: each adds '
-                             '<name>_pair<M> arms (the 4-wave path on the '
-                             '8-wave, two-waves-per-SIMD kernel)')
+    parser.add_argument('--pair', action='store_true',
+                        help='add <name>_pair arms: the 4-wave path on the '
+                             '8-wave, two-waves-per-SIMD kernel '
+                             '(gemm_set_pair)')
     args = parser.parse_args()
     group_ms = [int(g) for g in args.group_m.split(',') if g]
-    pair_modes = [int(m) for m in args.pair.split(',') if m]
+    pair_modes = [1] if args.pair else []
     default_gm = mod.gemm_group_m()
     for spec in args.shapes.split(','):
         M, N, K = (int(v) for v in spec.split('x'))
@@ -146,7 +146,7 @@ def main():
                         mod.gemm_set_pair(mode)
                         fn()
                         mod.gemm_set_pair(0)
-                    fns['%s_pair%d' % (base, mode)] = arm_pair
+                    fns['%s_pair' % base] = arm_pair
         if args.only:
             keep = set(args.only.split(','))
             fns = {k: v for k, v in fns.items() if k in keep}
