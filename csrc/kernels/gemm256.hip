@@ -1534,7 +1534,6 @@ hipError_t gemm256_prepare() {
     g_cu_count = cus;
   hipError_t err = configure256_all<256, 8>();
   if (err == hipSuccess) err = configure_persist<EPI_NONE>();
-  if (err == hipSuccess) err = configure_persist<EPI_BIAS_GELU>();
   if (err == hipSuccess) err = configure_persist<EPI_BIAS_RESIDUAL>();
   if (err == hipSuccess) err = configure256_all<128, 8>();
   if (err == hipSuccess) err = configure256_all<256, 4>();
@@ -1599,8 +1598,12 @@ hipError_t launch_gemm256_persist(const uint16_t* A, const uint16_t* B,
       return launch_persist_epi<EPI_NONE>(A, B, C, bias, R, M, N, K, grid,
                                           stream);
     case EPI_BIAS_GELU:
-      return launch_persist_epi<EPI_BIAS_GELU>(A, B, C, bias, R, M, N, K,
-                                               grid, stream);
+      // the persistent bias+GELU kernel carried the next tile's address
+      // state across the GELU epilogue and spilled a VGPR; it also ran
+      // 1-2 % slower than the one-tile kernel (round 3): the GELU epilogue
+      // runs the one-tile grid
+      return launch256<256, 4>(A, B, C, bias, R, M, N, K, K, 1,
+                               EPI_BIAS_GELU, stream);
     case EPI_BIAS_RESIDUAL:
       return launch_persist_epi<EPI_BIAS_RESIDUAL>(A, B, C, bias, R, M, N, K,
                                                    grid, stream);
