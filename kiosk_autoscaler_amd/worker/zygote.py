@@ -483,12 +483,15 @@ class _HsaPreinit(object):
                           % self.status)
             return None      # (or the request came before the init)
         gpu = _request_gpu(request)
+        candidate = request
         if self.gpu is not None and gpu == self.gpu:
-            # the worker pins its GPU at the ROCr level, as the init did
-            request.setdefault('env', {})['ROCR_VISIBLE_DEVICES'] = self.gpu
-        worker = _rocr_env(_worker_env(request))
+            # the worker would pin its GPU at the ROCr level, as the init did
+            candidate = dict(request, env=dict(request.get('env', {}),
+                                               ROCR_VISIBLE_DEVICES=self.gpu))
+        worker = _rocr_env(_worker_env(candidate))
         if worker == self.snapshot and \
                 (self.gpu is None or gpu == self.gpu):
+            request['env'] = candidate.get('env', {})
             return self.done_ns
         self.lib.hsa_shut_down()
         self.lib = None

@@ -363,6 +363,18 @@ def test_slot_bound_embryo_of_another_gpu_is_shut_down(monkeypatch):
     assert 'ROCR_VISIBLE_DEVICES' not in request['env']
 
 
+def test_slot_bound_embryo_under_the_visible_pin_is_shut_down(monkeypatch):
+    """WORKER_PIN=visible: the worker keeps every managed GPU visible, so an
+    init bound to its GPU alone cannot be kept -- shut down, and the
+    request's environment is left as the manager sent it."""
+    import json
+    pin = {'gpu': '6', 'visible': ['4', '5', '6', '7']}
+    stamp, calls, request = _settled(monkeypatch, None,
+                                     ['--pin', json.dumps(pin)], {}, gpu='6')
+    assert calls == ['init', 'shut_down'] and stamp is None
+    assert 'ROCR_VISIBLE_DEVICES' not in request['env']
+
+
 def test_embryo_of_another_template_shuts_rocr_down(monkeypatch):
     """an HSA_* setting the assignment's template env changes
     (SDMA off here) was silently ignored by a kept init."""
