@@ -194,6 +194,21 @@ class NodeComm(object):
                        new)
         return True
 
+    def _shared_device(self, members):
+        """Devices (visible ids) that more than one member's slot uses."""
+        device = {s.index: s.visible_id for s in self.m.slots
+                  if getattr(s, 'kind', 'gpu') == 'gpu' and
+                  s.visible_id not in (None, '')}
+        seen, shared = set(), []
+        for index, _ in members:
+            dev = device.get(index)
+            if dev is None:
+                continue
+            if dev in seen and dev not in shared:
+                shared.append(dev)
+            seen.add(dev)
+        return shared
+
     def _bound(self):
         """slot index -> the process currently serving that slot."""
         bound = {}
@@ -464,7 +479,18 @@ class NodeComm(object):
         n = len(members)
         warm = all(getattr(proc, 'rccl_inits', 0) > 0 for _, proc in members)
         rccl = self.transport_override in (None, 'rccl')
-        lib = self.current_lib()
+        transport = self.transport_override
+        shared = self._shared_device(members)
+        if rccl and shared and self.fallback:
+            # RCCL refuses two ranks on one device ("Duplicate GPU"): a
+            # generation over slots that share a device (a one-GPU
+            # rehearsal of several slots) runs on the fallback transport
+            # from the start -- no failed RCCL generation, no library
+            # switch, no fallback counted
+            transport, rccl = self.fallback, False
+            self.m.events.emit('node_comm_shared_device', gen=self.gen,
+                               devices=shared, transport=transport)
+        lib = self.current_lib() if rccl else None
         # a library switch loads a library new to every rank: the longer
         # first-generation budget
         warm = warm and all(getattr(proc, 'rccl_lib', None) == lib
@@ -474,15 +500,15 @@ class NodeComm(object):
         for rank, (_, proc) in enumerate(members):
             message = {'cmd': 'comm_init', 'gen': self.gen, 'rank': rank,
                        'nranks': n, 'timeout': self.gen_timeout}
-            if self.transport_override:
-                message['transport'] = self.transport_override
+            if transport:
+                message['transport'] = transport
             if lib:
                 message['lib'] = lib
             proc.pipe.send(message)
         self.m.events.emit('node_comm_init', gen=self.gen, n=n,
                            slots=[index for index, _ in members],
                            pids=[proc.pid for _, proc in members],
-                           transport=self.transport_override, lib=lib)
+                           transport=transport, lib=lib)
         logger.info('Node communicator generation %d: %d ranks.', self.gen, n)
         self.m._publish_pool()
 

@@ -361,6 +361,69 @@ def test_node_comm_falls_back_after_failed_generations():
     assert 'transport' not in manager.standbys[0].sent[-1]
 
 
+def test_node_comm_library_ladder_unit():
+    """The ladder without processes: two failed generations on the slim
+    library move the node to the stock one (asked for in every
+    ``comm_init``), two more move it to the fallback transport."""
+    from kiosk_autoscaler_amd.gpumgr.nodecomm import NodeComm
+    manager = _FakeManager(2)
+    node = NodeComm(manager, fallback='shm', fallback_after=2)
+    node.rccl_libs = ['/c/slim/librccl.so.1', '/opt/rocm/lib/librccl.so.1']
+    procs = [manager.standbys[0], manager.standbys[1]]
+    libs = []
+    for gen in (1, 2, 3, 4):
+        node.step()
+        init = procs[1].sent[-1]
+        assert init['gen'] == gen and 'transport' not in init
+        libs.append(init['lib'])
+        for rank in (1, 0):
+            node.on_message(procs[rank], {'ev': 'comm_ready', 'gen': gen,
+                                          'rank': rank, 'ok': False,
+                                          'detail': 'rccl refused'})
+        node.step()
+        node.retry_at = 0.0
+    assert libs == node.rccl_libs[:1] * 2 + node.rccl_libs[1:] * 2
+    kinds = [e['ev'] for e in manager.emitted]
+    assert kinds.count('node_comm_library') == 1
+    assert kinds.count('node_comm_fallback') == 1
+    node.step()
+    init = procs[0].sent[-1]
+    assert init['gen'] == 5 and init['transport'] == 'shm'
+    assert 'lib' not in init
+
+
+def test_generation_over_a_shared_device_starts_on_the_fallback():
+    """Slots that share a device (eight slots on one GPU): RCCL refuses two
+    ranks on one device, so such a generation runs on the fallback
+    transport from the start -- no failed RCCL generation, no library
+    switch, nothing counted as a fallback."""
+    from kiosk_autoscaler_amd.gpumgr.gpus import GpuSlot
+    from kiosk_autoscaler_amd.gpumgr.nodecomm import NodeComm
+    manager = _FakeManager(3)
+    manager.slots = [GpuSlot(0, '0'), GpuSlot(1, '0'), GpuSlot(2, '1')]
+    node = NodeComm(manager, fallback='shm', fallback_after=2)
+    node.rccl_libs = ['/c/slim/librccl.so.1', '/opt/rocm/lib/librccl.so.1']
+    node.step()
+    init = manager.standbys[0].sent[-1]
+    assert init['transport'] == 'shm' and 'lib' not in init
+    shared = [e for e in manager.emitted
+              if e['ev'] == 'node_comm_shared_device']
+    assert shared and shared[0]['devices'] == ['0']
+    for rank in range(3):
+        node.on_message(manager.standbys[rank], {
+            'ev': 'comm_ready', 'gen': 1, 'rank': rank, 'ok': True,
+            'transport': 'shm', 'init_ms': 1.0})
+    assert node.ready and node.transport == 'shm'
+    assert node.fallback_used is None and node.failures == 0
+    # distinct devices: RCCL, with the ladder's library
+    manager = _FakeManager(2)
+    node = NodeComm(manager, fallback='shm')
+    node.rccl_libs = ['/c/slim/librccl.so.1']
+    node.step()
+    init = manager.standbys[1].sent[-1]
+    assert 'transport' not in init and init['lib'] == '/c/slim/librccl.so.1'
+
+
 def test_node_comm_kills_a_rank_that_never_answers():
     """SURVEY §5.3 (a fence timeout marks a rank dead): ranks 0 and 1
     report a failed connect, rank 2 stays silent past the grace -- it is
