@@ -206,8 +206,11 @@ def standby_split(events, t_lo, t_hi):
 
     def close(pid, t_end, closer):
         start, opener = open_at.pop(pid)
-        if opener == 'drained' and closer == 'exit':
-            cmd = next((c for c in exit_cmds if start <= c <= t_end), None)
+        if opener in ('drained', 'retired') and closer == 'exit':
+            # a retired worker was told to exit at once (worker_retired);
+            # a recycled one when the pool parked or retired it
+            cmd = start if opener == 'retired' else next(
+                (c for c in exit_cmds if start <= c <= t_end), None)
             if cmd is None:
                 cmd = start
             parts['park_delay'] += clip(start, cmd)
@@ -225,7 +228,8 @@ def standby_split(events, t_lo, t_hi):
             # the drained worker's GPU stays held from its recycle on (its
             # 'standby' report follows after it freed its buffers)
             serving.discard(pid)
-            open_at.setdefault(pid, (e['t'], 'drained'))
+            open_at.setdefault(pid, (e['t'], 'retired' if ev ==
+                                     'worker_retired' else 'drained'))
         elif ev == 'standby_ready' and (e.get('preinit') or
                                         e.get('recycled')):
             if e.get('recycled'):

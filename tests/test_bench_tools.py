@@ -185,6 +185,16 @@ def test_standby_split_parts_sum_to_the_total():
     assert split['exit_teardown_ms_mean'] == pytest.approx(120.0)
     assert metrics.standby_gpu(events, 0, int(20e9)) == \
         pytest.approx(split['total_s'])
+    # a worker retired at once (worker_retired: its exit command went with
+    # the event) has no park delay, whenever the pool parks
+    retired = [
+        _ev('worker_retired', 5.0, pid=3),
+        _ev('pool_parked', 5.01),
+        _ev('standby_exit', 5.15, pid=3),
+    ]
+    split = metrics.standby_split(retired, 0, int(20e9))
+    assert split['park_delay_s'] == 0
+    assert split['exit_teardown_s'] == pytest.approx(0.15)
 
 
 def test_idle_queue_reads_per_second():
