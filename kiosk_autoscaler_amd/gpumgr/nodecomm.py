@@ -183,10 +183,9 @@ class NodeComm(object):
         self.lib_switches += 1
         self.failures = 0
         self.retry_at = now
-        # processes spawned from now on load it first (zygote children
-        # load it beside the copy the zygote mapped, at their connect)
-        import os
-        os.environ['KIOSK_RCCL_LIB'] = new
+        # processes spawned from now on load it first (``_environment``;
+        # zygote children load it beside the copy the zygote mapped, at
+        # their connect)
         self.m.events.emit('node_comm_library', gen=self.gen, lib=new,
                            previous=old, reason=reason)
         logger.warning('Node communicator: RCCL from %s failed %d '

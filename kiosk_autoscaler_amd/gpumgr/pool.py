@@ -91,10 +91,14 @@ class PoolMixin(object):
             argv.append('-S')
         return argv
 
-    @staticmethod
-    def _environment(template):
+    def _environment(self, template):
         env = dict(os.environ)
         env.update({k: str(v) for k, v in template.env.items()})
+        # the RCCL library the node ladder is on now: loaded first by a new
+        # process's preload (the manager's own environment stays as it was)
+        lib = self.node.current_lib() if self.node is not None else None
+        if lib:
+            env['KIOSK_RCCL_LIB'] = lib
         env['PYTHONUNBUFFERED'] = '1'
         root = os.path.dirname(os.path.dirname(os.path.dirname(
             os.path.abspath(__file__))))

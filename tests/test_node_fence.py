@@ -1106,6 +1106,7 @@ def test_broken_slim_rccl_ends_on_stock_rccl_not_shm(resp_server, tmp_path,
     shutil.copy(stock, str(slim))
     monkeypatch.setenv('KIOSK_RCCL_LADDER', os.pathsep.join([str(slim),
                                                              stock]))
+    before = os.environ.get('KIOSK_RCCL_LIB')
     s, client, events, manager, scaler = _node_stack(
         resp_server, 'rccl-fake', tmp_path,
         extra={'KIOSK_RCCL_LIB': str(slim),
@@ -1128,6 +1129,10 @@ def test_broken_slim_rccl_ends_on_stock_rccl_not_shm(resp_server, tmp_path,
                  len(_ready_ids(manager)) == 2, timeout=30)
     finally:
         manager.stop(timeout=15)
+    # the switch reaches new processes through their spawn environment; the
+    # manager's own stays as it was (a later manager in this process must
+    # not inherit a library under this test's tmp_path)
+    assert os.environ.get('KIOSK_RCCL_LIB') == before
     kinds = [e['ev'] for e in events.records]
     assert 'node_comm_fallback' not in kinds
     inits = [e for e in events.records if e['ev'] == 'node_comm_init']

@@ -2,7 +2,8 @@
 """Static check of the 4-wave GEMM kernels' asm-MFMA contract.
 
 hipcc pads no wait states after an inline-asm MFMA (cdna_hip_programming.md
-§5.7), so in every ``gemm256_kernel<*, 256, 4, *>`` the accumulators (AGPRs)
+§5.7), so in every ``gemm256_kernel<*, 256, 4, *>`` and ``gemm256p_kernel<*>``
+the accumulators (AGPRs)
 may be touched only by MFMAs until the ``s_nop`` drain that ends the k-loop,
 and no scratch (spill) access may appear anywhere -- except, in the
 persistent variant (``kPersist`` = 1: a loop over tiles around it all), a
@@ -25,8 +26,10 @@ AGPR = re.compile(r'\ba(\d+|\[\d+:\d+\])')
 
 def check(asm_text):
     problems = []
-    funcs = re.findall(r'^(_Z\S*gemm256_kernelILi\dELi256ELi4E\S*):',
-                       asm_text, re.M)
+    # the 4-wave kernels and the two-waves-per-SIMD arm (gemm256p_kernel):
+    # both issue their MFMAs as AGPR-pinned inline asm
+    funcs = re.findall(r'^(_Z\S*(?:gemm256_kernelILi\dELi256ELi4E|'
+                       r'gemm256p_kernelILi\d)\S*):', asm_text, re.M)
     if not funcs:
         problems.append('no 4-wave gemm256 kernel found')
     for name in funcs:
