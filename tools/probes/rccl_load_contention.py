@@ -52,6 +52,24 @@ def child():
                       'warm_init_ms': round(warm_ms, 1)}), flush=True)
 
 
+def _line(proc, want):
+    """The child's next stdout line starting with ``want`` (RCCL and ROCr
+    may print their own lines there first); None at EOF."""
+    for line in proc.stdout:
+        if line.startswith(want):
+            return line
+    return None
+
+
+def _failed(proc):
+    try:
+        rc = proc.wait(timeout=30)
+    except subprocess.TimeoutExpired:
+        rc = None
+    return RuntimeError('child failed (rc %s): %s' % (
+        rc, proc.stderr.read()[-600:]))
+
+
 def run(p, env):
     procs = [subprocess.Popen([sys.executable, __file__, '--child'], env=env,
                               stdin=subprocess.PIPE, stdout=subprocess.PIPE,
@@ -59,17 +77,17 @@ def run(p, env):
              for _ in range(p)]
     try:
         for proc in procs:
-            if proc.stdout.readline().strip() != 'ready':
-                raise RuntimeError('child failed: %s' % proc.stderr.read()[-400:])
+            if _line(proc, 'ready') is None:
+                raise _failed(proc)
         t0 = time.perf_counter()
         for proc in procs:
             proc.stdin.write('go\n')
             proc.stdin.flush()
         rows = []
         for proc in procs:
-            line = proc.stdout.readline()
-            if not line.startswith('{'):
-                raise RuntimeError('child failed: %s' % proc.stderr.read()[-400:])
+            line = _line(proc, '{')
+            if line is None:
+                raise _failed(proc)
             rows.append(json.loads(line))
         wall = (time.perf_counter() - t0) * 1e3
         for proc in procs:
