@@ -547,6 +547,11 @@ def main():
             # everything that forks runs before this process touches the GPU
             svc = Services(args, args.gpus).start()
             log('services up: redis :%d, standby pool booted' % svc.port)
+        else:
+            # a rank other than 0 starts no process and only brackets the
+            # timed region: it opens its own device alone, so each GPU of
+            # the node carries 2 rank processes (0 and its own), not N
+            restrict_rank_device(local_rank)
         import torch
         if world > 1:
             import datetime
@@ -567,6 +572,7 @@ def main():
         if use_cuda:
             # modulo: the N>1 launch path can be rehearsed on a box with
             # fewer devices than ranks (BENCH_GPU_IDS); identity on a node
+            # (a restricted rank sees its one device as 0)
             torch.cuda.set_device(local_rank % torch.cuda.device_count())
 
         def barrier():
@@ -909,6 +915,25 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         'wall_s': round(time.monotonic() - T_PROCESS_START, 1),
     })
     return line
+
+
+def rank_device(local_rank, env=None):
+    """The device a torchrun rank brackets the timed region on, as a
+    ``HIP_VISIBLE_DEVICES`` value: its entry of ``BENCH_GPU_IDS`` (the
+    one-box rehearsal, several ranks per device), else its local rank, in
+    the numbering of an inherited ``HIP_VISIBLE_DEVICES``."""
+    env = os.environ if env is None else env
+    ids = [i.strip() for i in (env.get('BENCH_GPU_IDS') or '').split(',')
+           if i.strip()]
+    index = int(ids[local_rank % len(ids)]) if ids else local_rank
+    visible = [v.strip() for v in (env.get('HIP_VISIBLE_DEVICES') or
+                                   '').split(',') if v.strip()]
+    return visible[index % len(visible)] if visible else str(index)
+
+
+def restrict_rank_device(local_rank):
+    """Before torch is imported: this rank's HIP sees its own device only."""
+    os.environ['HIP_VISIBLE_DEVICES'] = rank_device(local_rank)
 
 
 def managed_bdfs(n_gpus):

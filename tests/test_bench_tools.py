@@ -297,6 +297,20 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
         assert line['config']['engine'] == 'cpu-mock'
 
 
+def test_rank_device_follows_the_rehearsal_ids_and_inherited_visibility():
+    """A torchrun rank other than 0 opens its own device only: its local
+    rank, its entry of BENCH_GPU_IDS on a one-box rehearsal, in the
+    numbering of an inherited HIP_VISIBLE_DEVICES."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.rank_device(3, env={}) == '3'
+    assert bench.rank_device(1, env={'BENCH_GPU_IDS': '0,0'}) == '0'
+    assert bench.rank_device(2, env={'BENCH_GPU_IDS': '4,5,6'}) == '6'
+    assert bench.rank_device(1, env={'HIP_VISIBLE_DEVICES': '2,3'}) == '3'
+    assert bench.rank_device(1, env={'HIP_VISIBLE_DEVICES': '6,7',
+                                     'BENCH_GPU_IDS': '0,0'}) == '6'
+
+
 def test_util_sampler_degrades_without_driver():
     from kiosk_autoscaler_amd.bench import gpu_util
     sampler = gpu_util.UtilSampler(0.01)
