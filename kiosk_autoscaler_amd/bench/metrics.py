@@ -187,7 +187,9 @@ def standby_split(events, t_lo, t_hi):
       recycle until the pool parks or retires it (``POOL_IDLE_RELEASE_S``);
     * ``exit_teardown_s`` -- from that exit command until the process is
       reaped (HIP context + communicator teardown: the GPU is held until
-      the process is gone);
+      the process is gone); where the process stamped its ``os._exit``
+      (``exiting_t``), ``exit_user_ms_mean`` is the command -> ``os._exit``
+      part and ``exit_kernel_ms_mean`` the kernel's teardown after it;
     * ``other_s`` -- a recycled worker reassigned, or a fresh standby that
       exited unassigned.
 
@@ -196,6 +198,7 @@ def standby_split(events, t_lo, t_hi):
     serving = set()     # pids assigned and not recycled since
     parts = collections.Counter()
     teardowns = []
+    user, kernel = [], []
     evs = sorted(events, key=lambda e: e.get('t', 0))
     # instants an exit command went to parked / retired standbys
     exit_cmds = sorted(e['t'] for e in evs if e.get('ev') in (
@@ -204,7 +207,7 @@ def standby_split(events, t_lo, t_hi):
     def clip(a, b):
         return max(0, min(b, t_hi) - max(a, t_lo))
 
-    def close(pid, t_end, closer):
+    def close(pid, t_end, closer, exiting=None):
         start, opener = open_at.pop(pid)
         if opener in ('drained', 'retired') and closer == 'exit':
             # a retired worker was told to exit at once (worker_retired);
@@ -217,6 +220,9 @@ def standby_split(events, t_lo, t_hi):
             parts['exit_teardown'] += clip(cmd, t_end)
             if t_lo <= cmd <= t_hi:
                 teardowns.append((t_end - cmd) / 1e9)
+                if exiting is not None and cmd <= exiting <= t_end:
+                    user.append((exiting - cmd) / 1e6)
+                    kernel.append((t_end - exiting) / 1e6)
         elif opener == 'fresh' and closer == 'assign':
             parts['hold_before_assign'] += clip(start, t_end)
         else:
@@ -244,7 +250,7 @@ def standby_split(events, t_lo, t_hi):
             if pid in open_at:
                 close(pid, e['t'], 'assign')
         elif ev == 'standby_exit' and pid in open_at:
-            close(pid, e['t'], 'exit')
+            close(pid, e['t'], 'exit', e.get('exiting_t'))
     for start, _ in open_at.values():
         parts['other'] += clip(start, t_hi)
     out = {k + '_s': parts[k] / 1e9 for k in (
@@ -253,6 +259,8 @@ def standby_split(events, t_lo, t_hi):
     out['exit_teardown_ms_mean'] = (1e3 * sum(teardowns) / len(teardowns)
                                     if teardowns else None)
     out['exit_teardowns'] = len(teardowns)
+    out['exit_user_ms_mean'] = sum(user) / len(user) if user else None
+    out['exit_kernel_ms_mean'] = sum(kernel) / len(kernel) if kernel else None
     return out
 
 

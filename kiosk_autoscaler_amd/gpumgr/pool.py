@@ -969,9 +969,24 @@ class PoolMixin(object):
                                  code=proc.popen.returncode)
         for proc in list(self.retiring):
             if proc.popen.poll() is not None:
+                exiting = self._exiting_t(proc)
                 proc.close()
                 self.retiring.remove(proc)
                 self.events.emit('standby_exit', pid=proc.pid, slot=proc.slot,
-                                 code=proc.popen.returncode, retired=True)
+                                 code=proc.popen.returncode, retired=True,
+                                 exiting_t=exiting)
                 retired = True
         return retired
+
+    @staticmethod
+    def _exiting_t(proc):
+        """When a retired process called ``os._exit`` (its last message,
+        ``exiting``): the rest of its exit is the kernel's teardown."""
+        t = None
+        try:
+            for message in proc.pipe.read_messages():
+                if message is not None and message.get('ev') == 'exiting':
+                    t = message.get('t')
+        except (OSError, AttributeError, ValueError):
+            return None
+        return t

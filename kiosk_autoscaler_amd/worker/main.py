@@ -516,14 +516,21 @@ def main(argv=None):
             break
         recycles += 1
         # the engine's HBM is already freed: report first, collect after
-        # (the collection runs while the process waits as a standby)
+        # (the collection runs while the process waits as a standby -- and
+        # not at all when the manager retires it at once: ``collect``)
         channel.emit('recycled', code=code, keys_done=runtime.keys_done,
                      recycles=recycles)
-        gc.collect()
         pin = {'gpu': assignment.get('gpu'), 'slot': assignment.get('slot'),
                'cpus': assignment.get('cpus'),
                'visible': assignment.get('visible')}
-        assignment = None
+        assignment = _wait_for_assignment(channel, pin, preload_ns, backend,
+                                          preinit, collect=True)
+        if assignment is None:
+            code = 0
+            break
+        if isinstance(assignment, int):
+            code = assignment
+            break
     _join_device_open()     # never exit under a running device open
     if backend == 'hip':
         try:
@@ -536,6 +543,9 @@ def main(argv=None):
     # so the GPU slot frees promptly.
     sys.stdout.flush()
     sys.stderr.flush()
+    # the manager times a retired process's exit from here to its reaping
+    # (the kernel's teardown) apart from its own command to here
+    channel.emit('exiting', t=time.monotonic_ns(), code=code)
     os._exit(code)
 
 
@@ -618,10 +628,19 @@ def _hbm_free(backend, preinit):
         return None
 
 
-def _wait_for_assignment(channel, pin, preload_ns, backend, preinit):
+# a recycled worker waits this long for the manager's verdict (``exit`` when
+# the pool parks on that pass) before it runs the garbage collection
+COLLECT_AFTER_S = 0.02
+
+
+def _wait_for_assignment(channel, pin, preload_ns, backend, preinit,
+                         collect=False):
     """Standby: report, then block until ``assign`` (or ``exit``/EOF).
     With ``ENGINE_IDLE_RELEASE_S`` a kept engine is freed after that long
-    without an assignment (``engine_released``, with the new free HBM)."""
+    without an assignment (``engine_released``, with the new free HBM).
+    ``collect`` (a recycled worker): run ``gc.collect`` once no command came
+    within ``COLLECT_AFTER_S`` -- a worker retired at once exits without
+    it (a full collection of a PyTorch process is standby GPU time)."""
     from .channel import TIMEOUT
     pci = _device_pci(backend, preinit)
     if pci:
@@ -635,7 +654,13 @@ def _wait_for_assignment(channel, pin, preload_ns, backend, preinit):
         release_s = 0.0
     while True:
         timeout = release_s if release_s > 0 and _ENGINES else None
+        if collect:
+            timeout = COLLECT_AFTER_S
         message = channel.read_command(timeout=timeout)
+        if message is TIMEOUT and collect:
+            collect = False
+            gc.collect()
+            continue
         if message is TIMEOUT:
             released = _drop_cached_engines()
             channel.emit('engine_released', released_bytes=released,

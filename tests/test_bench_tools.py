@@ -190,11 +190,15 @@ def test_standby_split_parts_sum_to_the_total():
     retired = [
         _ev('worker_retired', 5.0, pid=3),
         _ev('pool_parked', 5.01),
-        _ev('standby_exit', 5.15, pid=3),
+        _ev('standby_exit', 5.15, pid=3, exiting_t=int(5.02e9)),
     ]
     split = metrics.standby_split(retired, 0, int(20e9))
     assert split['park_delay_s'] == 0
     assert split['exit_teardown_s'] == pytest.approx(0.15)
+    # the process's os._exit stamp splits its exit: 20 ms in the worker,
+    # 130 ms of the kernel's teardown
+    assert split['exit_user_ms_mean'] == pytest.approx(20.0)
+    assert split['exit_kernel_ms_mean'] == pytest.approx(130.0)
 
 
 def test_idle_queue_reads_per_second():

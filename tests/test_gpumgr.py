@@ -475,8 +475,13 @@ def test_pool_parks_after_idle_and_refills_on_demand(resp_server):
         until(lambda: not manager.standbys and not manager.retiring)
         assert client.get('kiosk:pool').split()[:2] == ['0', '0']
         assert client.get('kiosk:pool').split()[3] == '1'     # parked
-        # the retired standby's GPU time is closed in the metrics
+        # the retired standby's GPU time is closed in the metrics, and its
+        # last message stamped its os._exit (the kernel's teardown after it)
         until(lambda: 'standby_exit' in kinds())
+        exits = [e for e in events.records if e['ev'] == 'standby_exit' and
+                 e.get('retired')]
+        assert exits and all(isinstance(e.get('exiting_t'), int) and
+                             e['exiting_t'] <= e['t'] for e in exits)
         client.hset('predict:k', mapping={'status': 'new'})
         client.lpush('predict', 'predict:k')
         manager.patch_namespaced_deployment('park', 'default',

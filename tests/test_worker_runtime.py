@@ -511,3 +511,39 @@ def test_channel_cap_is_decided_without_importing_the_plugin(monkeypatch,
     assert worker_main._engine_collectives() is False
     monkeypatch.delenv('WORKER_ENGINE')
     assert worker_main._engine_collectives() is False
+
+
+def test_recycled_worker_retired_at_once_skips_the_collection(monkeypatch):
+    """A recycled worker runs ``gc.collect`` only once no command came
+    within ``COLLECT_AFTER_S``: one the manager retires on that pass exits
+    without it (a PyTorch process's full collection is standby GPU time)."""
+    from kiosk_autoscaler_amd.worker import main as wmain
+    from kiosk_autoscaler_amd.worker.channel import TIMEOUT
+    collected = []
+    monkeypatch.setattr(wmain.gc, 'collect', lambda: collected.append(1))
+
+    class FakeChannel(object):
+        def __init__(self, replies):
+            self.replies = list(replies)
+            self.timeouts = []
+            self.emitted = []
+            self.device_reported = False
+
+        def emit(self, ev, **fields):
+            self.emitted.append(ev)
+
+        def read_command(self, timeout=None):
+            self.timeouts.append(timeout)
+            return self.replies.pop(0)
+
+    exit_now = FakeChannel([{'cmd': 'exit'}])
+    assert wmain._wait_for_assignment(exit_now, None, 0, 'cpu', {},
+                                      collect=True) is None
+    assert collected == [] and exit_now.emitted == ['standby']
+    assert exit_now.timeouts == [wmain.COLLECT_AFTER_S]
+    # kept as a standby: collected once, then it blocks as before
+    kept = FakeChannel([TIMEOUT, {'cmd': 'assign', 'gpu': None}])
+    assert wmain._wait_for_assignment(kept, None, 0, 'cpu', {},
+                                      collect=True)['cmd'] == 'assign'
+    assert collected == [1]
+    assert kept.timeouts == [wmain.COLLECT_AFTER_S, None]
