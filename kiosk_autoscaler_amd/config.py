@@ -197,6 +197,11 @@ EXTRA_DEFAULTS = (
     # RCCL sees its peers), auto (isolate; visible from the next spawns on
     # once a multi-rank generation reports a non-xGMI peer path)
     ('WORKER_PIN', str, 'auto'),
+    # hardware queues per worker process (GPU_MAX_HW_QUEUES in its
+    # environment; 0 = HIP's own, 4): each queue pins a 173 MB host
+    # context-save area on MI355X, allocated at the queue's first use and
+    # freed page by page at the process's exit (profiles/r6_hw_queues)
+    ('WORKER_HW_QUEUES', int, 0),
     ('METRICS_PORT', str, '0'),             # Prometheus [addr:]port (0 = off)
     ('LOG_FILE', str, 'autoscaler.log'),
 )

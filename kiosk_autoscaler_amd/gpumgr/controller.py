@@ -174,7 +174,7 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                  fence_fallback='shm', fence_fallback_after=2,
                  fence_init_timeout=12.0, fence_transport=None,
                  zygote=False, pool_wake_poll_s=0.0, pool_wake_hold_s=0.0,
-                 pool_wake_lead_s=0.0, pin_mode='auto'):
+                 pool_wake_lead_s=0.0, pin_mode='auto', hw_queues=0):
         self.slots = list(slots)
         self.redis = redis_client
         self.state_ttl = int(state_ttl)
@@ -202,6 +202,12 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                              'got %r' % (pin_mode,))
         self.pin_auto = pin_mode == 'auto'
         self.pin_mode = 'visible' if pin_mode == 'visible' else 'isolate'
+        # WORKER_HW_QUEUES: GPU_MAX_HW_QUEUES of every process it spawns
+        # (0 = leave the environment's)
+        if int(hw_queues or 0) < 0 or int(hw_queues or 0) > 32:
+            raise ValueError('WORKER_HW_QUEUES must be 0..32, got %r'
+                             % (hw_queues,))
+        self.hw_queues = int(hw_queues or 0)
         self._init_pool(pool_size, pool_template, pool_mode, recycle,
                         pool_idle_release_s, pool_wake_poll_s,
                         pool_wake_hold_s, pool_wake_lead_s, zygote)

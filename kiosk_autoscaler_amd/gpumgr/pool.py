@@ -93,6 +93,9 @@ class PoolMixin(object):
 
     def _environment(self, template):
         env = dict(os.environ)
+        if getattr(self, 'hw_queues', 0):
+            # WORKER_HW_QUEUES (a template's own setting still wins)
+            env['GPU_MAX_HW_QUEUES'] = str(self.hw_queues)
         env.update({k: str(v) for k, v in template.env.items()})
         # the RCCL library the node ladder is on now: loaded first by a new
         # process's preload (the manager's own environment stays as it was)

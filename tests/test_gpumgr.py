@@ -81,6 +81,30 @@ def test_pin_modes_select_the_device():
     assert 'HIP_VISIBLE_DEVICES' not in env and device_ordinal(env) == 0
 
 
+def test_worker_hw_queues_reach_the_spawn_environment(monkeypatch):
+    """WORKER_HW_QUEUES sets GPU_MAX_HW_QUEUES for every process the
+    manager spawns, over the manager's own environment; a template's own
+    setting wins; 0 leaves the environment's."""
+    from kiosk_autoscaler_amd.gpumgr.gpus import GpuSlot
+    from kiosk_autoscaler_amd.gpumgr.process import WorkerTemplate
+    monkeypatch.setenv('GPU_MAX_HW_QUEUES', '4')
+    slots = [GpuSlot(0, '0')]
+    tpl = WorkerTemplate(module='kiosk_autoscaler_amd.worker.main')
+    manager = gpumgr.GpuManager(slots, hw_queues=2)
+    assert manager._environment(tpl)['GPU_MAX_HW_QUEUES'] == '2'
+    own = WorkerTemplate(module='kiosk_autoscaler_amd.worker.main',
+                         env={'GPU_MAX_HW_QUEUES': '1'})
+    assert manager._environment(own)['GPU_MAX_HW_QUEUES'] == '1'
+    assert gpumgr.GpuManager(slots)._environment(tpl)[
+        'GPU_MAX_HW_QUEUES'] == '4'
+    with pytest.raises(ValueError):
+        gpumgr.GpuManager(slots, hw_queues=64)
+    from kiosk_autoscaler_amd.config import Config, Settings
+    s = Settings(Config(environ={'WORKER_HW_QUEUES': '2', 'RESOURCE_NAME': 'w'},
+                        use_files=False))
+    assert s.WORKER_HW_QUEUES == 2
+
+
 def test_manager_switches_to_visible_pin_on_a_non_p2p_peer_path():
     """WORKER_PIN=auto: a multi-rank generation whose RCCL reports a peer
     path other than xGMI P2P moves the manager to the visible pin: the

@@ -16,6 +16,9 @@ Cases: ``ctx`` (HIP context + stream), ``engine`` (+ the production engine,
 before the exit; ``teardown_ms``), ``rccl`` (context + communicator, no
 engine).  One JSON line per case; ``EXIT_PROBE_TAG`` is copied into it
 (environment variants of one case, run one process each).
+``torch_engine_rccl_reset`` / ``_hsashut``: ``hipDeviceReset`` /
+``hsa_shut_down`` after ``go``, before the exit (does a user-space
+teardown shorten the kernel's?).
 """
 import json
 import os
@@ -27,7 +30,7 @@ sys.path.insert(0, ROOT)
 
 CASES = ('ctx', 'engine', 'engine_rccl', 'engine_free', 'torch_engine_rccl',
          'engine_rccl_abort', 'engine_rccl_destroy', 'rccl', 'streams_2',
-         'streams_hi_2')
+         'streams_hi_2', 'torch_engine_rccl_reset', 'torch_engine_rccl_hsashut')
 
 
 def child(case, mod, wfd, rfd):
@@ -75,7 +78,7 @@ def child(case, mod, wfd, rfd):
         free, total = mod.mem_info()
         info['rccl_hbm_mb'] = (total - free - before) / 1e6
         keep.append(fence)
-    if case.endswith(('_abort', '_destroy')):
+    if case.endswith(('_abort', '_destroy', '_reset', '_hsashut')):
         # timed in the child just before its exit: what the comm's own
         # teardown costs against the kernel's at exit
         info['teardown'] = case.rsplit('_', 1)[1]
@@ -89,7 +92,16 @@ def child(case, mod, wfd, rfd):
     os.read(rfd, 1)            # go
     if 'teardown' in info:
         t0 = time.monotonic_ns()
-        getattr(keep[-1], info['teardown'])()
+        if info['teardown'] == 'reset':
+            # the HIP runtime frees its device state in user space first
+            import ctypes
+            ctypes.CDLL('libamdhip64.so').hipDeviceReset()
+        elif info['teardown'] == 'hsashut':
+            # ROCr's own teardown (queues, signals, memory) before the exit
+            import ctypes
+            ctypes.CDLL('libhsa-runtime64.so.1').hsa_shut_down()
+        else:
+            getattr(keep[-1], info['teardown'])()
         os.write(wfd, ('%.3f\n' % ((time.monotonic_ns() - t0) / 1e6)).encode())
     os._exit(0)
 
@@ -116,6 +128,32 @@ def _memory(pid):
     except (OSError, ValueError):
         pass
     return out
+
+
+def _smaps(pid, top=10):
+    """``EXIT_PROBE_SMAPS=1``: the child's largest anonymous mappings
+    (what its exit frees page by page), with their THP share."""
+    rows = []
+    cur = None
+    try:
+        with open('/proc/%d/smaps' % pid) as f:
+            for line in f:
+                parts = line.split()
+                if '-' in parts[0] and not parts[0].endswith(':'):
+                    lo, hi = (int(x, 16) for x in parts[0].split('-'))
+                    cur = {'name': parts[5] if len(parts) > 5 else '[anon]',
+                           'perm': parts[1], 'size_mb': (hi - lo) >> 20,
+                           'anon_mb': 0, 'thp_mb': 0}
+                    rows.append(cur)
+                elif parts[0] == 'Anonymous:' and cur is not None:
+                    cur['anon_mb'] = int(parts[1]) >> 10
+                elif parts[0] == 'AnonHugePages:' and cur is not None:
+                    cur['thp_mb'] = int(parts[1]) >> 10
+    except OSError:
+        return None
+    rows.sort(key=lambda r: -r['anon_mb'])
+    total = sum(r['anon_mb'] for r in rows)
+    return {'anon_mb': total, 'mappings': len(rows), 'top': rows[:top]}
 
 
 def _wait_sampling(pid):
@@ -183,6 +221,8 @@ def main():
             time.sleep(0.2)
             threads = _threads(pid)
             info['mem'] = _memory(pid)
+            if os.environ.get('EXIT_PROBE_SMAPS') == '1':
+                info['smaps'] = _smaps(pid)
             t0 = time.monotonic_ns()
             os.write(go_w, b'g')
             status, where = _wait_sampling(pid)
@@ -197,6 +237,11 @@ def main():
             print(json.dumps(info), flush=True)
             os.close(up_r)
             os.close(go_w)
+            if os.WIFSIGNALED(status):
+                # a child that died by a signal: nothing more on the GPU
+                print(json.dumps({'stopped': case, 'signal':
+                                  os.WTERMSIG(status)}), flush=True)
+                return 3
             time.sleep(0.3)
     return 0
 
