@@ -198,10 +198,12 @@ EXTRA_DEFAULTS = (
     # once a multi-rank generation reports a non-xGMI peer path)
     ('WORKER_PIN', str, 'auto'),
     # hardware queues per worker process (GPU_MAX_HW_QUEUES in its
-    # environment; 0 = HIP's own, 4): each queue pins a 173 MB host
-    # context-save area on MI355X, allocated at the queue's first use and
-    # freed page by page at the process's exit (profiles/r6_hw_queues)
-    ('WORKER_HW_QUEUES', int, 0),
+    # environment; 0 = the environment's, HIP's default 4): on MI355X each
+    # queue adds a fully resident 173 MB anonymous host mapping, which the
+    # process's exit frees page by page; 2 exit ~11 ms faster than 4, and 1
+    # would put every stream, the fence's too, in one FIFO
+    # (profiles/r6_hw_queues)
+    ('WORKER_HW_QUEUES', int, 2),
     ('METRICS_PORT', str, '0'),             # Prometheus [addr:]port (0 = off)
     ('LOG_FILE', str, 'autoscaler.log'),
 )

@@ -82,9 +82,9 @@ def test_pin_modes_select_the_device():
 
 
 def test_worker_hw_queues_reach_the_spawn_environment(monkeypatch):
-    """WORKER_HW_QUEUES sets GPU_MAX_HW_QUEUES for every process the
-    manager spawns, over the manager's own environment; a template's own
-    setting wins; 0 leaves the environment's."""
+    """WORKER_HW_QUEUES (default 2) sets GPU_MAX_HW_QUEUES for every
+    process the manager spawns, over the manager's own environment; a
+    template's own setting wins; 0 leaves the environment's."""
     from kiosk_autoscaler_amd.gpumgr.gpus import GpuSlot
     from kiosk_autoscaler_amd.gpumgr.process import WorkerTemplate
     monkeypatch.setenv('GPU_MAX_HW_QUEUES', '4')
@@ -103,6 +103,8 @@ def test_worker_hw_queues_reach_the_spawn_environment(monkeypatch):
     s = Settings(Config(environ={'WORKER_HW_QUEUES': '2', 'RESOURCE_NAME': 'w'},
                         use_files=False))
     assert s.WORKER_HW_QUEUES == 2
+    s = Settings(Config(environ={'RESOURCE_NAME': 'w'}, use_files=False))
+    assert s.WORKER_HW_QUEUES == 2          # the default
 
 
 def test_manager_switches_to_visible_pin_on_a_non_p2p_peer_path():
