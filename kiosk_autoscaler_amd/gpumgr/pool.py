@@ -771,6 +771,10 @@ class PoolMixin(object):
         if self.node is not None and message.get('ev') in NODE_EVENTS:
             self.node.on_message(proc, message)
             return
+        if any(p is proc for p in self.retiring):
+            # a process retired on its 'recycled' report still sends the
+            # 'standby' of its recycle in the same batch: it is no standby
+            return
         if message.get('ev') == 'engine_released':
             proc.engine_cached = False
             proc.hbm_free = message.get('hbm_free')

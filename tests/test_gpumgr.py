@@ -1207,3 +1207,30 @@ def test_drained_worker_retires_at_once_when_the_pool_parks_anyway():
         ._parks_on_recycle()
     assert not gpumgr.GpuManager([], pool_idle_release_s=0)\
         ._parks_on_recycle()
+
+
+def test_retired_process_standby_report_is_ignored():
+    """A worker retired on its 'recycled' report sends the 'standby' of its
+    recycle in the same batch (it reports before it waits for the verdict):
+    the manager neither counts it as a booted standby nor checks its
+    device again."""
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    events = EventLog(source='test')
+    events.keep = True
+    manager = gpumgr.GpuManager([], events=events)
+
+    class Proc(object):
+        pid = 7
+        slot = 0
+        role = 'worker'
+        woken = False
+        booted = False
+        t_spawn = 0
+        engine_cached = True
+
+    proc = Proc()
+    manager.retiring.append(proc)
+    manager._on_standby_message(proc, {'ev': 'standby', 'pci': '0000:01:00.0',
+                                       'engine_cached': False})
+    assert not [e for e in events.records if e['ev'] == 'standby_ready']
+    assert manager.retiring == [proc] and proc.booted is False

@@ -20,17 +20,28 @@ CAP_S = 0.75
 
 
 def boots_of(path):
-    """Spawn -> booted+prebuilt of each fresh standby in one event log."""
+    """Spawn -> booted+prebuilt of each fresh standby a wake started in one
+    event log: after the pool first parked (the pool's first boot and cold
+    spawns are not wakes)."""
     out = []
+    events = []
     with open(path) as fh:
         for line in fh:
             try:
-                ev = json.loads(line)
+                events.append(json.loads(line))
             except ValueError:
                 continue
-            if ev.get('ev') == 'standby_ready' and ev.get('boot_s') and \
-                    not ev.get('recycled'):
-                out.append(float(ev['boot_s']))
+    parked = False
+    retired = set()     # (logs of 184647d..: a retired worker's report)
+    for ev in sorted(events, key=lambda e: e.get('t', 0)):
+        if ev.get('ev') == 'pool_parked':
+            parked = True
+        elif ev.get('ev') == 'worker_retired':
+            retired.add(ev.get('pid'))
+        elif parked and ev.get('ev') == 'standby_ready' and \
+                ev.get('boot_s') and not ev.get('recycled') and \
+                ev.get('pid') not in retired:
+            out.append(float(ev['boot_s']))
     return out
 
 
