@@ -819,6 +819,11 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         'gpu_alive_s': _r(summary['gpu_alive_s']),
         'gpu_busy_s': _r(summary['gpu_busy_s']),
         'gpu_idle_incl_standby_pct': _r(summary['gpu_idle_incl_standby_pct']),
+        # the woken standbys' boots (spawn -> booted), which the standby
+        # time above does not include, and the idle share counting them too
+        'standby_boot_gpu_s': _r(summary['boot_gpu_s']),
+        'gpu_idle_incl_standby_and_boot_pct': _r(
+            summary['gpu_idle_incl_standby_and_boot_pct']),
         # what that standby time holds: HBM only, no kernels (amdsmi device
         # VRAM over the pre-run baseline, per GPU: fresh pool, and the
         # median while no worker is alive -- recycled standbys keep their

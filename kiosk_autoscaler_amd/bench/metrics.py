@@ -177,6 +177,26 @@ def standby_gpu(events, t_lo, t_hi):
     return standby_split(events, t_lo, t_hi)['total_s']
 
 
+def boot_gpu(events, t_lo, t_hi):
+    """Seconds fresh standbys spent booting inside ``[t_lo, t_hi]``: from
+    ``process_spawn`` (an embryo handed its pin; its HIP context opens
+    ~15 ms later) to its ``standby_ready``.  Not part of
+    :func:`standby_split`, which starts at the boot's end; reported beside
+    it so the GPU time of a wake is complete."""
+    spawned = {}
+    total = 0
+    for e in sorted(events, key=lambda e: e.get('t', 0)):
+        ev = e.get('ev')
+        pid = e.get('pid')
+        if ev == 'process_spawn' and pid is not None:
+            spawned[pid] = e['t']
+        elif ev == 'standby_ready' and pid in spawned and \
+                not e.get('recycled'):
+            start = spawned.pop(pid)
+            total += max(0, min(e['t'], t_hi) - max(start, t_lo))
+    return total / 1e9
+
+
 def standby_split(events, t_lo, t_hi):
     """:func:`standby_gpu`, split by what the held time was (VERDICT r5
     weak 1):
@@ -580,12 +600,18 @@ def summarize(events, episodes):
     split = standby_split(events, t_lo, t_hi)
     standby_s = split['total_s']
     held = alive_s + standby_s
+    boot_s = boot_gpu(events, t_lo, t_hi)
     return {
         'standby_gpu_s': standby_s,
         'standby_split': split,
         # idle share if standby-held GPU time counted as alive-and-idle
         'gpu_idle_incl_standby_pct': (100.0 * (held - busy_s) / held
                                       if held > 0 else None),
+        # ... and the woken standbys' boots too
+        'boot_gpu_s': boot_s,
+        'gpu_idle_incl_standby_and_boot_pct': (
+            100.0 * (held + boot_s - busy_s) / (held + boot_s)
+            if held + boot_s > 0 else None),
         'latency_mean_s': _mean(lat),
         'cold_starts': len(lat),
         'first_key_latency_mean_s': _mean(first),

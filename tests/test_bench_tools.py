@@ -201,6 +201,22 @@ def test_standby_split_parts_sum_to_the_total():
     assert split['exit_kernel_ms_mean'] == pytest.approx(130.0)
 
 
+def test_boot_gpu_counts_fresh_standby_boots_only():
+    """A woken standby's boot (spawn -> standby_ready) is GPU time the
+    standby split does not hold: reported beside it; a recycled worker's
+    report is not a boot."""
+    events = [
+        _ev('process_spawn', 1.0, pid=1),
+        _ev('standby_ready', 1.06, pid=1, preinit={'x': 1}),
+        _ev('process_spawn', 4.95, pid=2),
+        _ev('standby_ready', 5.01, pid=2, preinit={'x': 1}),   # half in
+        _ev('standby_ready', 8.0, pid=1, recycled=True),
+    ]
+    assert metrics.boot_gpu(events, 0, int(20e9)) == pytest.approx(0.12)
+    assert metrics.boot_gpu(events, int(4.98e9), int(20e9)) == \
+        pytest.approx(0.03)
+
+
 def test_idle_queue_reads_per_second():
     events = [
         _ev('pool_parked', 1.0, queue_reads=100, queue_reads_fine=10),
