@@ -844,6 +844,10 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
             (hbm or {}).get('idle_last_mib') - (hbm or {}).get('idle_first_mib')
             if (hbm or {}).get('idle_last_mib') is not None and
             (hbm or {}).get('idle_first_mib') is not None else None, 1),
+        # the samples it compares: 'parked' (pool parked, no process of the
+        # run on the device) or 'idle' (no worker alive; a run that never
+        # parked)
+        'idle_node_hbm_drift_over': (hbm or {}).get('drift_over'),
         'cold_starts': summary['cold_starts'],
         'first_key_latency_mean_s': _r(summary['first_key_latency_mean_s']),
         'latency_p50_s': _r(summary['latency_p50_s']),

@@ -312,6 +312,11 @@ def idle_queue_reads(events, queues=1):
             'inside_window_reads': int(fine)}
 
 
+# a parked pool's first 0.3 s: the retired standbys' memory is still being
+# freed (their exit teardown, ~90 ms, plus the sampler's period)
+PARK_SETTLE_NS = 300_000_000
+
+
 def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
     """What the node holds in HBM, by phase (the memory behind
     ``standby_gpu_s``; a standby runs no kernels, so HBM is all it holds).
@@ -340,6 +345,25 @@ def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
 
     def serving(t):
         return any(a <= t <= b for a, b in spans)
+    # parked pool (``pool_parked`` -> ``pool_resumed``, past PARK_SETTLE_NS
+    # for the retired processes to free): no process of the run on the
+    # device.  The leak check compares these samples only -- an idle sample
+    # with a standby holding a prebuilt engine (job mode's wait for
+    # KEYS_PER_POD keys) is not drift.
+    parked_spans = []
+    park_at = None
+    for e in sorted(events, key=lambda e: e.get('t', 0)):
+        if e.get('ev') == 'pool_parked' and park_at is None:
+            park_at = e['t'] + PARK_SETTLE_NS
+        elif e.get('ev') == 'pool_resumed' and park_at is not None:
+            if e['t'] > park_at:
+                parked_spans.append((park_at, e['t']))
+            park_at = None
+    if park_at is not None:
+        parked_spans.append((park_at, t_hi))
+
+    def parked(t):
+        return any(a <= t <= b for a, b in parked_spans)
     # ENGINE_IDLE_RELEASE_S: idle samples taken after the standby freed its
     # kept engine (an ``engine_released`` since the last worker exit)
     releases = sorted(e['t'] for e in events
@@ -355,6 +379,7 @@ def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
         base = {}      # the "baseline" held memory the run later did not
     idle, busy, idle_released = [], [], []
     idle_timed = []     # (t, MiB): leak check over a long run
+    parked_timed = []
     for bdf, samples in device.items():
         zero = base.get(bdf, 0.0)
         for t, used in samples:
@@ -363,11 +388,16 @@ def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
                 (busy if on else idle).append(used - zero)
                 if not on:
                     idle_timed.append((t, used - zero))
+                    if parked(t):
+                        parked_timed.append((t, used - zero))
                 if not on and releases and released(t):
                     idle_released.append(used - zero)
     idle_timed.sort()
-    first = [v for _, v in idle_timed[:10]]
-    last = [v for _, v in idle_timed[-10:]]
+    parked_timed.sort()
+    # leak check over the parked samples when there are any
+    drift_timed = parked_timed or idle_timed
+    first = [v for _, v in drift_timed[:10]]
+    last = [v for _, v in drift_timed[-10:]]
     totals = [v for v in ((vram or {}).get('total_mib') or {}).values() if v]
     total = max(totals) if totals else None
     boot = None
@@ -383,11 +413,14 @@ def hbm_hold(events, vram, t_lo, t_hi, baseline=None, pool_boot=None):
                             if idle_mib is not None and total else None),
         'hbm_total_mib': total,
         'idle_released_mib_median': _pct(idle_released, 0.5),
-        # median of the first / last 10 idle samples (HBM drift of the run)
+        # median of the first / last 10 parked samples (idle ones without
+        # a parked span): the HBM drift of the run
         'idle_first_mib': _pct(first, 0.5),
         'idle_last_mib': _pct(last, 0.5),
+        'drift_over': 'parked' if parked_timed else 'idle',
         'samples': {'idle': len(idle), 'serving': len(busy),
-                    'idle_released': len(idle_released)},
+                    'idle_released': len(idle_released),
+                    'parked': len(parked_timed)},
         'over_baseline': bool(base),
     }
 

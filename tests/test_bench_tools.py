@@ -418,7 +418,9 @@ def test_hbm_hold_splits_device_vram_by_phase():
             'total_mib': {'bdf': 294912.0}}
     out = metrics.hbm_hold(events, vram, 0, 1000, baseline={'bdf': 300.0},
                            pool_boot={'bdf': 800.0})
-    assert out['samples'] == {'idle': 3, 'serving': 1, 'idle_released': 0}
+    assert out['samples'] == {'idle': 3, 'serving': 1, 'idle_released': 0,
+                              'parked': 0}
+    assert out['drift_over'] == 'idle'
     assert out['idle_released_mib_median'] is None
     assert out['pool_boot_mib'] == 500.0
     assert out['idle_mib_median'] == 2600.0
@@ -440,6 +442,39 @@ def test_hbm_hold_splits_device_vram_by_phase():
     assert out['idle_released_mib_median'] == 2600.0
     # a standby that exited stops counting toward standby_gpu_s
     assert metrics.standby_gpu(events, 0, 1000) == (100 + 100) / 1e9
+
+
+def test_hbm_drift_compares_parked_samples_only():
+    """Job mode: a woken standby holds its prebuilt engine while the queue
+    fills to KEYS_PER_POD (no worker alive, 2.5 GB).  The leak check
+    compares parked-pool samples, so that hold is not reported as -2.5 GB
+    of drift; a run that never parked falls back to the idle samples."""
+    from kiosk_autoscaler_amd.bench import metrics
+    s = 1_000_000_000
+    events = [
+        {'ev': 'pool_resumed', 't': 1 * s},          # woken, prebuilds
+        {'ev': 'worker_assigned', 't': 4 * s, 'worker': 'w0'},
+        {'ev': 'worker_exit', 't': 6 * s, 'worker': 'w0'},
+        {'ev': 'pool_parked', 't': 6 * s},
+        {'ev': 'pool_resumed', 't': 9 * s},
+        {'ev': 'pool_parked', 't': 12 * s},
+    ]
+    # standby with its engine at 2-3 s, the exit still freeing at 6.1 s,
+    # parked at 7-8 s and 13-14 s
+    samples = [(2 * s, 2518.0), (3 * s, 2518.0), (5 * s, 2600.0),
+               (6 * s + 100_000_000, 2000.0), (7 * s, 1.0), (8 * s, 1.0),
+               (10 * s, 2518.0), (13 * s, 1.0), (14 * s, 1.0)]
+    vram = {'device': {'bdf': samples}, 'total_mib': {'bdf': 294912.0}}
+    out = metrics.hbm_hold(events, vram, 0, 15 * s)
+    assert out['drift_over'] == 'parked'
+    assert out['samples']['parked'] == 4
+    assert out['idle_first_mib'] == 1.0 and out['idle_last_mib'] == 1.0
+    # the unparked idle samples still count toward the idle median
+    assert out['samples']['idle'] == 8
+    never_parked = [e for e in events if e['ev'] != 'pool_parked']
+    out = metrics.hbm_hold(never_parked, vram, 0, 15 * s)
+    assert out['drift_over'] == 'idle' and out['samples']['parked'] == 0
+    assert out['idle_first_mib'] > 1.0     # the standby's hold counts again
 
 
 def test_bench_tick_inproc_runs():
