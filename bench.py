@@ -868,6 +868,10 @@ def report(svc, gen, args, episodes, elapsed, util, sampler, budget):
         'pool_arrival_wakes': sum(1 for e in events
                                   if e.get('ev') == 'pool_resumed' and
                                   e.get('reason') == 'arrival'),
+        # arrival wakes skipped: the next tick would not scale for the keys
+        # waiting (KEYS_PER_POD under the reference's floor division)
+        'pool_wake_deferrals': sum(1 for e in events
+                                   if e.get('ev') == 'wake_deferred'),
         'cold_spawned_workers': sum(1 for e in events
                                     if e.get('ev') == 'worker_assigned' and
                                     e.get('from_pool') is False),

@@ -177,7 +177,8 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
                          pool_wake_hold_s=1.5 * float(settings.INTERVAL) + 1.0,
                          pool_wake_lead_s=settings.POOL_WAKE_LEAD_S,
                          pin_mode=settings.WORKER_PIN,
-                         hw_queues=settings.WORKER_HW_QUEUES)
+                         hw_queues=settings.WORKER_HW_QUEUES,
+                         scale_policy=getattr(settings, 'policy', None))
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

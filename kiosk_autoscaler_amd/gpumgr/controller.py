@@ -174,7 +174,8 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
                  fence_fallback='shm', fence_fallback_after=2,
                  fence_init_timeout=12.0, fence_transport=None,
                  zygote=False, pool_wake_poll_s=0.0, pool_wake_hold_s=0.0,
-                 pool_wake_lead_s=0.0, pin_mode='auto', hw_queues=0):
+                 pool_wake_lead_s=0.0, pin_mode='auto', hw_queues=0,
+                 scale_policy=None):
         self.slots = list(slots)
         self.redis = redis_client
         self.state_ttl = int(state_ttl)
@@ -208,6 +209,10 @@ class GpuManager(PoolMixin, FencingMixin, StateMixin):
             raise ValueError('WORKER_HW_QUEUES must be 0..32, got %r'
                              % (hw_queues,))
         self.hw_queues = int(hw_queues or 0)
+        # the autoscaler's SCALE_POLICY ('reference' | 'strict'): an arrival
+        # wakes a parked pool only for keys the next tick will scale for
+        # (None: any arrival wakes it)
+        self.wake_policy = scale_policy
         self._init_pool(pool_size, pool_template, pool_mode, recycle,
                         pool_idle_release_s, pool_wake_poll_s,
                         pool_wake_hold_s, pool_wake_lead_s, zygote)

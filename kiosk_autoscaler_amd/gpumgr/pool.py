@@ -14,6 +14,7 @@ import os
 import subprocess
 import time
 
+from .. import policy
 from .nodecomm import NODE_EVENTS
 from .process import (DRAINING, EXITED, ManagedProcess, Pipe,
                       bare_worker)
@@ -51,6 +52,9 @@ class PoolMixin(object):
         # the lead adapts to it (wake_lead)
         self._wake_boots = collections.deque(maxlen=16)
         self._wake_at = None      # a deferred arrival wake
+        self.wake_deferrals = 0   # wakes skipped: the tick would not scale
+        if not hasattr(self, 'wake_policy'):
+            self.wake_policy = None
         self._spawn_at = None     # a deferred standby spawn (awake pool)
         self._park_at = None      # when an idle pool is due to park
         self._next_arrival_check = 0.0
@@ -524,6 +528,15 @@ class PoolMixin(object):
                 self._wake_at = wake_at
         if self._wake_at is not None and now >= self._wake_at:
             self._wake_at = None
+            if self.pool_parked and not self._tick_would_scale():
+                # KEYS_PER_POD: the reference's floor division does not
+                # scale for these keys; a standby woken for them would hold
+                # its GPU (context, prebuilt engine) for the whole wake
+                # hold.  The next arrival re-arms the wake.
+                self.wake_deferrals += 1
+                self.events.emit('wake_deferred', waiting=self._waiting,
+                                 policy=self.wake_policy)
+                return False
             self._last_demand = now
             self._wake_until = now + self.pool_wake_hold_s
             if self.pool_parked:
@@ -715,6 +728,28 @@ class PoolMixin(object):
             self.events.emit('arrival', queues=grown,
                              parked=self.pool_parked)
         return bool(grown)
+
+    def _tick_would_scale(self):
+        """Whether the next tick scales up for the keys waiting now: the
+        autoscaler's policy (``wake_policy``) from zero replicas, per managed
+        resource over its queues and KEYS_PER_POD.  Under ``reference`` one
+        key below KEYS_PER_POD scales nothing (floor division per queue,
+        ``/root/reference/autoscaler/autoscaler.py:217``); under ``strict``
+        any key does.  True without a known policy or a reading (wake, as
+        before).  One pipelined LLEN per queue."""
+        if self.wake_policy not in policy.POLICIES or not self.resources:
+            return True
+        lengths = self._queue_lengths()
+        if lengths is None:
+            return True
+        self._waiting = sum(lengths.values())
+        for resource in self.resources.values():
+            keys = {q: lengths.get(q, 0) for q in resource.template.queues}
+            kpp = max(1, int(resource.template.keys_per_pod or 1))
+            if policy.decide(keys, 0, 1 << 30, kpp, 0,
+                             policy=self.wake_policy) > 0:
+                return True
+        return False
 
     def _take_standby(self, template, slot):
         """The standby pinned to ``slot`` (booted or still booting: it

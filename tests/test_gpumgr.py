@@ -677,6 +677,69 @@ def test_arrival_wake_waits_for_the_lead_before_the_tick(resp_server):
         manager.stop()
 
 
+@pytest.mark.parametrize('scale_policy', ['reference', 'strict'])
+def test_arrival_wake_waits_for_keys_the_tick_scales_for(resp_server,
+                                                         scale_policy):
+    """KEYS_PER_POD=3: under the reference policy one key is stranded by the
+    floor division (``/root/reference/autoscaler/autoscaler.py:217``), so
+    the wake it armed is deferred and the pool stays parked -- a woken
+    standby would hold its GPU through the whole wake hold for nothing
+    (job mode: 2.5 s a wake, profiles/r6_job).  The third key wakes it.
+    Under ``strict`` (ceiling division) the first key already does."""
+    import time
+    from kiosk_autoscaler_amd.config import Config, Settings
+    from kiosk_autoscaler_amd.redisq import StrictRedis
+    from kiosk_autoscaler_amd.utils.events import EventLog
+    env = {'REDIS_HOST': resp_server.host, 'REDIS_PORT': str(resp_server.port),
+           'QUEUES': 'predict', 'RESOURCE_NAME': 'kpp', 'MAX_PODS': '1',
+           'WORKER_BACKEND': 'cpu', 'WARM_POOL': '1', 'FENCE': 'none',
+           'REDIS_INTERVAL': '0', 'POOL_IDLE_RELEASE_S': '0.2',
+           'POOL_WAKE_POLL_S': '0.02', 'INTERVAL': '0.2',
+           'KEYS_PER_POD': '3', 'SCALE_POLICY': scale_policy}
+    s = Settings(Config(environ=env, use_files=False))
+    client = StrictRedis(host=resp_server.host, port=resp_server.port,
+                         decode_responses=True)
+    client.delete('predict')
+    events = EventLog(source='test')
+    events.keep = True
+    manager = gpumgr.build_manager(s, redis_client=client, events=events)
+    assert manager.wake_policy == scale_policy
+    manager.pool_wake_lead_s = 0.3
+    manager.start()
+
+    def until(predicate, timeout=30):
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            if predicate():
+                return
+            time.sleep(0.01)
+        raise AssertionError('timed out')
+    try:
+        until(lambda: manager.pool_parked and not manager.standbys)
+        manager.note_next_tick(time.monotonic() + 0.6)
+        client.lpush('predict', 'predict:a')
+        if scale_policy == 'strict':
+            until(lambda: manager.arrival_wakes == 1)
+            assert manager.wake_deferrals == 0
+            return
+        until(lambda: manager.wake_deferrals == 1)
+        time.sleep(0.3)
+        assert manager.arrival_wakes == 0 and manager.pool_parked
+        assert not manager.standbys
+        deferred = [e for e in events.records if e['ev'] == 'wake_deferred']
+        assert deferred[0]['waiting'] == 1
+        assert deferred[0]['policy'] == 'reference'
+        # two more keys: the tick now scales (3 // 3 = 1), the pool wakes
+        manager.note_next_tick(time.monotonic() + 0.6)
+        client.lpush('predict', 'predict:b', 'predict:c')
+        until(lambda: manager.arrival_wakes == 1)
+        until(lambda: manager.standbys)
+        assert manager.wake_deferrals == 1
+    finally:
+        manager.stop()
+        client.delete('predict')
+
+
 def test_wake_lead_sizes_for_the_second_slowest_recent_boot():
     """One slow HIP context (0.5 s) must not hold the next 15 wakes' GPUs
     for it: the lead follows the second slowest of the last 16 woken boots
