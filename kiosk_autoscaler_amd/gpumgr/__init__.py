@@ -134,8 +134,11 @@ def template_for(settings, backend=None, keys_per_pod=None):
 
 
 def build_manager(settings, redis_client=None, events=None, slots=None,
-                  extra_env=None):
-    """Build (not start) the manager + register the configured resource."""
+                  extra_env=None, wake_policy='settings'):
+    """Build (not start) the manager + register the configured resource.
+    ``wake_policy``: the scale policy an arrival wake is checked against
+    ('settings' = this process's ``SCALE_POLICY``; None = wake on any
+    arrival, for a daemon whose autoscalers' policies it does not know)."""
     from ..utils import hbm
     if slots is None:
         cpu_slots = max(1, settings.MAX_PODS)
@@ -178,7 +181,9 @@ def build_manager(settings, redis_client=None, events=None, slots=None,
                          pool_wake_lead_s=settings.POOL_WAKE_LEAD_S,
                          pin_mode=settings.WORKER_PIN,
                          hw_queues=settings.WORKER_HW_QUEUES,
-                         scale_policy=getattr(settings, 'policy', None))
+                         scale_policy=(getattr(settings, 'policy', None)
+                                       if wake_policy == 'settings'
+                                       else wake_policy))
     if settings.RESOURCE_NAME and settings.RESOURCE_TYPE in ('deployment',
                                                            'job'):
         manager.register(settings.RESOURCE_TYPE, settings.RESOURCE_NAMESPACE,

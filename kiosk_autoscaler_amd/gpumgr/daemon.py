@@ -249,8 +249,13 @@ def main(argv=None):
         events = EventLog(redis_client=redis, source='gpumgr')
     else:
         events = EventLog(path=settings.EVENT_LOG or None, source='gpumgr')
-    manager = build_manager(settings, redis_client=redis,
-                            events=events).start()
+    # the autoscalers on this daemon may run other policies than its own
+    # environment's: an arrival wake is deferred only under an explicit
+    # SCALE_POLICY here
+    manager = build_manager(
+        settings, redis_client=redis, events=events,
+        wake_policy=(settings.policy if os.environ.get('SCALE_POLICY')
+                     else None)).start()
     if settings.METRICS_PORT:
         from ..utils import metrics
         metrics.attach(events, settings.METRICS_PORT, manager=manager,

@@ -702,6 +702,9 @@ def test_arrival_wake_waits_for_keys_the_tick_scales_for(resp_server,
     client.delete('predict')
     events = EventLog(source='test')
     events.keep = True
+    # a daemon that does not know its autoscalers' policies wakes on any
+    # arrival (gpumgr/daemon.py)
+    assert gpumgr.build_manager(s, wake_policy=None).wake_policy is None
     manager = gpumgr.build_manager(s, redis_client=client, events=events)
     assert manager.wake_policy == scale_policy
     manager.pool_wake_lead_s = 0.3
