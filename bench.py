@@ -354,8 +354,9 @@ class Budget(object):
         self.cycle_max = max(self.cycle_max, seconds)
 
 
-def run_cycle(svc, gen, args, delay_s, on_s, tag, budget):
-    """One cold-start cycle whose first key lands ``delay_s`` before a tick.
+def run_cycle(svc, gen, args, delay_s, on_s, tag, budget, min_keys=1):
+    """One cold-start cycle whose first key lands ``delay_s`` before a tick
+    (``min_keys`` at once: a warmup's burst).
 
     Never raises on a slow drain: with a policy that strands keys (job +
     floor division) the cycle is recorded as stranded, its keys are cleared
@@ -369,7 +370,7 @@ def run_cycle(svc, gen, args, delay_s, on_s, tag, budget):
     while target < now + int(0.05e9):
         nxt += period
         target = nxt - int(delay_s * 1e9)
-    keys = gen.on_window(target, on_s)
+    keys = gen.on_window(target, on_s, min_keys=min_keys)
     t_first = keys[0][2]
     items = [k[0] for k in keys]
 
@@ -598,8 +599,11 @@ def main():
                 if w and not budget.fits(cycle * (1 + min(args.steps, 10))):
                     log('budget: skipping warmup %d..' % w)
                     break
+                # KEYS_PER_POD keys at once: fewer would be stranded by the
+                # reference's floor division (job mode, --kpp 4) and the
+                # warmup would exercise nothing but the drain timeout
                 run_cycle(svc, gen, args, 0.5 * args.interval, 0.0,
-                          'warmup %d' % w, budget)
+                          'warmup %d' % w, budget, min_keys=args.kpp)
                 warmups_done[0] += 1
         sampler = (start_util_sampler(args.gpus, svc.bdfs) if rank == 0
                    else None)

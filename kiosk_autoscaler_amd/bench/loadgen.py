@@ -43,11 +43,13 @@ class LoadGenerator(object):
         pipe.execute()
         return item, queue, now
 
-    def on_window(self, t_first_ns, on_s):
-        """Enqueue the first key at ``t_first_ns`` exactly, then Poisson
-        arrivals until the window closes.  Returns ``[(item, queue, t)]``."""
+    def on_window(self, t_first_ns, on_s, min_keys=1):
+        """Enqueue the first key at ``t_first_ns`` exactly (with
+        ``min_keys - 1`` more at once), then Poisson arrivals until the
+        window closes.  Returns ``[(item, queue, t)]``."""
         sleep_until_ns(t_first_ns)
-        keys = [self.enqueue(t_ns=time.monotonic_ns())]
+        keys = [self.enqueue(t_ns=time.monotonic_ns())
+                for _ in range(max(1, int(min_keys)))]
         end = t_first_ns + int(on_s * 1e9)
         t_next = t_first_ns + int(self.rng.expovariate(self.rate) * 1e9)
         while t_next < end:

@@ -243,6 +243,10 @@ def test_loadgen_writes_hash_before_key(redis_client):
     item = redis_client.rpop('predict')
     job = redis_client.hgetall(item)
     assert job['status'] == 'new' and job['service_ms'] == '5'
+    # a warmup burst: KEYS_PER_POD keys at the first instant, nothing after
+    redis_client.delete('predict')
+    keys = gen.on_window(time.monotonic_ns(), 0.0, min_keys=4)
+    assert len(keys) == 4 and redis_client.llen('predict') == 4
 
 
 @pytest.mark.slow
