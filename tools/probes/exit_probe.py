@@ -156,15 +156,50 @@ def _smaps(pid, top=10):
     return {'anon_mb': total, 'mappings': len(rows), 'top': rows[:top]}
 
 
-def _wait_sampling(pid):
+KFD_PROC = '/sys/class/kfd/kfd/proc/%d'
+
+
+def _kfd_dirs():
+    try:
+        return set(os.listdir(os.path.dirname(KFD_PROC)))
+    except OSError:
+        return set()
+
+
+def _wait_sampling(pid, t0=None, info=None):
     """``waitpid`` by polling, sampling every 0.5 ms where the exiting
     process's threads sleep in the kernel (``/proc/<pid>/task/*/wchan`` and
-    the thread state, readable by the owner): ``{state:wchan: samples}``."""
+    the thread state, readable by the owner): ``{state:wchan: samples}``.
+    With ``info``: ``kfd_gone_ms``, ``t0`` -> the instant the process's KFD
+    record (``/sys/class/kfd/kfd/proc/<pid>``, removed once the driver has
+    torn down its queues and GPU memory) disappeared."""
     import collections
     where = collections.Counter()
+    # the record is named by the host's PID, not this namespace's: the
+    # caller passes the directory that appeared while the child started
+    kfd = (info or {}).pop('_kfd_dir', None) or KFD_PROC % pid
+    watch = info is not None and os.path.exists(kfd)
+    if info is not None:
+        info['kfd_record'] = watch
     while True:
+        if watch and not os.path.exists(kfd):
+            info['kfd_gone_ms'] = (time.monotonic_ns() - t0) / 1e6
+            watch = False
         done, status = os.waitpid(pid, os.WNOHANG)
         if done:
+            if info is not None:
+                info['reaped_ms'] = (time.monotonic_ns() - t0) / 1e6
+            if watch and not os.path.exists(kfd):
+                info['kfd_gone_ms'] = (time.monotonic_ns() - t0) / 1e6
+            elif watch:
+                # still there when reaped: the driver's release work runs
+                # after the process (poll up to 0.5 s more)
+                info['kfd_after_reap'] = True
+                end = time.monotonic() + 0.5
+                while os.path.exists(kfd) and time.monotonic() < end:
+                    time.sleep(0.0005)
+                info['kfd_gone_ms'] = ((time.monotonic_ns() - t0) / 1e6
+                                       if not os.path.exists(kfd) else None)
             return status, dict(where.most_common(12))
         try:
             tids = os.listdir('/proc/%d/task' % pid)
@@ -199,6 +234,7 @@ def main():
         for rep in range(3):
             up_r, up_w = os.pipe()
             go_r, go_w = os.pipe()
+            kfd_before = _kfd_dirs()
             pid = os.fork()
             if pid == 0:
                 os.close(up_r)
@@ -218,6 +254,11 @@ def main():
                     break
                 line += chunk
             info = json.loads(line.decode() or '{}')
+            fresh = sorted(_kfd_dirs() - kfd_before)
+            info['kfd_new_records'] = len(fresh)
+            if len(fresh) == 1:
+                info['_kfd_dir'] = os.path.join(os.path.dirname(KFD_PROC),
+                                                fresh[0])
             time.sleep(0.2)
             threads = _threads(pid)
             info['mem'] = _memory(pid)
@@ -225,7 +266,7 @@ def main():
                 info['smaps'] = _smaps(pid)
             t0 = time.monotonic_ns()
             os.write(go_w, b'g')
-            status, where = _wait_sampling(pid)
+            status, where = _wait_sampling(pid, t0, info)
             if 'teardown' in info:
                 tail = os.read(up_r, 64).decode().strip()
                 info['teardown_ms'] = float(tail) if tail else None
