@@ -66,6 +66,7 @@ class PoolMixin(object):
         # keys waiting in the managed queues at the last reading: a
         # deep-idle pool keeps a standby per KEYS_PER_POD of them
         self._waiting = 0
+        self._waiting_by_queue = {}
         self._next_waiting_check = 0.0
         self.arrival_wakes = 0
         # LLEN commands this manager issued for the pool (arrival watch and
@@ -374,7 +375,7 @@ class PoolMixin(object):
         cap = self.pool_size if room is None else min(self.pool_size, room)
 
         def need():
-            n = max(0, -(-self._waiting_keys(now) // kpp) - idle)
+            n = max(0, self._workers_for_waiting(now, kpp) - idle)
             if now < self._wake_until:
                 n = max(n, 1)
             return min(cap, n)
@@ -457,7 +458,23 @@ class PoolMixin(object):
             lengths = self._queue_lengths()
             if lengths is not None:
                 self._waiting = sum(lengths.values())
+                self._waiting_by_queue = lengths
         return self._waiting
+
+    def _workers_for_waiting(self, now, kpp):
+        """Workers the keys waiting now justify: ceil(keys / KEYS_PER_POD)
+        in all, or, under the reference policy (``wake_policy``), its
+        per-queue floor division summed over the managed resources -- the
+        keys a reference tick strands below KEYS_PER_POD get no standby."""
+        waiting = self._waiting_keys(now)
+        by_queue = getattr(self, '_waiting_by_queue', None)
+        if self.wake_policy != 'reference' or not by_queue or \
+                not self.resources:
+            return -(-waiting // kpp)
+        return sum(by_queue.get(q, 0) //
+                   max(1, int(r.template.keys_per_pod or 1))
+                   for r in self.resources.values()
+                   for q in r.template.queues)
 
     def _queue_lengths(self):
         """``{queue: LLEN}`` over every managed queue, or None."""
@@ -721,6 +738,7 @@ class PoolMixin(object):
             return False
         queues = sorted(lengths)
         self._waiting = sum(lengths.values())
+        self._waiting_by_queue = lengths
         self._next_waiting_check = now + self.pool_wake_poll_s
         before, self._queued = self._queued, lengths
         grown = [q for q in queues if lengths[q] > before.get(q, 0)]
@@ -743,6 +761,7 @@ class PoolMixin(object):
         if lengths is None:
             return True
         self._waiting = sum(lengths.values())
+        self._waiting_by_queue = lengths
         for resource in self.resources.values():
             keys = {q: lengths.get(q, 0) for q in resource.template.queues}
             kpp = max(1, int(resource.template.keys_per_pod or 1))

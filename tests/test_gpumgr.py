@@ -743,6 +743,25 @@ def test_arrival_wake_waits_for_keys_the_tick_scales_for(resp_server,
         client.delete('predict')
 
 
+def test_standbys_for_waiting_keys_follow_the_policy():
+    """A woken deep-idle pool keeps one standby per worker the waiting keys
+    justify: under ``reference`` the per-queue floor division (keys it
+    strands below KEYS_PER_POD get none), otherwise ceil over all keys."""
+    from kiosk_autoscaler_amd.config import Config, Settings
+    env = {'QUEUES': 'predict,track', 'RESOURCE_NAME': 'kpp',
+           'MAX_PODS': '4', 'WORKER_BACKEND': 'cpu', 'WARM_POOL': '1',
+           'FENCE': 'none', 'KEYS_PER_POD': '4', 'REDIS_HOST': '127.0.0.1'}
+    for scale_policy, want in (('reference', 1), ('strict', 3), (None, 3)):
+        s = Settings(Config(environ=dict(env, SCALE_POLICY=scale_policy or
+                                         'reference'), use_files=False))
+        manager = gpumgr.build_manager(s, wake_policy=scale_policy or None)
+        manager._waiting_by_queue = {'predict': 6, 'track': 3}
+        manager._waiting = 9
+        manager._next_waiting_check = float('inf')    # the cached reading
+        # predict: 6 // 4 = 1, track: 3 // 4 = 0; ceil(9 / 4) = 3
+        assert manager._workers_for_waiting(0.0, 4) == want, scale_policy
+
+
 def test_wake_lead_sizes_for_the_second_slowest_recent_boot():
     """One slow HIP context (0.5 s) must not hold the next 15 wakes' GPUs
     for it: the lead follows the second slowest of the last 16 woken boots
