@@ -471,10 +471,14 @@ class PoolMixin(object):
         if self.wake_policy != 'reference' or not by_queue or \
                 not self.resources:
             return -(-waiting // kpp)
-        return sum(by_queue.get(q, 0) //
-                   max(1, int(r.template.keys_per_pod or 1))
-                   for r in self.resources.values()
-                   for q in r.template.queues)
+        # each queue once (resources of several autoscalers may share one),
+        # at the smallest KEYS_PER_POD that reads it
+        queue_kpp = {}
+        for r in self.resources.values():
+            for q in r.template.queues:
+                k = max(1, int(r.template.keys_per_pod or 1))
+                queue_kpp[q] = min(k, queue_kpp.get(q, k))
+        return sum(by_queue.get(q, 0) // k for q, k in queue_kpp.items())
 
     def _queue_lengths(self):
         """``{queue: LLEN}`` over every managed queue, or None."""
