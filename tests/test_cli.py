@@ -195,7 +195,9 @@ def test_journal_costs_little_per_record(tmp_path):
     try:
         base = min(per_record(plain) for _ in range(3))
         cost = min(per_record(held) for _ in range(3))
-        assert cost - base < 20e-6
+        # under a line tracer (tools/covtrace.py) every traced line costs
+        # microseconds: the bound is for untraced runs
+        assert cost - base < (20e-6 if sys.gettrace() is None else 2e-3)
     finally:
         plain.close()
         held.close()
